@@ -1,0 +1,142 @@
+/*
+ * rr.h — C-ABI of librr, the MI355X (gfx950) embed+search library.
+ *
+ * The reference (Mak-GIBA/research_image_retrieval, src/benchmark) is pure
+ * Python/PyTorch and has no FFI of its own: its "operator API" is duck-typed
+ * Python.  Every entry point below replaces one torch/numpy
+ * call site on the reference's extract-and-rank hot path; the citation in
+ * each comment names that site (paths relative to src/benchmark/).  The
+ * Python mirror of the reference API (research_image_retrieval_amd/) binds
+ * these with ctypes; INTEGRATION.md shows the binding.
+ *
+ * Conventions
+ *   - All tensors are caller-owned DEVICE pointers (e.g. torch data_ptr()).
+ *     Dense row-major, fp32 unless stated.  Images/activations are NHWC.
+ *   - `stream` is a hipStream_t passed as void* (NULL = default stream).
+ *     Every call is stream-ordered and asynchronous: no host sync inside,
+ *     except the explicit *_collect / *_sync helpers.
+ *   - Return value: 0 on success, a negative RR_E* code on error; the message
+ *     is available from rr_last_error(h).  The library never aborts.
+ *   - One handle per device; handles are independent across threads.
+ */
+#ifndef RR_H_
+#define RR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RR_OK 0
+#define RR_EINVAL (-1)    /* bad argument / unsupported shape */
+#define RR_EHIP (-2)      /* HIP runtime error */
+#define RR_EWORKSPACE (-3) /* workspace too small */
+#define RR_EOVERFLOW (-4) /* candidate buffer overflow (see rr_cosine_topk) */
+
+typedef struct rr_handle_s* rr_handle_t;
+
+/* ---- handle ------------------------------------------------------------ */
+const char* rr_version(void);
+int rr_create(int device, rr_handle_t* out);
+int rr_destroy(rr_handle_t h);
+const char* rr_last_error(rr_handle_t h);
+
+/* Per-kernel-class HIP-event timing (used by bench.py for the roofline).
+ * When enabled, every launch of a timed class is bracketed by hipEvents on
+ * the launch stream; rr_timing_collect synchronises those events and returns
+ * the accumulated milliseconds and launch count for `cls`, then resets it.
+ * Classes: 0 = cosine GEMM (filter + dense), 1 = conv/linear GEMM,
+ *          2 = top-k select/merge, 3 = elementwise (preprocess/pool/norm). */
+int rr_timing_enable(rr_handle_t h, int enable);
+int rr_timing_collect(rr_handle_t h, int cls, double* ms, long long* launches);
+
+/* ---- search (ranker) ----------------------------------------------------
+ * Replaces iris_evaluate.py:383 `torch.mm(q, g.t())` + :386
+ * `np.argsort(-similarity, axis=1)` (the only ranking driver), truncated to
+ * the top k, with a STABLE order: score descending, then gallery index
+ * ascending.  Scores are exact fp32 MFMA dot products (v_mfma_f32_32x32x2_f32,
+ * a fixed k-ordered fmaf chain restated bit-for-bit by oracle/cosine_topk.c).
+ *
+ *   queries [nq][d], gallery [n][d]  (rows are expected L2-normalised by the
+ *   caller, as iris_evaluate.py:379-380 does; the kernel does not renormalise)
+ *   out_scores [nq][k] fp32, out_idx [nq][k] int64 = row + idx_offset.
+ *   If n < k the tail is filled with (-inf, -1).
+ *   1 <= k <= 16384, d % 4 == 0, 16-byte aligned rows.
+ * Workspace: rr_cosine_topk_workspace_size(nq, n, d, k) bytes of device
+ * memory, any alignment >= 256.  The candidate buffer is sized for the worst
+ * case, so RR_EOVERFLOW cannot occur with that size.                        */
+size_t rr_cosine_topk_workspace_size(int nq, long long n, int d, int k);
+int rr_cosine_topk(rr_handle_t h, const float* queries, int nq,
+                   const float* gallery, long long n, int d, int k,
+                   long long idx_offset, float* out_scores, long long* out_idx,
+                   void* workspace, size_t workspace_bytes, void* stream);
+
+/* Dense cosine scores, gallery-major: scores[j][i] = <gallery_j, query_i>,
+ * i.e. the transpose of iris_evaluate.py:383's similarity matrix. [n][nq]. */
+int rr_cosine_scores(rr_handle_t h, const float* queries, int nq,
+                     const float* gallery, long long n, int d, float* scores,
+                     void* stream);
+
+/* Merge nparts partial top-k lists (the per-shard results gathered over RCCL)
+ * into one top-k_out list per query, same stable order.  Layout
+ * part_scores/part_idx [nparts][nq][k_in]; entries with idx < 0 are padding.
+ * Indices must be < 2^32.  No reference counterpart (the reference never
+ * shards); it is the k-way merge of SURVEY.md §8(e).        */
+int rr_topk_merge(rr_handle_t h, const float* part_scores,
+                  const long long* part_idx, int nparts, int nq, int k_in,
+                  int k_out, float* out_scores, long long* out_idx,
+                  void* stream);
+
+/* ---- embed (extractor) ---------------------------------------------------
+ * uint8 HWC pixels -> fp32 NHWC, (x/255 - mean[c]) / std[c].
+ * Replaces transforms.ToTensor + Normalize(mean=[.485,.456,.406],
+ * std=[.229,.224,.225]) (dataset/configdataset.py:417, :430-436).          */
+int rr_preprocess_u8(rr_handle_t h, const uint8_t* img_nhwc, int b, int hgt,
+                     int wid, const float* mean3, const float* std3,
+                     float* out_nhwc, void* stream);
+
+/* fp32 NCHW -> NHWC relayout (the reference's forward_test input is NCHW). */
+int rr_nchw_to_nhwc(rr_handle_t h, const float* in, int b, int c, int hgt,
+                    int wid, float* out, void* stream);
+
+/* 2-D convolution, NHWC, implicit GEMM on fp32 MFMA with a fused epilogue:
+ * y = relu?( conv(x, w) + bias[co] + residual? ).  Weights [cout][kh][kw][cin]
+ * with eval-mode BatchNorm already folded into w/bias by the host.
+ * Replaces the torchvision ResNet conv/BN/ReLU/residual ops behind
+ * networks/backbone.py:103-109 and models/gem_pooling.py:44,61.
+ * residual may be NULL; output is [b][oh][ow][cout].
+ * Constraints: cin % 4 == 0 or cin < 32 (generic gather path).             */
+int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin,
+              const float* w, const float* bias, int cout, int kh, int kw,
+              int stride, int pad, const float* residual, int relu, float* y,
+              void* stream);
+
+/* Max pool (torchvision ResNet stem maxpool 3x3/2 pad 1), NHWC. */
+int rr_maxpool2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int c,
+                 int k, int stride, int pad, float* y, void* stream);
+
+/* GeM pooling over the spatial axis of an NHWC map [b][hw][c] -> [b][c]:
+ * (mean_hw clamp(x, eps)^p)^(1/p).  Replaces networks/RetrievalNet.py:324-325
+ * (gem, python-float p) and models/gem_pooling.py:20-23 (GeMPooling).      */
+int rr_gem_pool(rr_handle_t h, const float* x, int b, int hw, int c, float p,
+                float eps, float* out, void* stream);
+
+/* y[m][n] = x[m][:] . w[n][:] + bias[n]   (bias may be NULL).
+ * Replaces GeM.whiten 1x1 conv (networks/RetrievalNet.py:332,342),
+ * GeMModel.feature_proj Linear (models/gem_pooling.py:50,68) and the
+ * PCA-whitening ConvDimReduction apply (networks/spca.py:205-227).        */
+int rr_linear(rr_handle_t h, const float* x, int m, int k, const float* w,
+              const float* bias, int n, float* y, void* stream);
+
+/* Row-wise L2 normalisation x / max(||x||_2, eps), in place allowed.
+ * Replaces F.normalize (networks/RetrievalNet.py:343, models/gem_pooling.py:91,
+ * utils/helpfunc.py:44, iris_evaluate.py:379-380).                        */
+int rr_l2_normalize(rr_handle_t h, const float* x, int m, int d, float eps,
+                    float* y, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RR_H_ */

@@ -1,0 +1,104 @@
+"""ctypes binding of librr.so (include/rr.h).
+
+The library is built in-tree (``make -C research_image_retrieval_amd/csrc``,
+or ``__graft_entry__.build()``).  There is no fallback: if librr.so is missing
+or cannot be loaded every op raises, so a GPU run can never silently take a
+CPU or eager-PyTorch path.
+"""
+import ctypes
+import os
+import subprocess
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "librr.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+RR_OK, RR_EINVAL, RR_EHIP, RR_EWORKSPACE, RR_EOVERFLOW = 0, -1, -2, -3, -4
+
+# timing classes (rr_timing_enable / rr_timing_collect)
+TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM = 0, 1, 2, 3
+
+_lib = None
+_lock = threading.RLock()
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_ll = ctypes.c_longlong
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes): exactly the symbols include/rr.h declares
+SIGNATURES = {
+    "rr_version": (ctypes.c_char_p, []),
+    "rr_create": (_i, [_i, ctypes.POINTER(_vp)]),
+    "rr_destroy": (_i, [_vp]),
+    "rr_last_error": (ctypes.c_char_p, [_vp]),
+    "rr_timing_enable": (_i, [_vp, _i]),
+    "rr_timing_collect": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_ll)]),
+    "rr_cosine_topk_workspace_size": (_sz, [_i, _ll, _i, _i]),
+    "rr_cosine_topk": (_i, [_vp, _vp, _i, _vp, _ll, _i, _i, _ll, _vp, _vp, _vp, _sz, _vp]),
+    "rr_cosine_scores": (_i, [_vp, _vp, _i, _vp, _ll, _i, _vp, _vp]),
+    "rr_topk_merge": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
+    "rr_preprocess_u8": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "rr_nchw_to_nhwc": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "rr_conv2d": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
+    "rr_maxpool2d": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "rr_gem_pool": (_i, [_vp, _vp, _i, _i, _i, _f, _f, _vp, _vp]),
+    "rr_linear": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _vp]),
+    "rr_l2_normalize": (_i, [_vp, _vp, _i, _i, _f, _vp, _vp]),
+}
+
+
+class RRError(RuntimeError):
+    pass
+
+
+def build(force=False):
+    """Compile librr.so for gfx950 with hipcc (in-tree)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", CSRC, "-j4"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RRError(
+                    f"librr.so not found at {LIB_PATH}: build it with `make -C {CSRC}` "
+                    "(there is deliberately no CPU/eager fallback)")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+_handles = {}
+
+
+def handle(device_index):
+    """Per-device librr handle (created once)."""
+    h = _handles.get(device_index)
+    if h is None:
+        with _lock:
+            h = _handles.get(device_index)
+            if h is None:
+                out = _vp()
+                rc = lib().rr_create(int(device_index), ctypes.byref(out))
+                if rc != RR_OK:
+                    raise RRError(f"rr_create(device={device_index}) failed with {rc}")
+                h = out.value
+                _handles[device_index] = h
+    return h
+
+
+def check(rc, h, what):
+    if rc != RR_OK:
+        msg = lib().rr_last_error(h)
+        raise RRError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")

@@ -1,0 +1,174 @@
+// embed_ops.hip — HBM-bound embed-path kernels (gfx950): input normalisation,
+// NCHW->NHWC relayout, stem max-pool, GeM pooling, row L2 normalisation.
+// All are single-pass streaming kernels with coalesced 4-/16-byte accesses
+// along the innermost (channel) axis; reductions use wavefront shuffles.
+#include "rr_internal.hpp"
+
+namespace rr {
+
+// (x/255 - mean[c]) / std[c]; same op order and IEEE division as
+// torchvision ToTensor().div(255) + Normalize().sub_(mean).div_(std)
+// (dataset/configdataset.py:417,430-436).
+__global__ void preprocess_u8_kernel(const uint8_t* __restrict__ in, long long n_px, float m0, float m1, float m2,
+                                     float s0, float s1, float s2, float* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < n_px; p += stride) {
+    const uint8_t* px = in + p * 3;
+    float* o = out + p * 3;
+    o[0] = ((float)px[0] / 255.0f - m0) / s0;
+    o[1] = ((float)px[1] / 255.0f - m1) / s1;
+    o[2] = ((float)px[2] / 255.0f - m2) / s2;
+  }
+}
+
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ in, int C, long long HW, long long total,
+                                    float* __restrict__ out) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
+    const int c = (int)(o % C);
+    const long long t = o / C;
+    const long long hw = t % HW;
+    const long long b = t / HW;
+    out[o] = in[(b * C + c) * HW + hw];
+  }
+}
+
+// max pool, NHWC; out-of-bounds taps are -inf (PyTorch max_pool2d padding).
+__global__ void maxpool_kernel(const float* __restrict__ x, int B, int H, int W, int C, int k, int stride, int pad,
+                               int OH, int OW, float* __restrict__ y) {
+  const long long total = (long long)B * OH * OW * C;
+  const long long gstride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gstride) {
+    const int c = (int)(o % C);
+    long long t = o / C;
+    const int ow = (int)(t % OW);
+    t /= OW;
+    const int oh = (int)(t % OH);
+    const int b = (int)(t / OH);
+    float m = -__builtin_inff();
+    for (int dh = 0; dh < k; ++dh) {
+      const int ih = oh * stride - pad + dh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int dw = 0; dw < k; ++dw) {
+        const int iw = ow * stride - pad + dw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        m = fmaxf(m, x[(((long long)b * H + ih) * W + iw) * C + c]);
+      }
+    }
+    y[o] = m;
+  }
+}
+
+// GeM over the spatial axis of [B][HW][C]: (sum_hw clamp(x,eps)^p / HW)^(1/p).
+// p == 3 uses (x*x)*x, the op torch's pow(tensor, 3.0) kernel emits
+// (networks/RetrievalNet.py:325); other p use powf.
+__global__ void gem_kernel(const float* __restrict__ x, int B, int HW, int C, float p, float eps, int p_is_3,
+                           float* __restrict__ out) {
+  const long long total = (long long)B * C;
+  const long long gstride = (long long)gridDim.x * blockDim.x;
+  const float inv_p = 1.0f / p;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gstride) {
+    const int c = (int)(o % C);
+    const long long b = o / C;
+    const float* xp = x + b * (long long)HW * C + c;
+    float acc = 0.f;
+    for (int i = 0; i < HW; ++i) {
+      const float v = fmaxf(xp[(long long)i * C], eps);
+      acc += p_is_3 ? (v * v) * v : powf(v, p);
+    }
+    out[o] = powf(acc / (float)HW, inv_p);
+  }
+}
+
+// One wave per row: x / max(||x||_2, eps)  (F.normalize semantics).
+__global__ __launch_bounds__(256) void l2norm_kernel(const float* __restrict__ x, int M, int D, float eps,
+                                                     float* __restrict__ y) {
+  const int wave = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (wave >= M) return;
+  const float* xr = x + (long long)wave * D;
+  float* yr = y + (long long)wave * D;
+  float ss = 0.f;
+  for (int i = lane; i < D; i += 64) ss = fmaf(xr[i], xr[i], ss);
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+  const float nrm = fmaxf(sqrtf(ss), eps);
+  for (int i = lane; i < D; i += 64) yr[i] = xr[i] / nrm;
+}
+
+static dim3 grid_for(long long n, int block) {
+  long long g = (n + block - 1) / block;
+  if (g > 256 * 16) g = 256 * 16;
+  if (g < 1) g = 1;
+  return dim3((unsigned)g);
+}
+
+}  // namespace rr
+
+using namespace rr;
+
+extern "C" int rr_preprocess_u8(rr_handle_t h, const uint8_t* img, int b, int hgt, int wid, const float* mean3,
+                                const float* std3, float* out, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!img || !out || !mean3 || !std3 || b < 0 || hgt < 0 || wid < 0)
+    return set_error(h, RR_EINVAL, "rr_preprocess_u8: bad argument");
+  const long long npx = (long long)b * hgt * wid;
+  if (npx == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  hipLaunchKernelGGL(preprocess_u8_kernel, grid_for(npx, 256), dim3(256), 0, s, img, npx, mean3[0], mean3[1],
+                     mean3[2], std3[0], std3[1], std3[2], out);
+  return check_hip(h, hipGetLastError(), "preprocess launch");
+}
+
+extern "C" int rr_nchw_to_nhwc(rr_handle_t h, const float* in, int b, int c, int hgt, int wid, float* out,
+                               void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!in || !out || b < 0 || c <= 0 || hgt < 0 || wid < 0) return set_error(h, RR_EINVAL, "rr_nchw_to_nhwc: bad argument");
+  const long long total = (long long)b * c * hgt * wid;
+  if (total == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid_for(total, 256), dim3(256), 0, s, in, c, (long long)hgt * wid, total,
+                     out);
+  return check_hip(h, hipGetLastError(), "nchw_to_nhwc launch");
+}
+
+extern "C" int rr_maxpool2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int c, int k, int stride, int pad,
+                            float* y, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !y || b < 0 || c <= 0 || k <= 0 || stride <= 0 || pad < 0 || 2 * pad > k)
+    return set_error(h, RR_EINVAL, "rr_maxpool2d: bad argument");
+  const int oh = (hgt + 2 * pad - k) / stride + 1, ow = (wid + 2 * pad - k) / stride + 1;
+  if (oh <= 0 || ow <= 0) return set_error(h, RR_EINVAL, "rr_maxpool2d: empty output");
+  const long long total = (long long)b * oh * ow * c;
+  if (total == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  hipLaunchKernelGGL(maxpool_kernel, grid_for(total, 256), dim3(256), 0, s, x, b, hgt, wid, c, k, stride, pad, oh, ow,
+                     y);
+  return check_hip(h, hipGetLastError(), "maxpool launch");
+}
+
+extern "C" int rr_gem_pool(rr_handle_t h, const float* x, int b, int hw, int c, float p, float eps, float* out,
+                           void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !out || b < 0 || hw <= 0 || c <= 0 || !(p > 0.f)) return set_error(h, RR_EINVAL, "rr_gem_pool: bad argument");
+  const long long total = (long long)b * c;
+  if (total == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  hipLaunchKernelGGL(gem_kernel, grid_for(total, 256), dim3(256), 0, s, x, b, hw, c, p, eps, p == 3.0f ? 1 : 0, out);
+  return check_hip(h, hipGetLastError(), "gem launch");
+}
+
+extern "C" int rr_l2_normalize(rr_handle_t h, const float* x, int m, int d, float eps, float* y, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !y || m < 0 || d <= 0) return set_error(h, RR_EINVAL, "rr_l2_normalize: bad argument");
+  if (m == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  const long long threads = (long long)m * 64;
+  hipLaunchKernelGGL(l2norm_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, x, m, d, eps, y);
+  return check_hip(h, hipGetLastError(), "l2norm launch");
+}

@@ -1,0 +1,326 @@
+// gemm_f32.hip — fp32 MFMA GEMM core for gfx950 (CDNA4).
+//
+// C[M,N] = A[M,K] . B[N,K]^T with A and B both K-contiguous ("NT" layout).
+// One core serves three reference call sites:
+//   * cosine ranker  : A = gallery rows, B = query rows  (iris_evaluate.py:383)
+//   * conv layers    : A = implicit im2col of an NHWC map, B = weights
+//                      [Cout][KH][KW][Cin]               (networks/backbone.py:103-109)
+//   * projections    : A = pooled descriptors, B = W     (networks/RetrievalNet.py:342,
+//                                                         models/gem_pooling.py:68)
+//
+// Arithmetic: v_mfma_f32_32x32x2_f32 (exact f32 in, f32 accumulate; every
+// output element is a k-ordered fmaf chain).  Within each 16-deep k chunk the
+// lane half h of MFMA e supplies k = 16c + 8h + e, so the chain visits
+// k = 16c+0, 16c+8, 16c+1, 16c+9, ..., 16c+7, 16c+15 — oracle/cosine_topk.c
+// restates exactly this order, which makes GPU scores bit-identical to the
+// oracle's.
+//
+// Tiling: a wave owns a 64x64 output block (2x2 MFMA tiles of 32x32, 64
+// accumulator registers); a workgroup is WM x WN waves.  BK = 32: each k-tile
+// of A and B is register-staged (one float4 per lane-chunk, coalesced along
+// K) into a double-buffered LDS image of 128-byte rows whose 16-byte slots are
+// XOR-swizzled by (row>>1)&7, which makes the fragment ds_read_b128 (lane
+// groups of 16 distinct rows, same slot) bank-conflict free.  One barrier per
+// k-tile; the next tile's global loads are in flight under the MFMAs.
+// Block ids are remapped so consecutive tiles of one XCD share the A panel
+// (the streamed gallery / activation rows) in that XCD's L2.
+#include "rr_internal.hpp"
+
+namespace rr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 32;
+
+__device__ __forceinline__ int swz(int row, int slot) { return slot ^ ((row >> 1) & 7); }
+
+template <int WM, int WN, int AMODE, int EMODE>
+__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int tiles_n) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int BM = 64 * WM, BN = 64 * WN;
+  constexpr int ROWS_PER_PASS = NT / 8;
+  constexpr int A_CH = BM / ROWS_PER_PASS;
+  constexpr int B_CH = BN / ROWS_PER_PASS;
+  static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for block");
+  constexpr int BUF = (BM + BN) * BK;  // floats per LDS buffer
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+
+  // XCD-aware bijective block remap (blocks b, b+8, ... share an XCD).
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tn = wgid % tiles_n, tm = wgid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+
+  const int slot = tid & 7;
+  const int crow = tid >> 3;
+  const int K = g.K;
+  const int nk = (K + BK - 1) / BK;
+
+  // ---- per-chunk A row state ----
+  const float* a_ptr[A_CH];
+  int a_ih0[A_CH], a_iw0[A_CH];
+  bool a_ok[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int m = m0 + crow + i * ROWS_PER_PASS;
+    a_ok[i] = m < g.M;
+    if constexpr (AMODE == A_DENSE) {
+      a_ptr[i] = g.A + (long long)(a_ok[i] ? m : 0) * g.lda;
+      a_ih0[i] = 0;
+      a_iw0[i] = 0;
+    } else {
+      const int mm = a_ok[i] ? m : 0;
+      const int ohw = g.OH * g.OW;
+      const int b = mm / ohw;
+      const int rem = mm - b * ohw;
+      const int oh = rem / g.OW;
+      const int ow = rem - oh * g.OW;
+      a_ptr[i] = g.A + (long long)b * g.H * g.W * g.Cin;
+      a_ih0[i] = oh * g.stride - g.pad;
+      a_iw0[i] = ow * g.stride - g.pad;
+    }
+  }
+  const float* b_ptr[B_CH];
+  bool b_ok[B_CH];
+#pragma unroll
+  for (int i = 0; i < B_CH; ++i) {
+    const int n = n0 + crow + i * ROWS_PER_PASS;
+    b_ok[i] = n < g.N;
+    b_ptr[i] = g.B + (long long)(b_ok[i] ? n : 0) * g.ldb;
+  }
+
+  f32x4 ra[A_CH], rb[B_CH];
+
+  auto load_tile = [&](int kt) {
+    const int k = kt * BK + slot * 4;
+    const bool kok = k < K;
+    if constexpr (AMODE == A_DENSE) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        ra[i] = (a_ok[i] && kok) ? *reinterpret_cast<const f32x4*>(a_ptr[i] + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    } else if constexpr (AMODE == A_CONV) {
+      // Cin % 32 == 0: the whole 32-deep k-tile lies in one (kh, kw) tap.
+      const int k0 = kt * BK;
+      const int khw = k0 / g.Cin;
+      const int cin0 = k0 - khw * g.Cin;
+      const int kh = khw / g.KW;
+      const int kw = khw - kh * g.KW;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+        const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        ra[i] = ok ? *reinterpret_cast<const f32x4*>(a_ptr[i] + ((long long)ih * g.W + iw) * g.Cin + cin0 + slot * 4)
+                   : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+      // generic gather (small / odd Cin, e.g. the 7x7 stem with Cin = 3)
+      const int kwc = g.KW * g.Cin;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int kk = k + e;
+          if (a_ok[i] && kk < K) {
+            const int kh = kk / kwc;
+            const int r2 = kk - kh * kwc;
+            const int kw = r2 / g.Cin;
+            const int c = r2 - kw * g.Cin;
+            const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+            if ((unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W)
+              v[e] = a_ptr[i][((long long)ih * g.W + iw) * g.Cin + c];
+          }
+        }
+        ra[i] = v;
+      }
+    }
+    if constexpr (AMODE == A_CONV_GENERIC) {
+      // K need not be a multiple of 4 here (stem: 7*7*3 = 147): scalar loads
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        f32x4 v = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          if (b_ok[i] && k + e < K) v[e] = b_ptr[i][k + e];
+        rb[i] = v;
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < B_CH; ++i) {
+        rb[i] = (b_ok[i] && kok) ? *reinterpret_cast<const f32x4*>(b_ptr[i] + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+
+  auto store_tile = [&](int buf) {
+    float* la = lds + buf * BUF;
+    float* lb = la + BM * BK;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int row = crow + i * ROWS_PER_PASS;
+      *reinterpret_cast<f32x4*>(la + row * BK + swz(row, slot) * 4) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int row = crow + i * ROWS_PER_PASS;
+      *reinterpret_cast<f32x4*>(lb + row * BK + swz(row, slot) * 4) = rb[i];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int lr = lane & 31, lh = lane >> 5;
+
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile(kt + 1);
+    const float* la = lds + cur * BUF;
+    const float* lb = la + BM * BK;
+#pragma unroll
+    for (int c2 = 0; c2 < 2; ++c2) {
+      f32x4 af[2][2], bf[2][2];
+      const int s0 = c2 * 4 + 2 * lh;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 64 + i * 32 + lr;
+        af[i][0] = *reinterpret_cast<const f32x4*>(la + row * BK + swz(row, s0) * 4);
+        af[i][1] = *reinterpret_cast<const f32x4*>(la + row * BK + swz(row, s0 + 1) * 4);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wn * 64 + j * 32 + lr;
+        bf[j][0] = *reinterpret_cast<const f32x4*>(lb + row * BK + swz(row, s0) * 4);
+        bf[j][1] = *reinterpret_cast<const f32x4*>(lb + row * BK + swz(row, s0 + 1) * 4);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e >> 2][e & 3], bf[j][e >> 2][e & 3],
+                                                             acc[i][j], 0, 0, 0);
+      }
+    }
+    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  // 32x32 C/D map: col (N index) = lane & 31, row (M index) = (r&3) + 8(r>>2) + 4(lane>>5)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = n0 + wn * 64 + j * 32 + lr;
+    const bool nok = n < g.N;
+    if constexpr (EMODE == E_STORE) {
+      const float bv = (g.bias != nullptr && nok) ? g.bias[n] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          if (nok && m < g.M) {
+            float v = acc[i][j][r] + bv;
+            const long long o = (long long)m * g.ldc + n;
+            if (g.residual != nullptr) v += g.residual[o];
+            if (g.relu) v = fmaxf(v, 0.f);
+            g.C[o] = v;
+          }
+        }
+      }
+    } else if constexpr (EMODE == E_SCORES_T) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int mb = m0 + wm * 64 + i * 32 + 8 * q + 4 * lh;
+          if (!nok) continue;
+          float* dst = g.C + (long long)n * g.ldc + mb;
+          if (mb + 3 < g.M) {
+            *reinterpret_cast<f32x4*>(dst) =
+                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (mb + e < g.M) dst[e] = acc[i][j][4 * q + e];
+          }
+        }
+      }
+    } else {  // E_FILTER: keep only scores strictly above the query's threshold
+      const float t = nok ? g.tau[n] : __builtin_inff();
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const float v = acc[i][j][r];
+          if (v > t && m < g.M) {
+            const int pos = atomicAdd(g.cnt + n, 1);
+            if (pos < g.cap) g.cand[(long long)n * g.cap + pos] = make_key(v, (uint32_t)(g.row_offset + m));
+          }
+        }
+      }
+    }
+  }
+}
+
+template <int WM, int WN, int AM, int EM>
+static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
+  constexpr int BM = 64 * WM, BN = 64 * WN;
+  const long long tiles_m = (g.M + BM - 1) / BM;
+  const long long tiles_n = (g.N + BN - 1) / BN;
+  const long long nblk = tiles_m * tiles_n;
+  if (nblk <= 0) return hipSuccess;
+  if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, AM, EM>), dim3((unsigned)nblk), dim3(64 * WM * WN), 0, s, g,
+                     (int)tiles_n);
+  return hipGetLastError();
+}
+
+template <int AM, int EM>
+static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
+  // Narrow B (N <= 64: e.g. 64-channel convs, few queries) -> 256x64 tiles.
+  if (g.N <= 64) return launch_t<4, 1, AM, EM>(g, s);
+  return launch_t<2, 2, AM, EM>(g, s);
+}
+
+int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStream_t s, int timer_cls) {
+  if (g.M < 0 || g.N < 0 || g.K <= 0) return set_error(h, RR_EINVAL, "gemm: bad shape");
+  if (amode != A_CONV_GENERIC && (g.K & 3) != 0) return set_error(h, RR_EINVAL, "gemm: K must be a multiple of 4");
+  if (amode == A_DENSE && (g.lda & 3)) return set_error(h, RR_EINVAL, "gemm: lda must be a multiple of 4");
+  if (amode != A_CONV_GENERIC && (g.ldb & 3) != 0) return set_error(h, RR_EINVAL, "gemm: ldb must be a multiple of 4");
+  if (emode == E_SCORES_T && (g.ldc & 3)) return set_error(h, RR_EINVAL, "gemm: ldc must be a multiple of 4");
+  if (amode == A_CONV && (g.Cin % BK) != 0) return set_error(h, RR_EINVAL, "gemm: A_CONV needs Cin % 32 == 0");
+  if (g.M == 0 || g.N == 0) return RR_OK;
+  hipError_t e = hipSuccess;
+  {
+    TimedLaunch tl(h, timer_cls, s);
+    if (amode == A_DENSE && emode == E_STORE) e = launch_cfg<A_DENSE, E_STORE>(g, s);
+    else if (amode == A_DENSE && emode == E_SCORES_T) e = launch_cfg<A_DENSE, E_SCORES_T>(g, s);
+    else if (amode == A_DENSE && emode == E_FILTER) e = launch_cfg<A_DENSE, E_FILTER>(g, s);
+    else if (amode == A_CONV && emode == E_STORE) e = launch_cfg<A_CONV, E_STORE>(g, s);
+    else if (amode == A_CONV_GENERIC && emode == E_STORE) e = launch_cfg<A_CONV_GENERIC, E_STORE>(g, s);
+    else return set_error(h, RR_EINVAL, "gemm: unsupported mode combination");
+  }
+  return check_hip(h, e, "gemm launch");
+}
+
+}  // namespace rr

@@ -1,0 +1,303 @@
+// rr_api.hip — C-ABI entry points of librr (see include/rr.h).
+#include <algorithm>
+#include <cstring>
+
+#include "rr_internal.hpp"
+
+namespace rr {
+
+int set_error(rr_handle_s* h, int code, const std::string& msg) {
+  if (h) h->last_error = msg;
+  return code;
+}
+
+int check_hip(rr_handle_s* h, hipError_t e, const char* what) {
+  if (e == hipSuccess) return RR_OK;
+  return set_error(h, RR_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+TimedLaunch::TimedLaunch(rr_handle_s* h_, int cls_, hipStream_t s_) : h(h_), cls(cls_), s(s_) {
+  if (!h || !h->timing || cls < 0 || cls >= rr_handle_s::kClasses) return;
+  const int i = h->n_ev[cls];
+  if (i >= rr_handle_s::kMaxEv) return;
+  if (!h->ev_start[cls][i]) {
+    if (hipEventCreate(&h->ev_start[cls][i]) != hipSuccess) return;
+    if (hipEventCreate(&h->ev_stop[cls][i]) != hipSuccess) return;
+  }
+  if (hipEventRecord(h->ev_start[cls][i], s) != hipSuccess) return;
+  slot = i;
+}
+
+TimedLaunch::~TimedLaunch() {
+  if (slot < 0) return;
+  if (hipEventRecord(h->ev_stop[cls][slot], s) == hipSuccess) h->n_ev[cls] = slot + 1;
+}
+
+// Sample size of the threshold-seeding pass of rr_cosine_topk.
+static long long seed_rows(long long n, int k) {
+  const long long smax = std::max<long long>(32768, k);
+  return n <= smax ? n : smax;
+}
+
+static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+struct TopkWs {
+  long long s, ld, cap;
+  size_t off_scores, off_tau, off_cnt, off_ovf, off_cand, total;
+};
+
+static TopkWs topk_layout(int nq, long long n, int k) {
+  TopkWs w{};
+  w.s = seed_rows(n, k);
+  w.ld = (w.s + 3) & ~3LL;
+  w.cap = k + (n - w.s);  // worst case: every non-seed row passes its threshold
+  size_t o = 0;
+  w.off_scores = o;
+  o = align256(o + (size_t)nq * w.ld * 4);
+  w.off_tau = o;
+  o = align256(o + (size_t)nq * 4);
+  w.off_cnt = o;
+  o = align256(o + (size_t)nq * 4);
+  w.off_ovf = o;
+  o = align256(o + 4);
+  w.off_cand = o;
+  o = align256(o + (size_t)nq * w.cap * 8);
+  w.total = o;
+  return w;
+}
+
+}  // namespace rr
+
+using namespace rr;
+
+extern "C" {
+
+const char* rr_version(void) { return "librr 0.1.0 (gfx950, fp32 MFMA)"; }
+
+int rr_create(int device, rr_handle_t* out) {
+  if (!out) return RR_EINVAL;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return RR_EHIP;
+  rr_handle_s* h = new (std::nothrow) rr_handle_s();
+  if (!h) return RR_EINVAL;
+  h->device = device;
+  *out = h;
+  return RR_OK;
+}
+
+int rr_destroy(rr_handle_t h) {
+  if (!h) return RR_EINVAL;
+  for (int c = 0; c < rr_handle_s::kClasses; ++c)
+    for (int i = 0; i < rr_handle_s::kMaxEv; ++i) {
+      if (h->ev_start[c][i]) (void)hipEventDestroy(h->ev_start[c][i]);
+      if (h->ev_stop[c][i]) (void)hipEventDestroy(h->ev_stop[c][i]);
+    }
+  delete h;
+  return RR_OK;
+}
+
+const char* rr_last_error(rr_handle_t h) { return h ? h->last_error.c_str() : "null handle"; }
+
+int rr_timing_enable(rr_handle_t h, int enable) {
+  if (!h) return RR_EINVAL;
+  h->timing = enable != 0;
+  for (int c = 0; c < rr_handle_s::kClasses; ++c) {
+    h->n_ev[c] = 0;
+    h->acc_ms[c] = 0;
+    h->acc_launches[c] = 0;
+  }
+  return RR_OK;
+}
+
+int rr_timing_collect(rr_handle_t h, int cls, double* ms, long long* launches) {
+  if (!h || cls < 0 || cls >= rr_handle_s::kClasses) return RR_EINVAL;
+  for (int i = 0; i < h->n_ev[cls]; ++i) {
+    if (int rc = check_hip(h, hipEventSynchronize(h->ev_stop[cls][i]), "timing sync")) return rc;
+    float t = 0.f;
+    if (int rc = check_hip(h, hipEventElapsedTime(&t, h->ev_start[cls][i], h->ev_stop[cls][i]), "timing elapsed"))
+      return rc;
+    h->acc_ms[cls] += t;
+    h->acc_launches[cls] += 1;
+  }
+  h->n_ev[cls] = 0;
+  if (ms) *ms = h->acc_ms[cls];
+  if (launches) *launches = h->acc_launches[cls];
+  h->acc_ms[cls] = 0;
+  h->acc_launches[cls] = 0;
+  return RR_OK;
+}
+
+size_t rr_cosine_topk_workspace_size(int nq, long long n, int d, int k) {
+  (void)d;
+  if (nq <= 0 || k <= 0) return 256;
+  return topk_layout(nq, n > 0 ? n : 1, k).total;
+}
+
+int rr_cosine_topk(rr_handle_t h, const float* queries, int nq, const float* gallery, long long n, int d, int k,
+                   long long idx_offset, float* out_scores, long long* out_idx, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (nq < 0 || n < 0 || d <= 0 || (d & 3) || k < 1 || k > 16384)
+    return set_error(h, RR_EINVAL, "rr_cosine_topk: need nq,n >= 0, d % 4 == 0, 1 <= k <= 16384");
+  if (n >= 0xffffffffLL) return set_error(h, RR_EINVAL, "rr_cosine_topk: gallery shard must have < 2^32 rows");
+  if (nq == 0) return RR_OK;
+  if (!queries || !out_scores || !out_idx || (n > 0 && !gallery))
+    return set_error(h, RR_EINVAL, "rr_cosine_topk: null pointer");
+  if (((uintptr_t)queries & 15) || ((uintptr_t)gallery & 15))
+    return set_error(h, RR_EINVAL, "rr_cosine_topk: queries/gallery must be 16-byte aligned");
+  hipStream_t s = (hipStream_t)stream;
+  const TopkWs L = topk_layout(nq, n > 0 ? n : 1, k);
+  if (n == 0) {
+    // nothing to rank: all padding
+    if (!workspace || workspace_bytes < L.total) return set_error(h, RR_EWORKSPACE, "rr_cosine_topk: workspace too small");
+    char* ws = (char*)workspace;
+    int* cnt = (int*)(ws + L.off_cnt);
+    if (int rc = check_hip(h, hipMemsetAsync(cnt, 0, (size_t)nq * 4, s), "memset")) return rc;
+    return launch_select_final(h, (unsigned long long*)(ws + L.off_cand), L.cap, cnt, nq, k, idx_offset, out_scores,
+                               out_idx, (int*)(ws + L.off_ovf), s);
+  }
+  if (!workspace || workspace_bytes < L.total)
+    return set_error(h, RR_EWORKSPACE, "rr_cosine_topk: workspace too small (query rr_cosine_topk_workspace_size)");
+  char* ws = (char*)workspace;
+  float* scores_t = (float*)(ws + L.off_scores);
+  float* tau = (float*)(ws + L.off_tau);
+  int* cnt = (int*)(ws + L.off_cnt);
+  int* ovf = (int*)(ws + L.off_ovf);
+  unsigned long long* cand = (unsigned long long*)(ws + L.off_cand);
+
+  if (int rc = check_hip(h, hipMemsetAsync(ovf, 0, 4, s), "memset")) return rc;
+
+  // 1. exact scores of the first s gallery rows (query-major)
+  GemmArgs g;
+  g.A = gallery;
+  g.lda = d;
+  g.M = (int)L.s;
+  g.K = d;
+  g.B = queries;
+  g.ldb = d;
+  g.N = nq;
+  g.C = scores_t;
+  g.ldc = L.ld;
+  if (int rc = launch_gemm(h, A_DENSE, E_SCORES_T, g, s, kTimeCosine)) return rc;
+  // 2. seed candidates with their exact top-k; tau = k-th best score
+  if (int rc = launch_select_dense_seed(h, scores_t, L.ld, (int)L.s, nq, k, 0, cand, L.cap, cnt, tau, s)) return rc;
+  // 3. remaining rows: fused GEMM + threshold filter (scores never hit HBM)
+  if (n > L.s) {
+    long long done = L.s;
+    while (done < n) {
+      const long long rows = std::min<long long>(n - done, 0x7fffff00LL);
+      GemmArgs f;
+      f.A = gallery + done * d;
+      f.lda = d;
+      f.M = (int)rows;
+      f.K = d;
+      f.B = queries;
+      f.ldb = d;
+      f.N = nq;
+      f.tau = tau;
+      f.cand = cand;
+      f.cnt = cnt;
+      f.cap = L.cap;
+      f.row_offset = done;
+      if (int rc = launch_gemm(h, A_DENSE, E_FILTER, f, s, kTimeCosine)) return rc;
+      done += rows;
+    }
+  }
+  // 4. exact top-k of the survivors, stable order
+  return launch_select_final(h, cand, L.cap, cnt, nq, k, idx_offset, out_scores, out_idx, ovf, s);
+}
+
+int rr_cosine_scores(rr_handle_t h, const float* queries, int nq, const float* gallery, long long n, int d,
+                     float* scores, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (nq < 0 || n < 0 || n > 0x7fffffffLL || d <= 0 || (d & 3))
+    return set_error(h, RR_EINVAL, "rr_cosine_scores: bad shape");
+  if (nq == 0 || n == 0) return RR_OK;
+  if (!queries || !gallery || !scores) return set_error(h, RR_EINVAL, "rr_cosine_scores: null pointer");
+  GemmArgs g;
+  g.A = gallery;
+  g.lda = d;
+  g.M = (int)n;
+  g.K = d;
+  g.B = queries;
+  g.ldb = d;
+  g.N = nq;
+  g.C = scores;
+  g.ldc = nq;
+  return launch_gemm(h, A_DENSE, E_STORE, g, (hipStream_t)stream, kTimeCosine);
+}
+
+int rr_topk_merge(rr_handle_t h, const float* ps, const long long* pi, int nparts, int nq, int k_in, int k_out,
+                  float* os, long long* oi, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!ps || !pi || !os || !oi) return set_error(h, RR_EINVAL, "rr_topk_merge: null pointer");
+  return launch_merge(h, ps, pi, nparts, nq, k_in, k_out, os, oi, (hipStream_t)stream);
+}
+
+int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, const float* w, const float* bias,
+              int cout, int kh, int kw, int stride, int pad, const float* residual, int relu, float* y,
+              void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !w || !y || b < 0 || hgt <= 0 || wid <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 ||
+      stride <= 0 || pad < 0)
+    return set_error(h, RR_EINVAL, "rr_conv2d: bad argument");
+  const int oh = (hgt + 2 * pad - kh) / stride + 1, ow = (wid + 2 * pad - kw) / stride + 1;
+  if (oh <= 0 || ow <= 0) return set_error(h, RR_EINVAL, "rr_conv2d: empty output");
+  const long long M = (long long)b * oh * ow;
+  if (M > 0x7fffffffLL) return set_error(h, RR_EINVAL, "rr_conv2d: too many output pixels");
+  GemmArgs g;
+  g.A = x;
+  g.M = (int)M;
+  g.K = kh * kw * cin;
+  g.H = hgt;
+  g.W = wid;
+  g.Cin = cin;
+  g.OH = oh;
+  g.OW = ow;
+  g.KH = kh;
+  g.KW = kw;
+  g.stride = stride;
+  g.pad = pad;
+  g.B = w;
+  g.ldb = g.K;
+  g.N = cout;
+  g.C = y;
+  g.ldc = cout;
+  g.bias = bias;
+  g.residual = residual;
+  g.relu = relu;
+  int amode;
+  if (kh == 1 && kw == 1 && stride == 1 && pad == 0 && (cin & 3) == 0) {
+    amode = A_DENSE;
+    g.lda = cin;
+  } else if (cin % 32 == 0) {
+    amode = A_CONV;
+  } else {
+    amode = A_CONV_GENERIC;
+  }
+  if (amode != A_CONV_GENERIC && (((uintptr_t)x & 15) || ((uintptr_t)w & 15)))
+    return set_error(h, RR_EINVAL, "rr_conv2d: x/w must be 16-byte aligned");
+  return launch_gemm(h, amode, E_STORE, g, (hipStream_t)stream, kTimeGemm);
+}
+
+int rr_linear(rr_handle_t h, const float* x, int m, int k, const float* w, const float* bias, int n, float* y,
+              void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !w || !y || m < 0 || k <= 0 || n <= 0 || (k & 3)) return set_error(h, RR_EINVAL, "rr_linear: bad argument");
+  if (((uintptr_t)x & 15) || ((uintptr_t)w & 15)) return set_error(h, RR_EINVAL, "rr_linear: x/w must be 16-byte aligned");
+  GemmArgs g;
+  g.A = x;
+  g.lda = k;
+  g.M = m;
+  g.K = k;
+  g.B = w;
+  g.ldb = k;
+  g.N = n;
+  g.C = y;
+  g.ldc = n;
+  g.bias = bias;
+  return launch_gemm(h, A_DENSE, E_STORE, g, (hipStream_t)stream, kTimeGemm);
+}
+
+}  // extern "C"

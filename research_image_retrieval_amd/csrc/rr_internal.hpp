@@ -1,0 +1,108 @@
+// rr_internal.hpp — shared declarations for librr (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+
+#include "../../include/rr.h"
+
+struct rr_handle_s {
+  int device = 0;
+  std::string last_error;
+  // timing (see rr_timing_enable)
+  bool timing = false;
+  static constexpr int kClasses = 4;
+  static constexpr int kMaxEv = 4096;
+  hipEvent_t ev_start[kClasses][kMaxEv] = {};
+  hipEvent_t ev_stop[kClasses][kMaxEv] = {};
+  int n_ev[kClasses] = {};
+  double acc_ms[kClasses] = {};
+  long long acc_launches[kClasses] = {};
+};
+
+namespace rr {
+
+enum TimerClass { kTimeCosine = 0, kTimeGemm = 1, kTimeSelect = 2, kTimeElem = 3 };
+
+// RAII-style bracket: records start/stop events on `stream` when timing is on.
+struct TimedLaunch {
+  rr_handle_s* h;
+  int cls;
+  hipStream_t s;
+  int slot = -1;
+  TimedLaunch(rr_handle_s* h_, int cls_, hipStream_t s_);
+  ~TimedLaunch();
+};
+
+int set_error(rr_handle_s* h, int code, const std::string& msg);
+int check_hip(rr_handle_s* h, hipError_t e, const char* what);
+
+// ---- ordered 64-bit keys: score descending, then index ascending --------
+// key = (ord(score) << 32) | ~idx ; larger key = better rank.
+__host__ __device__ inline uint32_t ord_f32(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  if (u == 0x80000000u) u = 0u;  // -0.0 ranks as +0.0 (equal scores tie-break on index)
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__host__ __device__ inline float unord_f32(uint32_t o) {
+  uint32_t u = (o & 0x80000000u) ? (o & 0x7fffffffu) : ~o;
+  float f;
+  __builtin_memcpy(&f, &u, 4);
+  return f;
+}
+__host__ __device__ inline unsigned long long make_key(float s, uint32_t idx) {
+  return ((unsigned long long)ord_f32(s) << 32) | (unsigned long long)(~idx);
+}
+__host__ __device__ inline uint32_t key_idx(unsigned long long k) {
+  return ~(uint32_t)(k & 0xffffffffull);
+}
+__host__ __device__ inline float key_score(unsigned long long k) {
+  return unord_f32((uint32_t)(k >> 32));
+}
+
+// ---- GEMM core launchers (gemm_f32.hip) ---------------------------------
+enum AMode { A_DENSE = 0, A_CONV = 1, A_CONV_GENERIC = 2 };
+enum EMode { E_STORE = 0, E_SCORES_T = 1, E_FILTER = 2 };
+
+struct GemmArgs {
+  // A operand (M rows x K): dense [M][lda] or implicit im2col of NHWC input
+  const float* A = nullptr;
+  long long lda = 0;
+  int M = 0, K = 0;
+  int H = 0, W = 0, Cin = 0, OH = 0, OW = 0, KH = 1, KW = 1, stride = 1, pad = 0;
+  // B operand (N rows x K), dense [N][ldb], K contiguous
+  const float* B = nullptr;
+  long long ldb = 0;
+  int N = 0;
+  // epilogue
+  float* C = nullptr;
+  long long ldc = 0;
+  const float* bias = nullptr;
+  const float* residual = nullptr;
+  int relu = 0;
+  // filter epilogue (cosine top-k candidates): per B-row (query) threshold
+  const float* tau = nullptr;
+  unsigned long long* cand = nullptr;
+  int* cnt = nullptr;
+  long long cap = 0;
+  long long row_offset = 0;  // added to the A row index in candidate keys
+};
+
+int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls);
+
+// ---- top-k kernels (topk.hip) -------------------------------------------
+// Dense scores, query-major [nq][ld] (first `rows` valid) -> per query the
+// top-min(k,rows) keys written to cand[q][0..), cnt[q], tau[q].
+int launch_select_dense_seed(rr_handle_s* h, const float* scores_t, long long ld, int rows, int nq,
+                             int k, long long row_offset, unsigned long long* cand, long long cap,
+                             int* cnt, float* tau, hipStream_t s);
+// candidates cand[q][0..cnt[q]) -> sorted top-k (scores, idx + idx_offset)
+int launch_select_final(rr_handle_s* h, const unsigned long long* cand, long long cap,
+                        const int* cnt, int nq, int k, long long idx_offset, float* out_scores,
+                        long long* out_idx, int* overflow_flag, hipStream_t s);
+int launch_merge(rr_handle_s* h, const float* ps, const long long* pi, int nparts, int nq, int kin,
+                 int kout, float* os, long long* oi, hipStream_t s);
+
+}  // namespace rr

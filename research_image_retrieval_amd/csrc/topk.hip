@@ -1,0 +1,235 @@
+// topk.hip — per-query top-k selection for the cosine ranker (gfx950).
+//
+// Replaces the full `np.argsort(-similarity, axis=1)` of iris_evaluate.py:386
+// with an exact top-k under a STABLE order (score desc, gallery index asc).
+// Every candidate is a 64-bit key  (ord(score) << 32) | ~index  whose unsigned
+// order is exactly that ranking order, so selection is an integer problem:
+//   1. MSB-first radix select (8 passes x 8 bits, 256-bin LDS histogram,
+//      parallel suffix scan) finds the k-th largest key; a pass stops early as
+//      soon as the bucket holding the k-th key is entirely selected;
+//   2. the <= k winning keys are gathered into LDS and bitonic-sorted
+//      descending (power-of-two padded with key 0 = "no entry").
+// One 256-thread workgroup per query.
+#include "rr_internal.hpp"
+
+namespace rr {
+
+constexpr int SEL_NT = 256;
+constexpr int SEL_MAX_K = 16384;
+
+struct SelShared {
+  unsigned int scan[SEL_NT];
+  int digit, above, dcnt, gcount, all;
+};
+
+// Src: callable int64 index -> key (0 = empty / padding, never selected)
+template <class Src>
+__device__ int block_select_sort(Src src, long long count, int k, int P, unsigned long long* skeys,
+                                 SelShared& sh) {
+  const int tid = threadIdx.x;
+  unsigned long long prefix = 0, mask = 0;
+  int remaining = k;
+  int fshift = 0;
+  bool all = false;
+  for (int pass = 0; pass < 8; ++pass) {
+    const int shift = 56 - 8 * pass;
+    sh.scan[tid] = 0;
+    __syncthreads();
+    for (long long i = tid; i < count; i += SEL_NT) {
+      const unsigned long long key = src(i);
+      if (key != 0ull && (key & mask) == prefix) atomicAdd(&sh.scan[(key >> shift) & 255u], 1u);
+    }
+    __syncthreads();
+    // inclusive suffix sum over digits: scan[t] = sum_{e >= t} hist[e]
+    const unsigned int mine = sh.scan[tid];
+    for (int off = 1; off < SEL_NT; off <<= 1) {
+      const unsigned int add = (tid + off < SEL_NT) ? sh.scan[tid + off] : 0u;
+      __syncthreads();
+      sh.scan[tid] += add;
+      __syncthreads();
+    }
+    if (pass == 0 && tid == 0) sh.all = (sh.scan[0] <= (unsigned)k) ? 1 : 0;
+    {
+      const unsigned int incl = sh.scan[tid];
+      const unsigned int excl = incl - mine;
+      if (mine > 0 && incl >= (unsigned)remaining && excl < (unsigned)remaining) {
+        sh.digit = tid;
+        sh.above = (int)excl;
+        sh.dcnt = (int)mine;
+      }
+    }
+    __syncthreads();
+    if (sh.all) {
+      all = true;
+      break;
+    }
+    remaining -= sh.above;
+    prefix |= (unsigned long long)sh.digit << shift;
+    mask |= 0xffull << shift;
+    const bool done = (sh.dcnt == remaining);
+    fshift = shift;
+    __syncthreads();
+    if (done) break;
+  }
+
+  // gather winners
+  if (tid == 0) sh.gcount = 0;
+  __syncthreads();
+  const unsigned long long ptop = prefix >> fshift;
+  for (long long i = tid; i < count; i += SEL_NT) {
+    const unsigned long long key = src(i);
+    if (key != 0ull && (all || (key >> fshift) >= ptop)) {
+      const int pos = atomicAdd(&sh.gcount, 1);
+      if (pos < P) skeys[pos] = key;
+    }
+  }
+  __syncthreads();
+  const int nsel = sh.gcount < P ? sh.gcount : P;
+  for (int i = nsel + tid; i < P; i += SEL_NT) skeys[i] = 0ull;
+  __syncthreads();
+
+  // bitonic sort, descending
+  for (int size = 2; size <= P; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = tid; i < (P >> 1); i += SEL_NT) {
+        const int pos = 2 * i - (i & (stride - 1));
+        const int par = pos + stride;
+        const bool desc = (pos & size) == 0;
+        const unsigned long long a = skeys[pos], b = skeys[par];
+        if ((a < b) == desc && a != b) {
+          skeys[pos] = b;
+          skeys[par] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  return nsel < k ? nsel : k;
+}
+
+__device__ inline void write_out(const unsigned long long* skeys, int nsel, int k, long long offset,
+                                 float* os, long long* oi) {
+  for (int r = threadIdx.x; r < k; r += SEL_NT) {
+    const unsigned long long key = r < nsel ? skeys[r] : 0ull;
+    if (key != 0ull) {
+      os[r] = key_score(key);
+      oi[r] = (long long)key_idx(key) + offset;
+    } else {
+      os[r] = -__builtin_inff();
+      oi[r] = -1;
+    }
+  }
+}
+
+// Dense query-major scores -> seed the candidate buffer with the exact top-k
+// of the first `rows` gallery rows, and the threshold tau = k-th best score.
+__global__ __launch_bounds__(SEL_NT) void select_dense_seed_kernel(const float* __restrict__ st, long long ld,
+                                                                   int rows, int k, int P, long long row_offset,
+                                                                   unsigned long long* cand, long long cap,
+                                                                   int* cnt, float* tau) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long skeys[];
+  __shared__ SelShared sh;
+  const int q = blockIdx.x;
+  const float* col = st + (long long)q * ld;
+  auto src = [&](long long i) -> unsigned long long { return make_key(col[i], (uint32_t)(row_offset + i)); };
+  const int nsel = block_select_sort(src, rows, k, P, skeys, sh);
+  unsigned long long* cq = cand + (long long)q * cap;
+  for (int r = threadIdx.x; r < nsel; r += SEL_NT) cq[r] = skeys[r];
+  if (threadIdx.x == 0) {
+    cnt[q] = nsel;
+    tau[q] = (nsel >= k) ? key_score(skeys[k - 1]) : -__builtin_inff();
+  }
+}
+
+__global__ __launch_bounds__(SEL_NT) void select_final_kernel(const unsigned long long* __restrict__ cand,
+                                                              long long cap, const int* __restrict__ cnt, int k,
+                                                              int P, long long offset, float* os, long long* oi,
+                                                              int* overflow) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long skeys[];
+  __shared__ SelShared sh;
+  const int q = blockIdx.x;
+  const long long c = cnt[q];
+  if (c > cap && threadIdx.x == 0) atomicAdd(overflow, 1);
+  const long long count = c < cap ? c : cap;
+  const unsigned long long* cq = cand + (long long)q * cap;
+  auto src = [&](long long i) -> unsigned long long { return cq[i]; };
+  const int nsel = block_select_sort(src, count, k, P, skeys, sh);
+  write_out(skeys, nsel, k, offset, os + (long long)q * k, oi + (long long)q * k);
+}
+
+__global__ __launch_bounds__(SEL_NT) void merge_kernel(const float* __restrict__ ps, const long long* __restrict__ pi,
+                                                       int nparts, int nq, int kin, int kout, int P, float* os,
+                                                       long long* oi) {
+  extern __shared__ __attribute__((aligned(16))) unsigned long long skeys[];
+  __shared__ SelShared sh;
+  const int q = blockIdx.x;
+  auto src = [&](long long i) -> unsigned long long {
+    const long long p = i / kin, r = i - p * kin;
+    const long long o = (p * nq + q) * (long long)kin + r;
+    const long long idx = pi[o];
+    return idx < 0 ? 0ull : make_key(ps[o], (uint32_t)idx);
+  };
+  const int nsel = block_select_sort(src, (long long)nparts * kin, kout, P, skeys, sh);
+  write_out(skeys, nsel, kout, 0, os + (long long)q * kout, oi + (long long)q * kout);
+}
+
+static int pow2_at_least(int k) {
+  int p = 1;
+  while (p < k) p <<= 1;
+  return p;
+}
+
+static int check_k(rr_handle_s* h, int k) {
+  if (k < 1 || k > SEL_MAX_K) return set_error(h, RR_EINVAL, "top-k: k must be in [1, 16384]");
+  return RR_OK;
+}
+
+static hipError_t set_lds(const void* fn, size_t bytes) {
+  if (bytes <= 64 * 1024) return hipSuccess;
+  return hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+
+int launch_select_dense_seed(rr_handle_s* h, const float* st, long long ld, int rows, int nq, int k,
+                             long long row_offset, unsigned long long* cand, long long cap, int* cnt, float* tau,
+                             hipStream_t s) {
+  if (int rc = check_k(h, k)) return rc;
+  if (nq <= 0) return RR_OK;
+  const int P = pow2_at_least(k);
+  const size_t lds = (size_t)P * 8;
+  hipError_t e = set_lds((const void*)select_dense_seed_kernel, lds);
+  if (e != hipSuccess) return check_hip(h, e, "select_dense_seed attr");
+  TimedLaunch tl(h, kTimeSelect, s);
+  hipLaunchKernelGGL(select_dense_seed_kernel, dim3(nq), dim3(SEL_NT), lds, s, st, ld, rows, k, P, row_offset,
+                     cand, cap, cnt, tau);
+  return check_hip(h, hipGetLastError(), "select_dense_seed launch");
+}
+
+int launch_select_final(rr_handle_s* h, const unsigned long long* cand, long long cap, const int* cnt, int nq, int k,
+                        long long offset, float* os, long long* oi, int* overflow, hipStream_t s) {
+  if (int rc = check_k(h, k)) return rc;
+  if (nq <= 0) return RR_OK;
+  const int P = pow2_at_least(k);
+  const size_t lds = (size_t)P * 8;
+  hipError_t e = set_lds((const void*)select_final_kernel, lds);
+  if (e != hipSuccess) return check_hip(h, e, "select_final attr");
+  TimedLaunch tl(h, kTimeSelect, s);
+  hipLaunchKernelGGL(select_final_kernel, dim3(nq), dim3(SEL_NT), lds, s, cand, cap, cnt, k, P, offset, os, oi,
+                     overflow);
+  return check_hip(h, hipGetLastError(), "select_final launch");
+}
+
+int launch_merge(rr_handle_s* h, const float* ps, const long long* pi, int nparts, int nq, int kin, int kout,
+                 float* os, long long* oi, hipStream_t s) {
+  if (int rc = check_k(h, kout)) return rc;
+  if (nparts <= 0 || kin <= 0) return set_error(h, RR_EINVAL, "merge: nparts and k_in must be positive");
+  if (nq <= 0) return RR_OK;
+  const int P = pow2_at_least(kout);
+  const size_t lds = (size_t)P * 8;
+  hipError_t e = set_lds((const void*)merge_kernel, lds);
+  if (e != hipSuccess) return check_hip(h, e, "merge attr");
+  TimedLaunch tl(h, kTimeSelect, s);
+  hipLaunchKernelGGL(merge_kernel, dim3(nq), dim3(SEL_NT), lds, s, ps, pi, nparts, nq, kin, kout, P, os, oi);
+  return check_hip(h, hipGetLastError(), "merge launch");
+}
+
+}  // namespace rr

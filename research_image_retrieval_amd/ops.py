@@ -1,0 +1,208 @@
+"""Torch-tensor wrappers over the librr C-ABI (one function per rr_* entry).
+
+PyTorch is used only for device memory and the current HIP stream; every op
+below runs a hand-written gfx950 kernel from librr.so.  Inputs must be
+contiguous fp32 (uint8 for images) tensors on a ROCm device.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+
+_NULL = None
+
+
+def _dev(t):
+    if not t.is_cuda:
+        raise ValueError("librr ops need ROCm device tensors (got a CPU tensor)")
+    return t.device.index if t.device.index is not None else torch.cuda.current_device()
+
+
+def _ptr(t):
+    return None if t is None else ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _f32(t, name):
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name}: expected float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    return t
+
+
+def preprocess_u8(img_nhwc, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)):
+    """uint8 [B,H,W,3] -> fp32 NHWC normalised (ToTensor + Normalize)."""
+    if img_nhwc.dtype != torch.uint8 or img_nhwc.dim() != 4 or img_nhwc.shape[3] != 3:
+        raise ValueError("preprocess_u8: expected uint8 [B,H,W,3]")
+    img_nhwc = img_nhwc.contiguous()
+    dev = _dev(img_nhwc)
+    b, h, w, _ = img_nhwc.shape
+    out = torch.empty((b, h, w, 3), dtype=torch.float32, device=img_nhwc.device)
+    m = (ctypes.c_float * 3)(*mean)
+    s = (ctypes.c_float * 3)(*std)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_preprocess_u8(hd, _ptr(img_nhwc), b, h, w, ctypes.cast(m, ctypes.c_void_p),
+                                           ctypes.cast(s, ctypes.c_void_p), _ptr(out), _stream(dev)), hd,
+               "rr_preprocess_u8")
+    return out
+
+
+def nchw_to_nhwc(x):
+    x = _f32(x.contiguous(), "nchw_to_nhwc")
+    dev = _dev(x)
+    b, c, h, w = x.shape
+    out = torch.empty((b, h, w, c), dtype=torch.float32, device=x.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_nchw_to_nhwc(hd, _ptr(x), b, c, h, w, _ptr(out), _stream(dev)), hd, "rr_nchw_to_nhwc")
+    return out
+
+
+def conv2d(x, w, bias, stride=1, pad=0, residual=None, relu=False):
+    """NHWC conv with fused bias/residual/ReLU; w is [Cout,KH,KW,Cin]."""
+    _f32(x, "conv2d x")
+    _f32(w, "conv2d w")
+    dev = _dev(x)
+    b, h, wd, cin = x.shape
+    cout, kh, kw, cin_w = w.shape
+    if cin_w != cin:
+        raise ValueError(f"conv2d: Cin mismatch {cin} vs {cin_w}")
+    oh = (h + 2 * pad - kh) // stride + 1
+    ow = (wd + 2 * pad - kw) // stride + 1
+    y = torch.empty((b, oh, ow, cout), dtype=torch.float32, device=x.device)
+    if residual is not None:
+        _f32(residual, "conv2d residual")
+        if tuple(residual.shape) != tuple(y.shape):
+            raise ValueError("conv2d: residual shape mismatch")
+    if bias is not None:
+        _f32(bias, "conv2d bias")
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_conv2d(hd, _ptr(x), b, h, wd, cin, _ptr(w), _ptr(bias), cout, kh, kw, stride, pad,
+                                    _ptr(residual), int(relu), _ptr(y), _stream(dev)), hd, "rr_conv2d")
+    return y
+
+
+def maxpool2d(x, k=3, stride=2, pad=1):
+    _f32(x, "maxpool2d")
+    dev = _dev(x)
+    b, h, w, c = x.shape
+    oh = (h + 2 * pad - k) // stride + 1
+    ow = (w + 2 * pad - k) // stride + 1
+    y = torch.empty((b, oh, ow, c), dtype=torch.float32, device=x.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_maxpool2d(hd, _ptr(x), b, h, w, c, k, stride, pad, _ptr(y), _stream(dev)), hd,
+               "rr_maxpool2d")
+    return y
+
+
+def gem_pool(x_nhwc, p=3.0, eps=1e-6):
+    """[B,H,W,C] (or [B,HW,C]) -> [B,C] GeM."""
+    _f32(x_nhwc, "gem_pool")
+    dev = _dev(x_nhwc)
+    b, c = x_nhwc.shape[0], x_nhwc.shape[-1]
+    hw = x_nhwc.numel() // (b * c) if b * c else 0
+    out = torch.empty((b, c), dtype=torch.float32, device=x_nhwc.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_gem_pool(hd, _ptr(x_nhwc), b, hw, c, float(p), float(eps), _ptr(out), _stream(dev)), hd,
+               "rr_gem_pool")
+    return out
+
+
+def linear(x, w, bias=None):
+    """y = x @ w.T + bias, x [M,K], w [N,K]."""
+    _f32(x, "linear x")
+    _f32(w, "linear w")
+    dev = _dev(x)
+    m, k = x.shape
+    n = w.shape[0]
+    y = torch.empty((m, n), dtype=torch.float32, device=x.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_linear(hd, _ptr(x), m, k, _ptr(w), _ptr(bias), n, _ptr(y), _stream(dev)), hd,
+               "rr_linear")
+    return y
+
+
+def l2_normalize(x, eps=1e-12, out=None):
+    _f32(x, "l2_normalize")
+    dev = _dev(x)
+    m, d = x.shape
+    y = torch.empty_like(x) if out is None else out
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_l2_normalize(hd, _ptr(x), m, d, float(eps), _ptr(y), _stream(dev)), hd,
+               "rr_l2_normalize")
+    return y
+
+
+def cosine_topk_workspace_size(nq, n, d, k):
+    return int(_lib.lib().rr_cosine_topk_workspace_size(int(nq), int(n), int(d), int(k)))
+
+
+def cosine_topk(queries, gallery, k, idx_offset=0, workspace=None):
+    """Exact stable top-k of queries [nq,D] against gallery [N,D] -> (scores [nq,k] fp32, idx [nq,k] int64)."""
+    _f32(queries, "cosine_topk queries")
+    _f32(gallery, "cosine_topk gallery")
+    dev = _dev(queries)
+    nq, d = queries.shape
+    n = gallery.shape[0]
+    if gallery.shape[1] != d:
+        raise ValueError("cosine_topk: descriptor dims differ")
+    need = cosine_topk_workspace_size(nq, n, d, k)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=queries.device)
+    os_ = torch.empty((nq, k), dtype=torch.float32, device=queries.device)
+    oi = torch.empty((nq, k), dtype=torch.int64, device=queries.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_cosine_topk(hd, _ptr(queries), nq, _ptr(gallery), n, d, k, int(idx_offset), _ptr(os_),
+                                         _ptr(oi), _ptr(workspace), workspace.numel(), _stream(dev)), hd,
+               "rr_cosine_topk")
+    return os_, oi
+
+
+def cosine_scores(queries, gallery):
+    """Dense scores, gallery-major [N, nq] (= similarity.T of iris_evaluate.py:383)."""
+    _f32(queries, "cosine_scores queries")
+    _f32(gallery, "cosine_scores gallery")
+    dev = _dev(queries)
+    nq, d = queries.shape
+    n = gallery.shape[0]
+    out = torch.empty((n, nq), dtype=torch.float32, device=queries.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_cosine_scores(hd, _ptr(queries), nq, _ptr(gallery), n, d, _ptr(out), _stream(dev)), hd,
+               "rr_cosine_scores")
+    return out
+
+
+def topk_merge(part_scores, part_idx, k_out):
+    """[P,nq,kin] partial lists -> stable top-k_out per query."""
+    _f32(part_scores, "topk_merge scores")
+    if part_idx.dtype != torch.int64 or not part_idx.is_contiguous():
+        raise TypeError("topk_merge: idx must be contiguous int64")
+    dev = _dev(part_scores)
+    p, nq, kin = part_scores.shape
+    os_ = torch.empty((nq, k_out), dtype=torch.float32, device=part_scores.device)
+    oi = torch.empty((nq, k_out), dtype=torch.int64, device=part_scores.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_topk_merge(hd, _ptr(part_scores), _ptr(part_idx), p, nq, kin, k_out, _ptr(os_), _ptr(oi),
+                                        _stream(dev)), hd, "rr_topk_merge")
+    return os_, oi
+
+
+class KernelTimer:
+    """HIP-event timing of librr kernel classes on their launch stream."""
+
+    def __init__(self, device_index):
+        self.h = _lib.handle(device_index)
+
+    def enable(self, on=True):
+        _lib.check(_lib.lib().rr_timing_enable(self.h, int(on)), self.h, "rr_timing_enable")
+
+    def collect(self, cls):
+        ms = ctypes.c_double()
+        n = ctypes.c_longlong()
+        _lib.check(_lib.lib().rr_timing_collect(self.h, cls, ctypes.byref(ms), ctypes.byref(n)), self.h,
+                   "rr_timing_collect")
+        return ms.value, n.value

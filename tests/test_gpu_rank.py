@@ -1,0 +1,70 @@
+"""GPU parity of the ranker (rr_cosine_topk / rr_cosine_scores / rr_topk_merge)
+against the C oracle (oracle/cosine_topk.c): bit-exact scores and indices.
+
+Reference: iris_evaluate.py:383 torch.mm + :386 np.argsort (stable tie-break)."""
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from research_image_retrieval_amd import ops
+
+pytestmark = pytest.mark.gpu
+
+
+def _normed(rng, n, d):
+    x = rng.randn(n, d).astype(np.float32)
+    x /= np.linalg.norm(x, axis=1, keepdims=True)
+    return x
+
+
+def test_mfma_chain_order_bitexact(cuda):
+    rng = np.random.RandomState(1)
+    q = _normed(rng, 37, 96)
+    g = _normed(rng, 1000, 96)
+    gpu = ops.cosine_scores(torch.from_numpy(q).to(cuda), torch.from_numpy(g).to(cuda)).cpu().numpy().T
+    res = {o: int((oracle.cosine_scores(q, g, order=o) != gpu).sum()) for o in (0, 1, 2)}
+    print("mismatches by oracle order:", res)
+    assert res[0] == 0, res
+
+
+@pytest.mark.parametrize("nq,n,d,k", [(16, 20000, 512, 100), (8, 50000, 2048, 100), (3, 40000, 512, 7),
+                                      (70, 4993, 512, 4993), (5, 60, 64, 100), (130, 33000, 128, 1)])
+def test_cosine_topk_matches_oracle(cuda, nq, n, d, k):
+    rng = np.random.RandomState(nq * 7 + n)
+    q = _normed(rng, nq, d)
+    g = _normed(rng, n, d)
+    # plant near-duplicates and exact ties (same row repeated)
+    for i in range(min(nq, 4)):
+        j = rng.randint(n)
+        g[j] = q[i]
+        if n > 10:
+            g[(j + 3) % n] = q[i]
+    s_gpu, i_gpu = ops.cosine_topk(torch.from_numpy(q).to(cuda), torch.from_numpy(g).to(cuda), k)
+    s_ref, i_ref = oracle.cosine_topk(q, g, k)
+    np.testing.assert_array_equal(i_gpu.cpu().numpy(), i_ref)
+    np.testing.assert_array_equal(s_gpu.cpu().numpy(), s_ref)
+
+
+def test_cosine_topk_idx_offset_and_empty(cuda):
+    rng = np.random.RandomState(3)
+    q = torch.from_numpy(_normed(rng, 4, 64)).to(cuda)
+    g = torch.from_numpy(_normed(rng, 300, 64)).to(cuda)
+    s, i = ops.cosine_topk(q, g, 10, idx_offset=1_000_000)
+    s2, i2 = ops.cosine_topk(q, g, 10)
+    assert torch.equal(i, i2 + 1_000_000) and torch.equal(s, s2)
+    s3, i3 = ops.cosine_topk(q, g[:0], 5)
+    assert (i3 == -1).all() and torch.isinf(s3).all()
+
+
+def test_topk_merge_matches_oracle(cuda):
+    rng = np.random.RandomState(5)
+    P, nq, kin, kout = 8, 33, 100, 100
+    ps = rng.randn(P, nq, kin).astype(np.float32)
+    pi = rng.permutation(P * nq * kin).reshape(P, nq, kin).astype(np.int64)
+    ps[1, :, :5] = ps[0, :, :5]  # cross-part exact ties
+    pi[2, :, -10:] = -1          # padding
+    so, io = ops.topk_merge(torch.from_numpy(ps).to(cuda), torch.from_numpy(pi).to(cuda), kout)
+    sr, ir = oracle.topk_merge(ps, pi, kout)
+    np.testing.assert_array_equal(io.cpu().numpy(), ir)
+    np.testing.assert_array_equal(so.cpu().numpy(), sr)
