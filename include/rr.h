@@ -113,6 +113,15 @@ int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin,
               int stride, int pad, const float* residual, int relu, float* y,
               void* stream);
 
+/* Bilinear resize, NHWC, align_corners=False, PyTorch source-index rule:
+ * src = max(scale * (dst + 0.5) - 0.5, 0) with scale = 1/scale_factor when a
+ * scale factor was given (inv_scale_h/w > 0) else in/out.  Replaces the
+ * F.interpolate(..., mode='bilinear', align_corners=False) calls of
+ * extract_vectors (utils/helpfunc.py:26, :38).                             */
+int rr_resize_bilinear(rr_handle_t h, const float* x, int b, int hgt, int wid,
+                       int c, int out_h, int out_w, float inv_scale_h,
+                       float inv_scale_w, float* y, void* stream);
+
 /* Max pool (torchvision ResNet stem maxpool 3x3/2 pad 1), NHWC. */
 int rr_maxpool2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int c,
                  int k, int stride, int pad, float* y, void* stream);

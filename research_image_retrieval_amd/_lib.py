@@ -43,6 +43,7 @@ SIGNATURES = {
     "rr_preprocess_u8": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "rr_nchw_to_nhwc": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "rr_conv2d": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
+    "rr_resize_bilinear": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _f, _f, _vp, _vp]),
     "rr_maxpool2d": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "rr_gem_pool": (_i, [_vp, _vp, _i, _i, _i, _f, _f, _vp, _vp]),
     "rr_linear": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _vp]),

@@ -33,6 +33,33 @@ __global__ void nchw_to_nhwc_kernel(const float* __restrict__ in, int C, long lo
   }
 }
 
+// bilinear, align_corners=False (ATen upsample_bilinear2d source-index rule)
+__global__ void resize_bilinear_kernel(const float* __restrict__ x, int B, int H, int W, int C, int OH, int OW,
+                                       float sh, float sw, float* __restrict__ y) {
+  const long long total = (long long)B * OH * OW * C;
+  const long long gstride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gstride) {
+    const int c = (int)(o % C);
+    long long t = o / C;
+    const int ow = (int)(t % OW);
+    t /= OW;
+    const int oh = (int)(t % OH);
+    const int b = (int)(t / OH);
+    float rh = sh * ((float)oh + 0.5f) - 0.5f;
+    float rw = sw * ((float)ow + 0.5f) - 0.5f;
+    rh = rh < 0.f ? 0.f : rh;
+    rw = rw < 0.f ? 0.f : rw;
+    const int h0 = (int)rh, w0 = (int)rw;
+    const int h1 = h0 + (h0 < H - 1 ? 1 : 0), w1 = w0 + (w0 < W - 1 ? 1 : 0);
+    const float lh1 = fminf(fmaxf(rh - (float)h0, 0.f), 1.f), lw1 = fminf(fmaxf(rw - (float)w0, 0.f), 1.f);
+    const float lh0 = 1.f - lh1, lw0 = 1.f - lw1;
+    const float* xb = x + (long long)b * H * W * C + c;
+    const float v00 = xb[((long long)h0 * W + w0) * C], v01 = xb[((long long)h0 * W + w1) * C];
+    const float v10 = xb[((long long)h1 * W + w0) * C], v11 = xb[((long long)h1 * W + w1) * C];
+    y[o] = (v00 * lw0 + v01 * lw1) * lh0 + (v10 * lw0 + v11 * lw1) * lh1;
+  }
+}
+
 // max pool, NHWC; out-of-bounds taps are -inf (PyTorch max_pool2d padding).
 __global__ void maxpool_kernel(const float* __restrict__ x, int B, int H, int W, int C, int k, int stride, int pad,
                                int OH, int OW, float* __restrict__ y) {
@@ -171,4 +198,20 @@ extern "C" int rr_l2_normalize(rr_handle_t h, const float* x, int m, int d, floa
   const long long threads = (long long)m * 64;
   hipLaunchKernelGGL(l2norm_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, x, m, d, eps, y);
   return check_hip(h, hipGetLastError(), "l2norm launch");
+}
+
+extern "C" int rr_resize_bilinear(rr_handle_t h, const float* x, int b, int hgt, int wid, int c, int out_h, int out_w,
+                                  float inv_scale_h, float inv_scale_w, float* y, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !y || b < 0 || hgt <= 0 || wid <= 0 || c <= 0 || out_h <= 0 || out_w <= 0)
+    return set_error(h, RR_EINVAL, "rr_resize_bilinear: bad argument");
+  const float sh = inv_scale_h > 0.f ? inv_scale_h : (float)hgt / (float)out_h;
+  const float sw = inv_scale_w > 0.f ? inv_scale_w : (float)wid / (float)out_w;
+  const long long total = (long long)b * out_h * out_w * c;
+  if (total == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  hipLaunchKernelGGL(resize_bilinear_kernel, grid_for(total, 256), dim3(256), 0, s, x, b, hgt, wid, c, out_h, out_w, sh,
+                     sw, y);
+  return check_hip(h, hipGetLastError(), "resize launch");
 }

@@ -1,0 +1,88 @@
+"""Gallery sharding across GPUs: one process per GPU,
+torch.distributed over RCCL ("nccl" backend on ROCm), xGMI underneath.
+
+Per search call, for a world of W ranks each holding B_r query descriptors and
+a contiguous gallery shard [lo_r, hi_r):
+  1. all-gather the query descriptors  -> every rank holds all Q = sum B_r;
+  2. local fused cosine top-k of all Q queries against the shard
+     (rr_cosine_topk, indices offset to global gallery rows);
+  3. all-to-all of the partial top-k lists (scores fp32, idx int64): rank r
+     receives, from every shard, the lists of its own B_r queries [W, B_r, k];
+  4. k-way merge (rr_topk_merge), stable order (score desc, global idx asc).
+The collectives move Q*D*4 and B_r*W*k*12 bytes per rank: latency-bound next
+to the GEMM.  Ranking work per rank is Q x N/W, so the units (images embedded and
+ranked against the whole gallery) scale weakly with W.
+
+The reference has no distributed evaluation (NCCL is
+training-only); this is new.  ``local_topk`` / ``merge`` are injectable so
+the choreography is unit-tested on CPU with gloo against the oracle; the
+product defaults are the librr kernels.
+"""
+import torch
+import torch.distributed as dist
+
+from . import ops
+
+
+def shard_bounds(n, world, rank):
+    """Contiguous row range of rank's shard (first n % world shards get +1)."""
+    base, extra = divmod(n, world)
+    lo = rank * base + min(rank, extra)
+    return lo, lo + base + (1 if rank < extra else 0)
+
+
+def _all_gather_var(t, group):
+    """all_gather of tensors whose first dim may differ across ranks."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n, group=group)
+    sizes = [int(s.item()) for s in sizes]
+    mx = max(sizes)
+    pad = t.new_zeros((mx,) + tuple(t.shape[1:]))
+    pad[: t.shape[0]] = t
+    outs = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(outs, pad, group=group)
+    return [o[:s] for o, s in zip(outs, sizes)], sizes
+
+
+class ShardedGallery:
+    """This rank's shard of a gallery that is row-partitioned over the group."""
+
+    def __init__(self, shard, global_offset, group=None, local_topk=None, merge=None, workspace=None):
+        self.shard = shard
+        self.offset = int(global_offset)
+        self.group = group
+        self._local_topk = local_topk
+        self._merge = merge
+        self._ws = workspace
+
+    def _local(self, q, k):
+        if self._local_topk is not None:
+            return self._local_topk(q, self.shard, k, self.offset)
+        need = ops.cosine_topk_workspace_size(q.shape[0], self.shard.shape[0], q.shape[1], k)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=q.device)
+        return ops.cosine_topk(q, self.shard, k, idx_offset=self.offset, workspace=self._ws)
+
+    def _merge_parts(self, ps, pi, k):
+        if self._merge is not None:
+            return self._merge(ps, pi, k)
+        return ops.topk_merge(ps, pi, k)
+
+    def search(self, queries, k):
+        """queries [B_r, D] (this rank's) -> (scores [B_r,k], global idx [B_r,k])."""
+        group = self.group
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        qs, sizes = _all_gather_var(queries.contiguous(), group)
+        allq = torch.cat(qs, 0).contiguous()
+        s, i = self._local(allq, k)
+        # each rank needs only its own queries' partial lists: all-to-all
+        # (B_r * W * k * 12 bytes in per rank instead of Q * W * k * 12)
+        mine = sizes[rank]
+        rs = s.new_empty((world * mine, k))
+        ri = i.new_empty((world * mine, k))
+        dist.all_to_all_single(rs, s.contiguous(), [mine] * world, sizes, group=group)
+        dist.all_to_all_single(ri, i.contiguous(), [mine] * world, sizes, group=group)
+        return self._merge_parts(rs.view(world, mine, k).contiguous(), ri.view(world, mine, k).contiguous(), k)

@@ -1,0 +1,194 @@
+"""networks-style extractors (reference: src/benchmark/networks/) on librr.
+
+Every object here exposes the reference's extractor contract
+(networks/RetrievalNet.py:327-344): ``.outputdim`` and
+``.forward_test(x: float32 [B,3,H,W]) -> float32 [B,outputdim]`` L2-normalised,
+eval-mode semantics, no autograd.  All arithmetic runs in librr's gfx950
+kernels; torch only allocates device buffers.  There is no CPU path: calling
+forward_test on a CPU tensor raises.
+"""
+import numpy as np
+import torch
+
+from . import ops
+from . import weights as W
+
+EPS_L2 = 1e-12  # F.normalize default eps (networks/RetrievalNet.py:343)
+
+
+class ResNet:
+    """torchvision resnet children[:-2] trunk (networks/backbone.py:60-109:
+    block1 = conv1/bn1/relu/maxpool, block2..5 = layer1..4), NHWC, BN folded.
+
+    forward(x_nhwc [B,H,W,3]) -> [B,H/32,W/32,2048] NHWC."""
+
+    outputdim_block5 = 2048
+    outputdim_block4 = 1024
+
+    def __init__(self, name="resnet101", state_dict=None, seed=0, device="cuda"):
+        if name not in W.RESNET_LAYERS:
+            raise ValueError(f"Unsupported or unknown architecture: {name}!")
+        self.name = name
+        sd = W.synthetic_resnet_state_dict(name, seed) if state_dict is None else W.to_torchvision_keys(state_dict)
+        self.device = torch.device(device)
+        folded = W.folded_resnet(sd, name)
+        self.convs = {k: (w.to(self.device), b.to(self.device)) for k, (w, b) in folded.items()}
+        self.layers = W.RESNET_LAYERS[name]
+
+    def _conv(self, x, name, stride, pad, relu, residual=None):
+        w, b = self.convs[name]
+        return ops.conv2d(x, w, b, stride, pad, residual, relu)
+
+    def forward(self, x):
+        x = self._conv(x, "conv1", 2, 3, True)
+        x = ops.maxpool2d(x, 3, 2, 1)
+        for li, nb in enumerate(self.layers):
+            for bi in range(nb):
+                p = f"layer{li + 1}.{bi}"
+                s = 2 if (bi == 0 and li > 0) else 1  # torchvision v1.5: stride on the 3x3
+                idn = self._conv(x, f"{p}.downsample.0", s, 0, False) if bi == 0 else x
+                y = self._conv(x, f"{p}.conv1", 1, 0, True)
+                y = self._conv(y, f"{p}.conv2", s, 1, True)
+                x = self._conv(y, f"{p}.conv3", 1, 0, True, residual=idn)
+        return x
+
+    __call__ = forward
+
+
+class gem:
+    """GeM pooling with python-float p (networks/RetrievalNet.py:318-325)."""
+
+    def __init__(self, p=3.0, eps=1e-6):
+        self.p = float(p)
+        self.eps = float(eps)
+
+    def __call__(self, x_nhwc):
+        return ops.gem_pool(x_nhwc, self.p, self.eps)
+
+
+class _Extractor:
+    def eval(self):
+        return self
+
+    def train(self, mode=False):
+        if mode:
+            raise NotImplementedError("training is out of scope (SURVEY.md §2: row 13)")
+        return self
+
+    def to(self, *_a, **_k):
+        return self
+
+    def _input(self, x):
+        if not isinstance(x, torch.Tensor) or not x.is_cuda:
+            raise ValueError("forward_test expects a float32 [B,3,H,W] tensor on a ROCm device")
+        x = x.float() if x.dtype != torch.float32 else x
+        return ops.nchw_to_nhwc(x.contiguous())
+
+    def forward_test_nhwc(self, x_nhwc):
+        raise NotImplementedError
+
+    @torch.no_grad()
+    def forward_test(self, x):
+        return self.forward_test_nhwc(self._input(x))
+
+    @torch.no_grad()
+    def forward_test_u8(self, img_nhwc_u8):
+        """uint8 [B,H,W,3] pixels -> descriptors, with ToTensor+Normalize fused
+        into the first kernel (dataset/configdataset.py:417)."""
+        return self.forward_test_nhwc(ops.preprocess_u8(img_nhwc_u8))
+
+
+class GeM(_Extractor):
+    """GeM network (networks/RetrievalNet.py:327-344): backbone -> gem(p=3) ->
+    whiten 1x1 conv (outputdim -> 2048, +bias) -> F.normalize.
+
+    As in the reference, the whitening conv takes ``outputdim`` input channels,
+    so the network is only well-formed for outputdim == 2048 (:332)."""
+
+    def __init__(self, outputdim=2048, backbone="resnet101", state_dict=None, whiten=None, seed=0, device="cuda"):
+        if outputdim != 2048:
+            raise ValueError("networks.GeM requires outputdim == 2048 (whiten is Conv2d(outputdim, 2048), "
+                             "networks/RetrievalNet.py:332)")
+        self.device = torch.device(device)
+        self.backbone = ResNet(backbone, state_dict, seed, device)
+        self.pooling = gem()
+        if whiten is None:
+            ww, wb = W.synthetic_linear(2048, outputdim, seed + 1)
+        else:
+            ww, wb = whiten
+            ww = ww.reshape(ww.shape[0], -1)
+        self.whiten_w = ww.float().contiguous().to(self.device)
+        self.whiten_b = wb.float().contiguous().to(self.device)
+        self.outputdim = outputdim
+
+    def forward_test_nhwc(self, x_nhwc):
+        f = self.backbone(x_nhwc)
+        f = self.pooling(f)
+        f = ops.linear(f, self.whiten_w, self.whiten_b)
+        return ops.l2_normalize(f, EPS_L2, out=f)
+
+
+class ConvDimReduction:
+    """PCA-whitening as a frozen 1x1 conv (networks/spca.py:205-227):
+    weight = P[:dim], bias = -(P m)[:dim]."""
+
+    def __init__(self, input_dim, dim, device="cuda"):
+        self.input_dim, self.dim = input_dim, dim
+        self.device = torch.device(device)
+        self.weight = None
+        self.bias = None
+
+    def initialize_pca_whitening(self, des):
+        """Fit (m, P) on descriptors des [N, input_dim] (numpy), exactly as
+        pcawhitenlearn_shrinkage (networks/backbone.py:42-58) + spca.py:215-227."""
+        m, P = pcawhitenlearn_shrinkage(np.asarray(des))
+        m, P = m.T, P.T
+        self.weight = torch.tensor(P[: self.dim, :], dtype=torch.float32).contiguous().to(self.device)
+        shift = -torch.mm(torch.tensor(P, dtype=torch.float32), torch.tensor(m, dtype=torch.float32)).squeeze()
+        self.bias = shift[: self.dim].contiguous().to(self.device)
+        return m.T, P.T
+
+    def set_params(self, weight, bias):
+        self.weight = weight.reshape(weight.shape[0], -1).float().contiguous().to(self.device)
+        self.bias = bias.float().contiguous().to(self.device)
+
+    def __call__(self, x):
+        if self.weight is None:
+            raise RuntimeError("ConvDimReduction: call initialize_pca_whitening or set_params first")
+        return ops.linear(x, self.weight, self.bias)
+
+
+def pcawhitenlearn_shrinkage(X, s=1.0):
+    """PCA whitening with shrinkage, restating networks/backbone.py:42-58 on the
+    host: symmetrised covariance of the centred descriptors, LAPACK geev
+    (np.linalg.eig, as the reference, so eigenvector signs agree), components in
+    descending eigenvalue order, projection scaled by lambda^(-s/2).
+    Returns (mean [1,D], P^T [D,D])."""
+    n = X.shape[0]
+    mean = X.mean(axis=0, keepdims=True)
+    centred = X - mean
+    gram = centred.T @ centred
+    cov = (gram + gram.T) / (2 * n)
+    lam, vec = np.linalg.eig(cov)
+    desc = np.argsort(lam)[::-1]
+    lam, vec = lam[desc], vec[:, desc]
+    # np.power, not `**`: numpy turns `x ** 0.5` into sqrt, 1 ulp off pow
+    proj = np.linalg.inv(np.diag(np.power(lam, 0.5 * s))) @ vec.T
+    return mean, proj.T
+
+
+class GeMPCAw(_Extractor):
+    """Config C3 extractor: networks.GeM (R101, 2048-d) -> PCA-whitening
+    (ConvDimReduction) -> L2.  The reference has no caller wiring the two
+    (SURVEY.md §3.4); this is the cirtorch-style composition normalise ->
+    whiten -> normalise."""
+
+    def __init__(self, net, pcaw):
+        self.net = net
+        self.pcaw = pcaw
+        self.outputdim = pcaw.dim
+
+    def forward_test_nhwc(self, x_nhwc):
+        f = self.net.forward_test_nhwc(x_nhwc)
+        f = self.pcaw(f)
+        return ops.l2_normalize(f, EPS_L2, out=f)

@@ -86,6 +86,20 @@ def conv2d(x, w, bias, stride=1, pad=0, residual=None, relu=False):
     return y
 
 
+def resize_bilinear(x_nhwc, out_h, out_w, scale_factor=None):
+    """NHWC bilinear resize, align_corners=False.  With ``scale_factor`` the
+    source index uses 1/scale_factor, as F.interpolate(scale_factor=s) does."""
+    _f32(x_nhwc, "resize_bilinear")
+    dev = _dev(x_nhwc)
+    b, h, w, c = x_nhwc.shape
+    y = torch.empty((b, out_h, out_w, c), dtype=torch.float32, device=x_nhwc.device)
+    inv = 0.0 if scale_factor is None else float(1.0 / scale_factor)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_resize_bilinear(hd, _ptr(x_nhwc), b, h, w, c, int(out_h), int(out_w), inv, inv, _ptr(y),
+                                             _stream(dev)), hd, "rr_resize_bilinear")
+    return y
+
+
 def maxpool2d(x, k=3, stride=2, pad=1):
     _f32(x, "maxpool2d")
     dev = _dev(x)

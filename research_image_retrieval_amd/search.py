@@ -1,0 +1,75 @@
+"""search — the reference ranker (iris_evaluate.py:378-386) on librr.
+
+Reference lines:
+    query_features = F.normalize(query_features, p=2, dim=1)      # :379
+    gallery_features = F.normalize(gallery_features, p=2, dim=1)  # :380
+    similarity = torch.mm(query_features, gallery_features.t())   # :383
+    ranks = np.argsort(-similarity, axis=1)                        # :386
+Here: descriptors are L2-normalised on the GPU, the cosine GEMM + top-k run
+fused in rr_cosine_topk (fp32 MFMA, stable order score desc / index asc), and
+ranks come back in the layout ``compute_map`` consumes:
+    k=None -> int64 ndarray [N, Q]   (compute_map(..., li=False), utils/evaluate.py:79-80)
+    k=int  -> list of Q int64 arrays (compute_map(..., li=True),  utils/evaluate.py:75-77)
+(the reference's own driver passes a [Q,N] array with li=False, a layout bug —
+SURVEY.md Appendix A.2 — which this API does not reproduce).
+"""
+import numpy as np
+import torch
+
+from . import ops
+
+MAX_FULL_RANK = 16384  # full ranking sorts one query's scores in LDS
+
+
+def _dev_f32(x, device):
+    if isinstance(x, np.ndarray):
+        x = torch.from_numpy(x)
+    return x.to(device=device, dtype=torch.float32).contiguous()
+
+
+class GallerySearcher:
+    """A gallery resident in HBM plus a reusable top-k workspace.
+
+    ``normalize=True`` applies F.normalize to the gallery once at load (as
+    iris_evaluate.py:380); pass False for descriptors that are already unit
+    norm (extractor outputs are)."""
+
+    def __init__(self, gallery, device="cuda", normalize=True, idx_offset=0):
+        self.device = torch.device(device)
+        g = _dev_f32(gallery, self.device)
+        self.gallery = ops.l2_normalize(g, 1e-12) if normalize else g
+        self.idx_offset = int(idx_offset)
+        self._ws = None
+
+    @property
+    def n(self):
+        return self.gallery.shape[0]
+
+    def topk(self, queries, k, normalize=True):
+        """-> (scores [Q,k] fp32, idx [Q,k] int64) on the device."""
+        q = _dev_f32(queries, self.device)
+        if normalize:
+            q = ops.l2_normalize(q, 1e-12)
+        need = ops.cosine_topk_workspace_size(q.shape[0], self.n, q.shape[1], k)
+        if self._ws is None or self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        return ops.cosine_topk(q, self.gallery, k, idx_offset=self.idx_offset, workspace=self._ws)
+
+
+def search(qvecs, vecs, k=None, return_scores=False, device="cuda", normalize=True):
+    """Rank gallery ``vecs`` [N,D] for every query in ``qvecs`` [Q,D].
+
+    k=None: full ranking, int64 [N, Q] (N <= 16384 per call).
+    k=int : list of Q int64 arrays of the top-k gallery indices."""
+    g = GallerySearcher(vecs, device=device, normalize=normalize)
+    n = g.n
+    kk = n if k is None else min(int(k), n)
+    if k is None and n > MAX_FULL_RANK:
+        raise ValueError(f"full ranking supports N <= {MAX_FULL_RANK}; pass k for larger galleries")
+    if kk == 0:
+        ranks = np.zeros((0, len(qvecs)), np.int64)
+        return (ranks, None) if return_scores else ranks
+    s, i = g.topk(qvecs, kk, normalize=normalize)
+    s, i = s.cpu().numpy(), i.cpu().numpy()
+    ranks = i.T.copy() if k is None else [row for row in i]
+    return (ranks, s) if return_scores else ranks

@@ -1,0 +1,146 @@
+"""Backbone weights: seeded synthetic torchvision-keyed state dicts, local
+checkpoint loading, reference key-layout remaps and eval-mode BN folding.
+
+No network access exists (pretrained=True/'v1'/'v2' in the reference downloads
+ImageNet weights, networks/backbone.py:63-72, models/gem_pooling.py:35-38), so
+weights come either from a LOCAL torchvision-keyed file or from a seeded
+generator.  The generator uses numpy RandomState (stream-stable across numpy
+versions) so the oracle, the tests and bench.py all rebuild identical weights
+from a seed.
+"""
+import collections
+
+import numpy as np
+import torch
+
+# torchvision resnet{50,101} bottleneck counts (networks/backbone.py:63-72 via
+# torchvision.models.resnet50/101; models/gem_pooling.py:34-38)
+RESNET_LAYERS = {"resnet50": (3, 4, 6, 3), "resnet101": (3, 4, 23, 3), "resnet152": (3, 8, 36, 3)}
+BN_EPS = 1e-5
+
+
+def resnet_conv_specs(arch):
+    """Ordered (prefix, cout, cin, k) of every conv + its BN prefix, torchvision layout."""
+    layers = RESNET_LAYERS[arch]
+    specs = [("conv1", "bn1", 64, 3, 7)]
+    inplanes = 64
+    for li, nblocks in enumerate(layers):
+        planes = 64 * (2 ** li)
+        for bi in range(nblocks):
+            p = f"layer{li + 1}.{bi}"
+            specs.append((f"{p}.conv1", f"{p}.bn1", planes, inplanes, 1))
+            specs.append((f"{p}.conv2", f"{p}.bn2", planes, planes, 3))
+            specs.append((f"{p}.conv3", f"{p}.bn3", planes * 4, planes, 1))
+            if bi == 0:
+                specs.append((f"{p}.downsample.0", f"{p}.downsample.1", planes * 4, inplanes, 1))
+            inplanes = planes * 4
+    return specs
+
+
+def synthetic_resnet_state_dict(arch="resnet101", seed=0):
+    """Seeded torchvision-keyed trunk weights (conv1..layer4; no fc).
+
+    Convs: Kaiming-normal (fan_out, ReLU), as torchvision's init.  BatchNorm
+    running statistics and affine parameters are randomised (not identity) so
+    that BN folding is exercised; the last BN of every bottleneck gets a small
+    gamma so activations stay O(1) through 33 residual blocks."""
+    rs = np.random.RandomState(seed)
+    sd = collections.OrderedDict()
+    for conv, bn, cout, cin, k in resnet_conv_specs(arch):
+        std = np.sqrt(2.0 / (cout * k * k))
+        sd[conv + ".weight"] = torch.from_numpy((rs.standard_normal((cout, cin, k, k)) * std).astype(np.float32))
+        last = bn.endswith("bn3") or bn.endswith("downsample.1")
+        lo, hi = (0.05, 0.25) if last else (0.5, 1.0)
+        sd[bn + ".weight"] = torch.from_numpy(rs.uniform(lo, hi, cout).astype(np.float32))
+        sd[bn + ".bias"] = torch.from_numpy((rs.standard_normal(cout) * 0.05).astype(np.float32))
+        sd[bn + ".running_mean"] = torch.from_numpy((rs.standard_normal(cout) * 0.05).astype(np.float32))
+        sd[bn + ".running_var"] = torch.from_numpy(rs.uniform(0.5, 1.5, cout).astype(np.float32))
+        sd[bn + ".num_batches_tracked"] = torch.tensor(0, dtype=torch.int64)
+    return sd
+
+
+def synthetic_linear(out_dim, in_dim, seed, bias=True, scale=None):
+    """Seeded Linear / 1x1-conv weights ([out,in], [out])."""
+    rs = np.random.RandomState(seed)
+    s = scale if scale is not None else 1.0 / np.sqrt(in_dim)
+    w = torch.from_numpy((rs.uniform(-1, 1, (out_dim, in_dim)) * s).astype(np.float32))
+    b = torch.from_numpy((rs.uniform(-1, 1, out_dim) * s).astype(np.float32)) if bias else None
+    return w, b
+
+
+# ---- reference key layouts -------------------------------------------------
+# networks.ResNet (networks/backbone.py:93-101) renames children[:-2] into
+# block1 = [conv1, bn1, relu, maxpool], block2..5 = layer1..4;
+# GeMModel (models/gem_pooling.py:44) keeps nn.Sequential indices 0..7.
+_SEQ_TO_TV = {"0": "conv1", "1": "bn1", "4": "layer1", "5": "layer2", "6": "layer3", "7": "layer4"}
+_BLOCK_TO_TV = {"block2": "layer1", "block3": "layer2", "block4": "layer3", "block5": "layer4"}
+
+
+def to_torchvision_keys(sd, prefix=""):
+    """Map a reference checkpoint's trunk keys to torchvision keys.
+
+    Accepts plain torchvision keys, networks-style ``backbone.block{1..5}.*``
+    (e.g. ``globalmodel.backbone.block1.0.weight`` saved by the reference's
+    load_checkpoint, utils/helpfunc.py:342-368) and Table-1
+    ``backbone.backbone.{0..7}.*`` keys.  Non-trunk keys are dropped."""
+    out = collections.OrderedDict()
+    for k, v in sd.items():
+        if prefix and not k.startswith(prefix):
+            continue
+        k2 = k[len(prefix):]
+        for lead in ("module.", "globalmodel.", "backbone.backbone.", "backbone."):
+            if k2.startswith(lead):
+                k2 = k2[len(lead):]
+        parts = k2.split(".")
+        if parts[0] == "block1" and len(parts) >= 3:
+            parts = [{"0": "conv1", "1": "bn1"}.get(parts[1], "?")] + parts[2:]
+        elif parts[0] in _BLOCK_TO_TV:
+            parts = [_BLOCK_TO_TV[parts[0]]] + parts[1:]
+        elif parts[0] in _SEQ_TO_TV:
+            parts = [_SEQ_TO_TV[parts[0]]] + parts[1:]
+        k2 = ".".join(parts)
+        if k2.startswith(("conv1.", "bn1.", "layer1.", "layer2.", "layer3.", "layer4.")):
+            out[k2] = v
+    return out
+
+
+def load_state_dict(path):
+    """Load a LOCAL checkpoint without executing anything from the file."""
+    if path.endswith(".safetensors"):
+        from safetensors.torch import load_file
+        return load_file(path)
+    obj = torch.load(path, map_location="cpu", weights_only=True)
+    for key in ("state_dict", "model"):
+        if isinstance(obj, dict) and key in obj and isinstance(obj[key], dict):
+            obj = obj[key]
+    return obj
+
+
+def fold_bn(conv_w, bn, eps=BN_EPS):
+    """Eval-mode BN folded into the preceding bias-free conv.
+
+    Returns (w [Cout,KH,KW,Cin] fp32 NHWC-ready, bias [Cout] fp32); the fold
+    is computed in float64 then rounded once."""
+    w = conv_w.double()
+    g = bn["weight"].double()
+    b = bn["bias"].double()
+    m = bn["running_mean"].double()
+    v = bn["running_var"].double()
+    scale = g / torch.sqrt(v + eps)
+    wf = (w * scale[:, None, None, None]).permute(0, 2, 3, 1).contiguous().float()
+    bf = (b - m * scale).float()
+    return wf, bf
+
+
+def folded_resnet(sd, arch):
+    """torchvision-keyed trunk -> ordered list of folded (name, w, b, stride, pad)."""
+    def bn(prefix):
+        return {k: sd[f"{prefix}.{k}"] for k in ("weight", "bias", "running_mean", "running_var")}
+
+    out = collections.OrderedDict()
+    for conv, bnp, cout, cin, k in resnet_conv_specs(arch):
+        w = sd[conv + ".weight"]
+        if tuple(w.shape) != (cout, cin, k, k):
+            raise ValueError(f"{conv}: expected {(cout, cin, k, k)}, got {tuple(w.shape)}")
+        out[conv] = fold_bn(w, bn(bnp))
+    return out

@@ -1,0 +1,39 @@
+"""The C-ABI library loads and exports every symbol include/rr.h declares
+(no compute calls: CPU-only container)."""
+import ctypes
+import os
+import re
+
+from research_image_retrieval_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_symbols():
+    txt = open(os.path.join(ROOT, "include", "rr.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(rr_[a-z0-9_]+)\s*\(", txt)))
+
+
+def test_header_matches_binding_table():
+    assert header_symbols() == sorted(_lib.SIGNATURES)
+
+
+def test_library_exports_all_symbols():
+    L = ctypes.CDLL(_lib.LIB_PATH)
+    for name in header_symbols():
+        assert hasattr(L, name), name
+    assert b"gfx950" in _lib.lib().rr_version()
+
+
+def test_library_is_gfx950_code_object():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_no_device_calls_error_cleanly_without_gpu():
+    # null handle -> RR_EINVAL, never a crash
+    L = _lib.lib()
+    assert L.rr_conv2d(None, None, 0, 0, 0, 0, None, None, 0, 0, 0, 0, 0, None, 0, None, None) == _lib.RR_EINVAL
+    assert L.rr_timing_enable(None, 1) == _lib.RR_EINVAL
+    assert L.rr_cosine_topk_workspace_size(256, 1_600_000, 2048, 100) >= 256 * (1_600_000 - 32768 + 100) * 8

@@ -1,0 +1,136 @@
+"""Pin the oracle (oracle/) and the host-side restatements to the golden
+fixtures generated from the reference's own functions (tests/golden/make_golden.py)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+import oracle
+from oracle import embed_ref
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+sys.path.insert(0, GOLD)
+import inputs as I  # noqa: E402
+
+
+def load(name):
+    return np.load(os.path.join(GOLD, name + ".npz"))
+
+
+def near_tie_mask(sorted_scores, eps=2e-6):
+    """True at rank r if the score there is within eps of rank r-1 or r+1."""
+    s = sorted_scores
+    d = np.abs(np.diff(s, axis=1)) < eps
+    m = np.zeros_like(s, dtype=bool)
+    m[:, 1:] |= d
+    m[:, :-1] |= d
+    return m
+
+
+@pytest.mark.parametrize("tag", ["rank_a", "rank_b"])
+def test_oracle_ranker_vs_reference(tag):
+    fx = load(tag)
+    q, g = I.rank_inputs(int(fx["seed"]), int(fx["nq"]), int(fx["n"]), int(fx["d"]))
+    s, i = oracle.cosine_topk(q, g, 100)
+    # cosine scores within 1e-5 of the reference's torch.mm (north_star bar)
+    assert np.abs(s - fx["top_scores"]).max() < 1e-5
+    # indices identical except at near-ties (|score gap| < 2e-6)
+    ties = near_tie_mask(fx["top_scores"])
+    mism = (i != fx["top_idx_stable"])
+    assert not (mism & ~ties).any(), np.argwhere(mism & ~ties)[:5]
+    # the planted exact duplicates make stable vs default-kind argsort matter
+    assert (fx["top_idx_default"].shape == i.shape)
+
+
+def test_oracle_gem_pooling_bitexact():
+    fx = load("gem")
+    x = torch.from_numpy(fx["x"])
+    assert np.array_equal(embed_ref.gem(x).numpy(), fx["gem"])
+    pt = torch.ones(1) * 3.0
+    gp = F.avg_pool2d(x.clamp(min=1e-6).pow(pt), (7, 7)).pow(1.0 / pt)
+    assert np.array_equal(gp.numpy(), fx["gempool"])
+    # the two reference variants differ by at most a few ulp
+    assert np.abs(fx["gem"] - fx["gempool"]).max() < 1e-6
+
+
+def test_oracle_extractor_tails():
+    fx = load("gem_tail")
+    from research_image_retrieval_amd.weights import synthetic_linear
+    x2 = torch.from_numpy(I.feature_map(int(fx["x2_seed"]), 2, 2048, 7, 7))
+    ww, wb = synthetic_linear(2048, 2048, int(fx["whiten_seed"]))
+    f = embed_ref.gem(x2)
+    out = F.normalize(F.conv2d(f, ww.view(2048, 2048, 1, 1), wb).squeeze(-1).squeeze(-1), dim=-1)
+    np.testing.assert_allclose(out.numpy(), fx["gem_net"], rtol=0, atol=1e-6)
+    pw, pb = synthetic_linear(512, 2048, int(fx["proj_seed"]))
+    pt = torch.ones(1) * 3.0
+    f2 = F.avg_pool2d(x2.clamp(min=1e-6).pow(pt), (7, 7)).pow(1.0 / pt).view(2, -1)
+    out2 = F.normalize(F.linear(f2, pw, pb), p=2, dim=1)
+    np.testing.assert_allclose(out2.numpy(), fx["gem_model"], rtol=0, atol=1e-6)
+
+
+def test_pca_whitening_learn_matches_reference():
+    from research_image_retrieval_amd.networks import ConvDimReduction, pcawhitenlearn_shrinkage
+    fx = load("pcaw")
+    m, PT = pcawhitenlearn_shrinkage(fx["X"])
+    np.testing.assert_array_equal(m, fx["mean"])
+    np.testing.assert_array_equal(PT, fx["PT"])
+    cdr = ConvDimReduction(64, 32, device="cpu")
+    cdr.initialize_pca_whitening(fx["X"])
+    np.testing.assert_array_equal(cdr.weight.numpy(), fx["w"].reshape(32, 64))
+    np.testing.assert_array_equal(cdr.bias.numpy(), fx["b"])
+    y = embed_ref.pcaw_apply(torch.from_numpy(fx["Y"]), cdr.weight, cdr.bias)
+    np.testing.assert_allclose(y.numpy(), fx["y"], rtol=0, atol=1e-6)
+
+
+def test_map_evaluator_bitexact():
+    from research_image_retrieval_amd.evaluate import compute_map, compute_map_and_print
+    fx = load("map")
+    gnd, ranks = I.map_inputs(int(fx["seed"]))
+    full = compute_map_and_print("roxford5k", "g", "global", ranks, gnd, kappas=[1, 5, 10])
+    assert np.array_equal(np.array(full), fx["full"])
+    lists = [ranks[:100, i] for i in range(ranks.shape[1])]
+    trunc = compute_map_and_print("rparis6k", "g", "global", lists, gnd, kappas=[1, 5, 10], li=True)
+    assert np.array_equal(np.array(trunc), fx["trunc"])
+    g_m = [{"ok": np.concatenate([x["easy"], x["hard"]]), "junk": x["junk"]} for x in gnd]
+    mAP, aps, pr, prs = compute_map(ranks, g_m, [1, 5, 10])
+    assert mAP == fx["medium_map"]
+    assert np.array_equal(aps, fx["medium_aps"]) and np.array_equal(pr, fx["medium_pr"])
+    assert np.array_equal(prs, fx["medium_prs"])
+    mAP2, aps2 = compute_map(ranks, g_m)
+    assert mAP2 == fx["medium_map_nokeeps"] and np.array_equal(aps2, fx["medium_aps_nokeeps"])
+
+
+def test_map_evaluator_handles_reference_crash_cases():
+    from research_image_retrieval_amd.evaluate import compute_map, compute_map_and_print
+    gnd = [{"ok": np.array([5, 6]), "junk": np.array([1])}, {"ok": np.array([0]), "junk": np.array([], dtype=int)}]
+    lists = [np.array([0, 1, 2]), np.array([0, 3])]  # query 0 has no positive in its list
+    mAP, aps, pr, prs = compute_map(lists, gnd, [1, 5], li=True)
+    assert aps[0] == 0.0 and aps[1] == 1.0 and prs[0].tolist() == [0.0, 0.0]
+    assert compute_map_and_print("oxford5k", "g", "global", np.array([[0, 0], [5, 3], [6, 1]]), gnd) >= 0
+
+
+def test_oracle_extract_vectors_multiscale():
+    fx = load("extract")
+    tn = I.TinyNetRef(int(fx["net_seed"]))
+    imgs = I.tiny_images(int(fx["img_seed"]))
+    v1 = embed_ref.extract_vectors_ref(tn.forward_test, imgs, ms=(1,))
+    v3 = embed_ref.extract_vectors_ref(tn.forward_test, imgs, ms=(1, 1 / np.sqrt(2), 1 / 2))
+    np.testing.assert_array_equal(v1.numpy(), fx["v1"])
+    np.testing.assert_array_equal(v3.numpy(), fx["v3"])
+
+
+def test_oracle_merge_and_topk_rows_consistent():
+    rs = np.random.RandomState(0)
+    s = rs.standard_normal((5, 300)).astype(np.float32)
+    s[:, 10] = s[:, 20]  # ties
+    ts, ti = oracle.topk_rows(s, 50)
+    np.testing.assert_array_equal(ti, oracle.argsort_stable_desc(s)[:, :50])
+    parts_s = np.stack([s[:, :150], s[:, 150:]])
+    p0s, p0i = oracle.topk_rows(parts_s[0], 50)
+    p1s, p1i = oracle.topk_rows(parts_s[1], 50, idx_offset=150)
+    ms, mi = oracle.topk_merge(np.stack([p0s, p1s]), np.stack([p0i, p1i]), 50)
+    np.testing.assert_array_equal(mi, ti)
+    np.testing.assert_array_equal(ms, ts)
