@@ -1,0 +1,253 @@
+"""bench.py — images embedded + ranked per second against a 1.6M x 2048 gallery
+(BASELINE.json metric), on librr's gfx950 kernels.
+
+Workload (config C3 of BASELINE.json, the one the metric is quoted on; it fits
+one MI355X: the 1.6M x 2048 fp32 gallery is 13.1 GB of the 288 GB HBM):
+  per GPU and step: B synthetic uint8 224x224x3 images (resident in HBM) ->
+  ToTensor+Normalize -> ResNet-101 (BN folded) -> GeM(p=3) -> whiten 1x1 conv
+  -> L2 -> PCA-whitening (2048 -> 2048) -> L2 -> exact stable top-100 cosine
+  search against the WHOLE gallery.
+  N GPUs: one process per GPU (torch.distributed.run), gallery row-sharded
+  (1.6M/N rows each), query descriptors all-gathered over RCCL, per-shard
+  fused top-k, partial lists exchanged by all-to-all, k-way merge.  Per-GPU
+  work is fixed as N grows ("weak" scaling): value = N * B * K / max-over-ranks time.
+
+One JSON line on rank 0 with the contract keys plus `roofline` (dominant
+kernel by measured time, HIP events on the launch stream), `roofline_by_kernel`
+and `cpu_baseline` (oracle CPU restatement of the reference path, rank 0, N=1).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from research_image_retrieval_amd import _lib, ops  # noqa: E402
+from research_image_retrieval_amd import weights as W  # noqa: E402
+from research_image_retrieval_amd.distributed import ShardedGallery, shard_bounds  # noqa: E402
+from research_image_retrieval_amd.networks import GeM, ConvDimReduction, GeMPCAw  # noqa: E402
+
+METRIC = "images embedded+ranked/sec on 1.6M×2048 gallery; mAP on ROxf/RPar"
+PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
+PEAK_HBM_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def make_gallery(n_total, d, lo, hi, device, seed=0):
+    """Rows [lo, hi) of a seeded Gaussian gallery, L2-normalised, generated on
+    the GPU in 64k-row blocks keyed by global block index (shard-invariant)."""
+    g = torch.empty((hi - lo, d), dtype=torch.float32, device=device)
+    blk = 65536
+    gen = torch.Generator(device=device)
+    b0 = lo // blk
+    for b in range(b0, (hi + blk - 1) // blk):
+        gen.manual_seed(seed * 1_000_003 + b)
+        rows = torch.randn((blk, d), generator=gen, device=device)
+        s, e = max(lo, b * blk), min(hi, (b + 1) * blk)
+        g[s - lo:e - lo] = rows[s - b * blk:e - b * blk]
+    ops.l2_normalize(g, 1e-12, out=g)
+    return g
+
+
+def build_extractor(arch, device, seed=0):
+    net = GeM(2048, backbone=arch, seed=seed, device=device)
+    pw = ConvDimReduction(2048, 2048, device=device)
+    w, b = W.synthetic_linear(2048, 2048, seed + 5, scale=1.0 / np.sqrt(2048))
+    pw.set_params(w, b)
+    return GeMPCAw(net, pw)
+
+
+def cpu_baseline(arch, n_total, d, k, seed=0):
+    """The reference's CPU path, timed on a bounded sample on this host:
+    batch-1 extraction (utils/helpfunc.py:18-48 semantics) through the oracle's
+    torch-CPU restatement of ResNet->GeM->whiten->L2->PCA-w->L2, then the
+    ranker of iris_evaluate.py:383-386 (torch.mm + full np.argsort) against a
+    200k-row gallery sample, scaled to the full gallery."""
+    from oracle import embed_ref
+    threads = torch.get_num_threads()
+    n_img, n_q, n_g = 4, 16, 200_000
+    sd = W.synthetic_resnet_state_dict(arch, seed)
+    ww, wb = W.synthetic_linear(2048, 2048, seed + 1)
+    pw, pb = W.synthetic_linear(2048, 2048, seed + 5, scale=1.0 / np.sqrt(2048))
+    rs = np.random.RandomState(1234)
+    imgs = torch.from_numpy(rs.randint(0, 256, size=(n_img, 224, 224, 3), dtype=np.uint8))
+    layers = W.RESNET_LAYERS[arch]
+    with torch.no_grad():
+        x = embed_ref.normalize_u8(imgs[:1])
+        embed_ref.gem_net_forward_test(x, sd, layers, ww, wb)  # warm-up
+        t0 = time.perf_counter()
+        for i in range(n_img):
+            x = embed_ref.normalize_u8(imgs[i:i + 1])
+            f = embed_ref.gem_net_forward_test(x, sd, layers, ww, wb)
+            embed_ref.pcaw_apply(f, pw, pb)
+        t_embed = (time.perf_counter() - t0) / n_img
+        gen = torch.Generator().manual_seed(7)
+        gal = torch.nn.functional.normalize(torch.randn(n_g, d, generator=gen), dim=1)
+        q = torch.nn.functional.normalize(torch.randn(n_q, d, generator=gen), dim=1)
+        t0 = time.perf_counter()
+        sim = torch.mm(q, gal.t()).numpy()
+        t_mm = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        np.argsort(-sim, axis=1)
+        t_sort = time.perf_counter() - t0
+        t0 = time.perf_counter()
+        torch.topk(torch.from_numpy(sim), k, dim=1)
+        t_topk = time.perf_counter() - t0
+    scale = n_total / n_g
+    t_rank = (t_mm + t_sort) * scale / n_q  # per query, full gallery, reference argsort
+    t_rank_topk = (t_mm + t_topk) * scale / n_q
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return {"value": 1.0 / (t_embed + t_rank), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n_img} images embedded at batch 1 (224x224, {arch}-GeM+PCA-w, fp32) + {n_q} queries "
+                      f"ranked against a {n_g}-row x {d} gallery sample (torch.mm + full np.argsort), "
+                      f"rank time scaled x{scale:.0f} to {n_total} rows",
+            "embed_s_per_image": t_embed, "rank_s_per_query_argsort": t_rank, "rank_s_per_query_topk": t_rank_topk,
+            "value_with_topk": 1.0 / (t_embed + t_rank_topk), "cpu_model": model}
+
+
+def load_traffic():
+    """Per-launch HBM bytes measured by rocprofv3 --pmc (profiles/traffic.json),
+    corrected per MI355X_MICROARCH.md §HBM; None if not collected."""
+    p = os.path.join(ROOT, "profiles", "traffic.json")
+    if os.path.exists(p):
+        try:
+            return json.load(open(p))
+        except (OSError, ValueError):
+            return None
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=256, help="images per GPU per step")
+    ap.add_argument("--gallery", type=int, default=1_600_000)
+    ap.add_argument("--dim", type=int, default=2048)
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--arch", default="resnet101")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    a = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    t_setup = time.time()
+    lo, hi = shard_bounds(a.gallery, world, rank)
+    gallery = make_gallery(a.gallery, a.dim, lo, hi, dev)
+    net = build_extractor(a.arch, dev)
+    rs = np.random.RandomState(1234 + rank)
+    imgs = torch.from_numpy(rs.randint(0, 256, size=(a.batch, 224, 224, 3), dtype=np.uint8)).to(dev)
+    q_total = a.batch * world
+    ws = torch.empty(ops.cosine_topk_workspace_size(q_total, hi - lo, a.dim, a.k), dtype=torch.uint8, device=dev)
+    sharded = ShardedGallery(gallery, lo, workspace=ws) if world > 1 else None
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: shard [{lo},{hi}) x {a.dim}, batch {a.batch}")
+
+    def step():
+        desc = net.forward_test_u8(imgs)
+        if sharded is not None:
+            return sharded.search(desc, a.k)
+        return ops.cosine_topk(desc, gallery, a.k, idx_offset=lo, workspace=ws)
+
+    for _ in range(a.warmup):
+        out = step()
+    torch.cuda.synchronize()
+    # sanity: a gallery row used as a query must come back first
+    chk_s, chk_i = ops.cosine_topk(gallery[:2].contiguous(), gallery, 1, idx_offset=lo, workspace=ws)
+    assert chk_i[:, 0].tolist() == [lo, lo + 1], chk_i
+
+    timer = ops.KernelTimer(local)
+    timer.enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        out = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    cls = {name: timer.collect(c) for name, c in (("cosine_filter", _lib.TIME_COSINE), ("conv_gemm", _lib.TIME_GEMM),
+                                                   ("select", _lib.TIME_SELECT), ("elementwise", _lib.TIME_ELEM),
+                                                   ("cosine_seed", _lib.TIME_COSINE_SEED))}
+    timer.enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    value = world * a.batch * a.steps / elapsed
+
+    # ---- roofline (algorithmic FLOPs / measured kernel time) ----
+    s_rows = min(hi - lo, max(32768, a.k))
+    flop_filter = 2.0 * q_total * max(0, (hi - lo) - s_rows) * a.dim  # per filter launch (one per step)
+    flop_seed = 2.0 * q_total * s_rows * a.dim
+    conv_flops_img = sum(W.resnet_conv_flops(a.arch, 224, 224).values()) + 2 * 2 * 2048 * 2048  # + whiten + PCA-w
+    traffic = load_traffic()
+    rk = {}
+    for name, fl in (("cosine_filter", flop_filter * a.steps), ("conv_gemm", conv_flops_img * a.batch * a.steps),
+                     ("cosine_seed", flop_seed * a.steps)):
+        ms, n = cls[name]
+        if n == 0 or ms <= 0:
+            continue
+        ach = fl / (ms / 1e3) / 1e12
+        rk[name] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK_FP32_TFLOPS, 4), "ms_per_step": round(ms / a.steps, 3),
+                    "launches_per_step": n / a.steps,
+                    "traffic": (traffic or {}).get(name)}
+    for name in ("select", "elementwise"):
+        ms, n = cls[name]
+        rk[name] = {"ms_per_step": round(ms / a.steps, 3), "launches_per_step": n / a.steps}
+    dominant = max(("cosine_filter", "conv_gemm"), key=lambda c: cls[c][0])
+    roof = dict(rk[dominant])
+    roof["kernel"] = dominant
+
+    res = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+           "data": "synthetic: uint8 224x224x3 images RandomState(1234+rank); seeded Gaussian L2-normalised "
+                   "gallery; seeded ResNet/whiten/PCA-w weights (no pretrained weights offline)",
+           "config": {"workload": f"C3: {a.arch}-GeM 2048-d + PCA-whiten, embed + exact top-{a.k} against a "
+                                  f"{a.gallery}x{a.dim} gallery", "global_batch": q_total,
+                      "images_per_gpu_per_step": a.batch, "gallery_rows": a.gallery, "dim": a.dim, "k": a.k,
+                      "parallelism": f"query-dp{world} + gallery-shard{world}"},
+           "roofline": roof, "roofline_by_kernel": rk}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        t = time.time()
+        res["cpu_baseline"] = cpu_baseline(a.arch, a.gallery, a.dim, a.k)
+        log(f"cpu baseline {time.time() - t:.1f}s")
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -47,8 +47,10 @@ const char* rr_last_error(rr_handle_t h);
  * When enabled, every launch of a timed class is bracketed by hipEvents on
  * the launch stream; rr_timing_collect synchronises those events and returns
  * the accumulated milliseconds and launch count for `cls`, then resets it.
- * Classes: 0 = cosine GEMM (filter + dense), 1 = conv/linear GEMM,
- *          2 = top-k select/merge, 3 = elementwise (preprocess/pool/norm). */
+ * Classes: 0 = cosine GEMM with the fused top-k filter epilogue,
+ *          1 = conv/linear GEMM, 2 = top-k select/merge,
+ *          3 = elementwise (preprocess/resize/pool/norm),
+ *          4 = dense cosine GEMM (top-k threshold seed, rr_cosine_scores). */
 int rr_timing_enable(rr_handle_t h, int enable);
 int rr_timing_collect(rr_handle_t h, int cls, double* ms, long long* launches);
 

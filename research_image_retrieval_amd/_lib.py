@@ -17,7 +17,7 @@ CSRC = os.path.join(_HERE, "csrc")
 RR_OK, RR_EINVAL, RR_EHIP, RR_EWORKSPACE, RR_EOVERFLOW = 0, -1, -2, -3, -4
 
 # timing classes (rr_timing_enable / rr_timing_collect)
-TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM = 0, 1, 2, 3
+TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM, TIME_COSINE_SEED = 0, 1, 2, 3, 4
 
 _lib = None
 _lock = threading.RLock()

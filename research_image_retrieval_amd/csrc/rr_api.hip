@@ -179,7 +179,7 @@ int rr_cosine_topk(rr_handle_t h, const float* queries, int nq, const float* gal
   g.N = nq;
   g.C = scores_t;
   g.ldc = L.ld;
-  if (int rc = launch_gemm(h, A_DENSE, E_SCORES_T, g, s, kTimeCosine)) return rc;
+  if (int rc = launch_gemm(h, A_DENSE, E_SCORES_T, g, s, kTimeCosineSeed)) return rc;
   // 2. seed candidates with their exact top-k; tau = k-th best score
   if (int rc = launch_select_dense_seed(h, scores_t, L.ld, (int)L.s, nq, k, 0, cand, L.cap, cnt, tau, s)) return rc;
   // 3. remaining rows: fused GEMM + threshold filter (scores never hit HBM)
@@ -225,7 +225,7 @@ int rr_cosine_scores(rr_handle_t h, const float* queries, int nq, const float* g
   g.N = nq;
   g.C = scores;
   g.ldc = nq;
-  return launch_gemm(h, A_DENSE, E_STORE, g, (hipStream_t)stream, kTimeCosine);
+  return launch_gemm(h, A_DENSE, E_STORE, g, (hipStream_t)stream, kTimeCosineSeed);
 }
 
 int rr_topk_merge(rr_handle_t h, const float* ps, const long long* pi, int nparts, int nq, int k_in, int k_out,

@@ -12,10 +12,14 @@ struct rr_handle_s {
   std::string last_error;
   // timing (see rr_timing_enable)
   bool timing = false;
-  static constexpr int kClasses = 4;
-  static constexpr int kMaxEv = 4096;
-  hipEvent_t ev_start[kClasses][kMaxEv] = {};
-  hipEvent_t ev_stop[kClasses][kMaxEv] = {};
+  static constexpr int kClasses = 5;
+  static constexpr int kMaxEv = 16384;
+  hipEvent_t (*ev_start)[kMaxEv] = new hipEvent_t[kClasses][kMaxEv]();
+  hipEvent_t (*ev_stop)[kMaxEv] = new hipEvent_t[kClasses][kMaxEv]();
+  ~rr_handle_s() {
+    delete[] ev_start;
+    delete[] ev_stop;
+  }
   int n_ev[kClasses] = {};
   double acc_ms[kClasses] = {};
   long long acc_launches[kClasses] = {};
@@ -23,7 +27,7 @@ struct rr_handle_s {
 
 namespace rr {
 
-enum TimerClass { kTimeCosine = 0, kTimeGemm = 1, kTimeSelect = 2, kTimeElem = 3 };
+enum TimerClass { kTimeCosine = 0, kTimeGemm = 1, kTimeSelect = 2, kTimeElem = 3, kTimeCosineSeed = 4 };
 
 // RAII-style bracket: records start/stop events on `stream` when timing is on.
 struct TimedLaunch {

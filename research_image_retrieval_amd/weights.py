@@ -144,3 +144,29 @@ def folded_resnet(sd, arch):
             raise ValueError(f"{conv}: expected {(cout, cin, k, k)}, got {tuple(w.shape)}")
         out[conv] = fold_bn(w, bn(bnp))
     return out
+
+
+def resnet_conv_flops(arch, h, w):
+    """Algorithmic FLOPs (2*M*N*K) of every trunk conv for one h x w image,
+    following networks.ResNet.forward's strides/pads."""
+    def out(x, k, s, p):
+        return (x + 2 * p - k) // s + 1
+
+    flops = {}
+    H, Wd = out(h, 7, 2, 3), out(w, 7, 2, 3)
+    flops["conv1"] = 2 * H * Wd * 64 * 7 * 7 * 3
+    H, Wd = out(H, 3, 2, 1), out(Wd, 3, 2, 1)
+    inplanes = 64
+    for li, nb in enumerate(RESNET_LAYERS[arch]):
+        planes = 64 * 2 ** li
+        for bi in range(nb):
+            s = 2 if (bi == 0 and li > 0) else 1
+            p = f"layer{li + 1}.{bi}"
+            Ho, Wo = out(H, 3, s, 1), out(Wd, 3, s, 1)
+            if bi == 0:
+                flops[p + ".downsample.0"] = 2 * Ho * Wo * planes * 4 * inplanes
+            flops[p + ".conv1"] = 2 * H * Wd * planes * inplanes
+            flops[p + ".conv2"] = 2 * Ho * Wo * planes * planes * 9
+            flops[p + ".conv3"] = 2 * Ho * Wo * planes * 4 * planes
+            H, Wd, inplanes = Ho, Wo, planes * 4
+    return flops
