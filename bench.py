@@ -75,7 +75,7 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
     200k-row gallery sample, scaled to the full gallery."""
     from oracle import embed_ref
     threads = torch.get_num_threads()
-    n_img, n_q, n_g = 4, 16, 200_000
+    n_img, n_q, n_g = 96, 64, 400_000
     sd = W.synthetic_resnet_state_dict(arch, seed)
     ww, wb = W.synthetic_linear(2048, 2048, seed + 1)
     pw, pb = W.synthetic_linear(2048, 2048, seed + 5, scale=1.0 / np.sqrt(2048))
