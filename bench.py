@@ -72,7 +72,7 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
     batch-1 extraction (utils/helpfunc.py:18-48 semantics) through the oracle's
     torch-CPU restatement of ResNet->GeM->whiten->L2->PCA-w->L2, then the
     ranker of iris_evaluate.py:383-386 (torch.mm + full np.argsort) against a
-    200k-row gallery sample, scaled to the full gallery."""
+    400k-row gallery sample, scaled to the full gallery."""
     from oracle import embed_ref
     threads = torch.get_num_threads()
     n_img, n_q, n_g = 96, 64, 400_000
