@@ -24,6 +24,8 @@
 // k-tile; the next tile's global loads are in flight under the MFMAs.
 // Block ids are remapped so consecutive tiles of one XCD share the A panel
 // (the streamed gallery / activation rows) in that XCD's L2.
+#include <cstdlib>
+
 #include "rr_internal.hpp"
 
 namespace rr {
@@ -43,6 +45,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
   constexpr int A_CH = BM / ROWS_PER_PASS;
   constexpr int B_CH = BN / ROWS_PER_PASS;
   static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for block");
+  static_assert(BM * BN <= 2 * (BM + BN) * 32, "C tile must fit the LDS staging buffers");
   constexpr int BUF = (BM + BN) * BK;  // floats per LDS buffer
   __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
 
@@ -231,21 +234,7 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
     const int n = n0 + wn * 64 + j * 32 + lr;
     const bool nok = n < g.N;
     if constexpr (EMODE == E_STORE) {
-      const float bv = (g.bias != nullptr && nok) ? g.bias[n] : 0.f;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          if (nok && m < g.M) {
-            float v = acc[i][j][r] + bv;
-            const long long o = (long long)m * g.ldc + n;
-            if (g.residual != nullptr) v += g.residual[o];
-            if (g.relu) v = fmaxf(v, 0.f);
-            g.C[o] = v;
-          }
-        }
-      }
+      // handled below through LDS
     } else if constexpr (EMODE == E_SCORES_T) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
@@ -280,6 +269,52 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
       }
     }
   }
+
+  if constexpr (EMODE == E_STORE) {
+    // Stage the BMxBN accumulator tile through LDS (free after the last
+    // barrier of the k-loop), then write whole rows: each lane moves 16 B,
+    // 32 lanes cover a 512-B row run, residual read the same way.
+    float* ct = lds;  // [BM][BN] row-major (BM*BN <= 2*BUF floats)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int col = wn * 64 + j * 32 + lr;
+          ct[row * BN + col] = acc[i][j][r];
+        }
+    __syncthreads();
+    constexpr int C4 = BN / 4;
+    const bool vec_ok = ((g.N & 3) == 0) && ((g.ldc & 3) == 0);
+    for (int idx = tid; idx < BM * C4; idx += NT) {
+      const int row = idx / C4, c4 = idx - row * C4;
+      const int m = m0 + row, n = n0 + c4 * 4;
+      if (m >= g.M || n >= g.N) continue;
+      f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
+      const long long o = (long long)m * g.ldc + n;
+      if (vec_ok) {
+        if (g.bias != nullptr) v += *reinterpret_cast<const f32x4*>(g.bias + n);
+        if (g.residual != nullptr) v += *reinterpret_cast<const f32x4*>(g.residual + o);
+        if (g.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        }
+        *reinterpret_cast<f32x4*>(g.C + o) = v;
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (n + e >= g.N) break;
+          float x = v[e];
+          if (g.bias != nullptr) x += g.bias[n + e];
+          if (g.residual != nullptr) x += g.residual[o + e];
+          if (g.relu) x = fmaxf(x, 0.f);
+          g.C[o + e] = x;
+        }
+      }
+    }
+  }
 }
 
 template <int WM, int WN, int AM, int EM>
@@ -295,10 +330,28 @@ static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   return hipGetLastError();
 }
 
+// Tile choice: both configs run 4 waves and 2 workgroups per CU (512 slots
+// on 256 CUs).  Estimated time ~ rounds x tile area, rounds = ceil(tiles /
+// 512): this charges both the padding of N (e.g. 320 queries on 128-wide
+// tiles) and the last partially-filled round (wave quantization).
+// RR_GEMM_CFG=22|41 forces a config (tuning experiments).
+static int pick_cfg(const GemmArgs& g) {
+  static const int forced = [] {
+    const char* e = getenv("RR_GEMM_CFG");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 22 || forced == 41) return forced;
+  const long long slots = 512;
+  const long long t22 = ((g.M + 127) / 128) * ((g.N + 127) / 128);
+  const long long t41 = ((g.M + 255) / 256) * ((g.N + 63) / 64);
+  const long long c22 = ((t22 + slots - 1) / slots) * 128 * 128;
+  const long long c41 = ((t41 + slots - 1) / slots) * 256 * 64;
+  return c41 < c22 ? 41 : 22;
+}
+
 template <int AM, int EM>
 static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
-  // Narrow B (N <= 64: e.g. 64-channel convs, few queries) -> 256x64 tiles.
-  if (g.N <= 64) return launch_t<4, 1, AM, EM>(g, s);
+  if (pick_cfg(g) == 41) return launch_t<4, 1, AM, EM>(g, s);
   return launch_t<2, 2, AM, EM>(g, s);
 }
 
