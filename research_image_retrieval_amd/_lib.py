@@ -11,7 +11,8 @@ import subprocess
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "librr.so")
+# RR_LIB_PATH: load an alternative build (A/B experiments on one device)
+LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(_HERE, "librr.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_EWORKSPACE, RR_EOVERFLOW = 0, -1, -2, -3, -4
