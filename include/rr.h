@@ -50,7 +50,8 @@ const char* rr_last_error(rr_handle_t h);
  * Classes: 0 = cosine GEMM with the fused top-k filter epilogue,
  *          1 = conv/linear GEMM, 2 = top-k select/merge,
  *          3 = elementwise (preprocess/resize/pool/norm),
- *          4 = dense cosine GEMM (top-k threshold seed, rr_cosine_scores). */
+ *          4 = dense cosine GEMM (top-k threshold seed, rr_cosine_scores),
+ *          5 = fused attention (ViT). */
 int rr_timing_enable(rr_handle_t h, int enable);
 int rr_timing_collect(rr_handle_t h, int cls, double* ms, long long* launches);
 
@@ -140,6 +141,42 @@ int rr_gem_pool(rr_handle_t h, const float* x, int b, int hw, int c, float p,
  * PCA-whitening ConvDimReduction apply (networks/spca.py:205-227).        */
 int rr_linear(rr_handle_t h, const float* x, int m, int k, const float* w,
               const float* bias, int n, float* y, void* stream);
+
+/* y = act(x . w^T + bias + residual); act 0 = none, 1 = ReLU, 2 = QuickGELU
+ * (x * sigmoid(1.702 x)).  bias / residual ([m][n]) may be NULL.  Replaces the
+ * ViT projections of networks/model.py:171-192 (MHA in/out_proj, c_fc +
+ * QuickGELU, c_proj + residual) and `ln_post(x[:,0]) @ proj` (:239-241).   */
+int rr_linear_ex(rr_handle_t h, const float* x, int m, int k, const float* w,
+                 const float* bias, int n, const float* residual, int act,
+                 float* y, void* stream);
+
+/* ---- ViT-B/16 (networks/model.py:206-243) ------------------------------ */
+/* LayerNorm over the last dim (fp32, biased variance), rows x + i*ldx ->
+ * dense y [m][d].  Replaces LayerNorm (:157-163): ln_pre, ln_1, ln_2, and
+ * ln_post on the CLS rows (ldx = seq*width).  d <= 4096.                   */
+int rr_layernorm(rr_handle_t h, const float* x, long long ldx, int m, int d,
+                 const float* gamma, const float* beta, float eps, float* y,
+                 void* stream);
+
+/* NHWC image -> non-overlapping patch rows [b*(H/p)*(W/p)][p*p*c], (kh,kw,c)
+ * order: with weights [width][p][p][c] the patch conv (:223, stride = kernel
+ * = p, no bias) becomes one dense GEMM (rr_linear).                        */
+int rr_patchify(rr_handle_t h, const float* x, int b, int hgt, int wid, int c,
+                int patch, float* y, void* stream);
+
+/* tokens [b][1+np][width]: row 0 = cls + pos[0], row 1+i = patches[b][i] +
+ * pos[1+i]  (class_embedding concat + positional_embedding, :226-227).     */
+int rr_vit_tokens(rr_handle_t h, const float* patches, int b, int npatch,
+                  int width, const float* cls, const float* pos, float* y,
+                  void* stream);
+
+/* Multi-head self-attention core: qkv [b*seq][3*heads*64] (q | k | v, the
+ * in_proj output) -> out [b*seq][heads*64] = softmax(q k^T / 8) v per head
+ * (nn.MultiheadAttention, ResidualAttentionBlock.attention :184-186).
+ * head_dim == 64, seq <= 256.  Fused on fp32 MFMA, scores never leave the
+ * CU.                                                                      */
+int rr_attention(rr_handle_t h, const float* qkv, int b, int seq, int heads,
+                 int head_dim, float* out, void* stream);
 
 /* Row-wise L2 normalisation x / max(||x||_2, eps), in place allowed.
  * Replaces F.normalize (networks/RetrievalNet.py:343, models/gem_pooling.py:91,

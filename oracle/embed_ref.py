@@ -119,3 +119,30 @@ def rank_ref(q, g):
     g = F.normalize(g, p=2, dim=1)
     sim = torch.mm(q, g.t()).numpy()
     return sim, np.argsort(-sim, axis=1, kind="stable")
+
+
+def vit_forward(x, sd, patch, width, layers, heads, eps=1e-5):
+    """networks/model.py:206-243 (VisionTransformer.forward) restated with
+    torch.nn.functional, NCHW fp32 input -> ln_post(x[:, 0]) @ proj."""
+    b = x.shape[0]
+    x = F.conv2d(x, sd["conv1.weight"], None, patch)
+    x = x.reshape(b, width, -1).permute(0, 2, 1)
+    cls = sd["class_embedding"] + torch.zeros(b, 1, width)
+    x = torch.cat([cls, x], dim=1) + sd["positional_embedding"]
+    x = F.layer_norm(x, (width,), sd["ln_pre.weight"], sd["ln_pre.bias"], eps)
+    hd = width // heads
+    for i in range(layers):
+        p = f"transformer.resblocks.{i}."
+        y = F.layer_norm(x, (width,), sd[p + "ln_1.weight"], sd[p + "ln_1.bias"], eps)
+        qkv = F.linear(y, sd[p + "attn.in_proj_weight"], sd[p + "attn.in_proj_bias"])
+        q, k, v = qkv.split(width, dim=-1)
+        sh = lambda t: t.reshape(b, -1, heads, hd).transpose(1, 2)  # noqa: E731
+        att = torch.softmax((sh(q) / hd ** 0.5) @ sh(k).transpose(-2, -1), dim=-1) @ sh(v)
+        att = att.transpose(1, 2).reshape(b, -1, width)
+        x = x + F.linear(att, sd[p + "attn.out_proj.weight"], sd[p + "attn.out_proj.bias"])
+        y = F.layer_norm(x, (width,), sd[p + "ln_2.weight"], sd[p + "ln_2.bias"], eps)
+        y = F.linear(y, sd[p + "mlp.c_fc.weight"], sd[p + "mlp.c_fc.bias"])
+        y = y * torch.sigmoid(1.702 * y)
+        x = x + F.linear(y, sd[p + "mlp.c_proj.weight"], sd[p + "mlp.c_proj.bias"])
+    x = F.layer_norm(x[:, 0, :], (width,), sd["ln_post.weight"], sd["ln_post.bias"], eps)
+    return x @ sd["proj"]

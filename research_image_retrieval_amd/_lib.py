@@ -18,7 +18,7 @@ CSRC = os.path.join(_HERE, "csrc")
 RR_OK, RR_EINVAL, RR_EHIP, RR_EWORKSPACE, RR_EOVERFLOW = 0, -1, -2, -3, -4
 
 # timing classes (rr_timing_enable / rr_timing_collect)
-TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM, TIME_COSINE_SEED = 0, 1, 2, 3, 4
+TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM, TIME_COSINE_SEED, TIME_ATTN = 0, 1, 2, 3, 4, 5
 
 _lib = None
 _lock = threading.RLock()
@@ -49,6 +49,11 @@ SIGNATURES = {
     "rr_gem_pool": (_i, [_vp, _vp, _i, _i, _i, _f, _f, _vp, _vp]),
     "rr_linear": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _vp]),
     "rr_l2_normalize": (_i, [_vp, _vp, _i, _i, _f, _vp, _vp]),
+    "rr_linear_ex": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp]),
+    "rr_layernorm": (_i, [_vp, _vp, _ll, _i, _i, _vp, _vp, _f, _vp, _vp]),
+    "rr_patchify": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
+    "rr_vit_tokens": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "rr_attention": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
 }
 
 

@@ -37,6 +37,9 @@ constexpr int BK = 32;
 
 __device__ __forceinline__ int swz(int row, int slot) { return slot ^ ((row >> 1) & 7); }
 
+// QuickGELU, x * sigmoid(1.702 x) (networks/model.py:166-168)
+__device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f + expf(-(1.702f * x)))); }
+
 template <int WM, int WN, int AMODE, int EMODE>
 __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int tiles_n) {
   constexpr int NT = 64 * WM * WN;
@@ -297,9 +300,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
       if (vec_ok) {
         if (g.bias != nullptr) v += *reinterpret_cast<const f32x4*>(g.bias + n);
         if (g.residual != nullptr) v += *reinterpret_cast<const f32x4*>(g.residual + o);
-        if (g.relu) {
+        if (g.relu == 1) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        } else if (g.relu == 2) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = quick_gelu(v[e]);
         }
         *reinterpret_cast<f32x4*>(g.C + o) = v;
       } else {
@@ -309,7 +315,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
           float x = v[e];
           if (g.bias != nullptr) x += g.bias[n + e];
           if (g.residual != nullptr) x += g.residual[o + e];
-          if (g.relu) x = fmaxf(x, 0.f);
+          if (g.relu == 1) x = fmaxf(x, 0.f);
+          else if (g.relu == 2) x = quick_gelu(x);
           g.C[o + e] = x;
         }
       }

@@ -283,6 +283,11 @@ int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, c
 
 int rr_linear(rr_handle_t h, const float* x, int m, int k, const float* w, const float* bias, int n, float* y,
               void* stream) {
+  return rr_linear_ex(h, x, m, k, w, bias, n, nullptr, 0, y, stream);
+}
+
+int rr_linear_ex(rr_handle_t h, const float* x, int m, int k, const float* w, const float* bias, int n,
+                 const float* residual, int act, float* y, void* stream) {
   if (!h) return RR_EINVAL;
   if (!x || !w || !y || m < 0 || k <= 0 || n <= 0 || (k & 3)) return set_error(h, RR_EINVAL, "rr_linear: bad argument");
   if (((uintptr_t)x & 15) || ((uintptr_t)w & 15)) return set_error(h, RR_EINVAL, "rr_linear: x/w must be 16-byte aligned");
@@ -297,6 +302,9 @@ int rr_linear(rr_handle_t h, const float* x, int m, int k, const float* w, const
   g.C = y;
   g.ldc = n;
   g.bias = bias;
+  g.residual = residual;
+  if (act < 0 || act > 2) return set_error(h, RR_EINVAL, "rr_linear_ex: act must be 0, 1 or 2");
+  g.relu = act;
   return launch_gemm(h, A_DENSE, E_STORE, g, (hipStream_t)stream, kTimeGemm);
 }
 

@@ -12,7 +12,7 @@ struct rr_handle_s {
   std::string last_error;
   // timing (see rr_timing_enable)
   bool timing = false;
-  static constexpr int kClasses = 5;
+  static constexpr int kClasses = 6;
   static constexpr int kMaxEv = 16384;
   hipEvent_t (*ev_start)[kMaxEv] = new hipEvent_t[kClasses][kMaxEv]();
   hipEvent_t (*ev_stop)[kMaxEv] = new hipEvent_t[kClasses][kMaxEv]();
@@ -27,7 +27,7 @@ struct rr_handle_s {
 
 namespace rr {
 
-enum TimerClass { kTimeCosine = 0, kTimeGemm = 1, kTimeSelect = 2, kTimeElem = 3, kTimeCosineSeed = 4 };
+enum TimerClass { kTimeCosine = 0, kTimeGemm = 1, kTimeSelect = 2, kTimeElem = 3, kTimeCosineSeed = 4, kTimeAttn = 5 };
 
 // RAII-style bracket: records start/stop events on `stream` when timing is on.
 struct TimedLaunch {
@@ -85,7 +85,7 @@ struct GemmArgs {
   long long ldc = 0;
   const float* bias = nullptr;
   const float* residual = nullptr;
-  int relu = 0;
+  int relu = 0;  // epilogue activation: 0 none, 1 ReLU, 2 QuickGELU
   // filter epilogue (cosine top-k candidates): per B-row (query) threshold
   const float* tau = nullptr;
   unsigned long long* cand = nullptr;

@@ -1,0 +1,314 @@
+// vit_ops.hip — CLIP-style ViT pieces for gfx950 (networks/model.py:157-243):
+// LayerNorm (fp32, :157-163), patchify for the 16x16/16 patch conv (:223),
+// class/positional token assembly (:226-227) and a fused multi-head
+// attention (nn.MultiheadAttention inside ResidualAttentionBlock, :171-188).
+// The projections (QKV, out-proj, MLP with QuickGELU, ln_post @ proj) run on
+// the fp32 MFMA GEMM core (gemm_f32.hip).
+#include "rr_internal.hpp"
+
+namespace rr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// One wave per row: y = (x - mean) / sqrt(var + eps) * gamma + beta, biased
+// variance, two-pass over the row held in registers (D <= 64 * 64).
+template <int PER_LANE>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, long long ldx, int M, int D,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps,
+                                                        float* __restrict__ y) {
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (long long)row * ldx;
+  float v[PER_LANE];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < D ? xr[c] : 0.f;
+    s += v[i];
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  const float mean = s / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int c = lane + 64 * i;
+    const float d = c < D ? v[i] - mean : 0.f;
+    q = fmaf(d, d, q);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
+  const float rstd = 1.0f / sqrtf(q / (float)D + eps);
+  float* yr = y + (long long)row * D;
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int c = lane + 64 * i;
+    if (c < D) yr[c] = (v[i] - mean) * rstd * gamma[c] + beta[c];
+  }
+}
+
+// NHWC [B][H][W][C] -> patch rows [B*(H/P)*(W/P)][P*P*C] in (kh, kw, c) order,
+// which matches conv weights permuted to [Cout][P][P][C].
+__global__ void patchify_kernel(const float* __restrict__ x, int B, int H, int W, int C, int P,
+                                float* __restrict__ y) {
+  const int gh = H / P, gw = W / P;
+  const long long kdim = (long long)P * P * C;
+  const long long total = (long long)B * gh * gw * kdim;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
+    const long long patch = o / kdim;
+    const int k = (int)(o - patch * kdim);
+    const int kh = k / (P * C);
+    const int r = k - kh * P * C;
+    const int kw = r / C;
+    const int c = r - kw * C;
+    const int b = (int)(patch / (gh * gw));
+    const int pp = (int)(patch - (long long)b * gh * gw);
+    const int ph = pp / gw, pw = pp - (pp / gw) * gw;
+    y[o] = x[(((long long)b * H + ph * P + kh) * W + pw * P + kw) * C + c];
+  }
+}
+
+// tokens[b][0] = cls + pos[0]; tokens[b][1+p] = patches[b][p] + pos[1+p]
+__global__ void vit_tokens_kernel(const float* __restrict__ patches, int B, int NP, int Wd,
+                                  const float* __restrict__ cls, const float* __restrict__ pos,
+                                  float* __restrict__ y) {
+  const long long total = (long long)B * (NP + 1) * Wd;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
+    const int c = (int)(o % Wd);
+    const long long t = o / Wd;
+    const int l = (int)(t % (NP + 1));
+    const long long b = t / (NP + 1);
+    const float v = l == 0 ? cls[c] : patches[(b * NP + (l - 1)) * Wd + c];
+    y[o] = v + pos[(long long)l * Wd + c];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused attention, head_dim 64, fp32 MFMA (v_mfma_f32_32x32x2_f32).
+// Workgroup = one (batch, head); wave w owns queries [32w, 32w+32).
+// K and V of the head are staged in LDS once (zero rows past seq).
+//  1. S^T = K . Q^T for all NC*32 keys, kept in NC accumulator tiles: lane =
+//     query, registers = keys (row map (r&3) + 8(r>>2) + 4(lane>>5)).
+//  2. exact softmax per query: max / exp / sum over the lane's registers plus
+//     the partner lane (lane ^ 32); padded keys masked to -inf.
+//  3. O = P . V with the S^T accumulator used directly as the A operand:
+//     lane (query, h) supplies P[query][key(r, h)] for MFMA step r, and the V
+//     fragment is read from LDS at that same key.  O /= rowsum; store.
+// Q is pre-scaled by 1/sqrt(64) = 0.125 (exact).
+template <int NC>
+__global__ __launch_bounds__(64 * NC) void attention_kernel(const float* __restrict__ qkv, int B, int L, int NH,
+                                                            float* __restrict__ out) {
+  constexpr int HD = 64;
+  constexpr int LP = NC * 32;
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* Ks = smem;            // [LP][HD], 16-B slots XOR-swizzled by (row & 15)
+  float* Vs = smem + LP * HD;  // [LP][HD] row-major
+  const int bh = blockIdx.x;
+  const int b = bh / NH, h = bh - (bh / NH) * NH;
+  const int width = NH * HD;
+  const long long ld = 3LL * width;
+  const float* base = qkv + (long long)b * L * ld;
+  const int tid = threadIdx.x;
+  // stage K and V
+  for (int idx = tid; idx < LP * (HD / 4); idx += 64 * NC) {
+    const int row = idx / (HD / 4), s4 = idx - row * (HD / 4);
+    f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+    if (row < L) {
+      kv = *reinterpret_cast<const f32x4*>(base + (long long)row * ld + width + h * HD + s4 * 4);
+      vv = *reinterpret_cast<const f32x4*>(base + (long long)row * ld + 2 * width + h * HD + s4 * 4);
+    }
+    *reinterpret_cast<f32x4*>(Ks + row * HD + ((s4 ^ (row & 15)) * 4)) = kv;
+    *reinterpret_cast<f32x4*>(Vs + row * HD + s4 * 4) = vv;
+  }
+  const int wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int q0 = wave * 32;
+  // Q fragment: lane (j, h) holds Q[q0 + j][16c + 8h + e], c < 4, e < 8
+  float qf[4][8];
+  {
+    const int q = q0 + lr;
+    const bool ok = q < L;
+    const float* qp = base + (long long)(ok ? q : 0) * ld + h * HD;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      f32x4 a = *reinterpret_cast<const f32x4*>(qp + 16 * c + 8 * lh);
+      f32x4 bq = *reinterpret_cast<const f32x4*>(qp + 16 * c + 8 * lh + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        qf[c][e] = ok ? a[e] * 0.125f : 0.f;
+        qf[c][4 + e] = ok ? bq[e] * 0.125f : 0.f;
+      }
+    }
+  }
+  __syncthreads();
+  // 1. scores
+  f32x16 st[NC];
+#pragma unroll
+  for (int kc = 0; kc < NC; ++kc) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st[kc][r] = 0.f;
+    const int krow = kc * 32 + lr;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int s0 = 4 * c + 2 * lh;
+      const f32x4 k0 = *reinterpret_cast<const f32x4*>(Ks + krow * HD + ((s0 ^ (krow & 15)) * 4));
+      const f32x4 k1 = *reinterpret_cast<const f32x4*>(Ks + krow * HD + (((s0 + 1) ^ (krow & 15)) * 4));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) st[kc] = __builtin_amdgcn_mfma_f32_32x32x2f32(k0[e], qf[c][e], st[kc], 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        st[kc] = __builtin_amdgcn_mfma_f32_32x32x2f32(k1[e], qf[c][4 + e], st[kc], 0, 0, 0);
+    }
+  }
+  // 2. softmax over keys (registers x partner lane)
+  float mx = -__builtin_inff();
+#pragma unroll
+  for (int kc = 0; kc < NC; ++kc)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kc * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (key >= L) st[kc][r] = -__builtin_inff();
+      mx = fmaxf(mx, st[kc][r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kc = 0; kc < NC; ++kc)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = expf(st[kc][r] - mx);
+      st[kc][r] = p;
+      sum += p;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.0f / sum;
+  // 3. O = P V  (two 32-wide output tiles over head_dim 64)
+  f32x16 o[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+#pragma unroll
+  for (int kc = 0; kc < NC; ++kc) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kc * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      const float v0 = Vs[key * HD + lr];
+      const float v1 = Vs[key * HD + 32 + lr];
+      o[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(st[kc][r], v0, o[0], 0, 0, 0);
+      o[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(st[kc][r], v1, o[1], 0, 0, 0);
+    }
+  }
+  // normalise (1/sum lives in the query's lane) and store: lane = d, regs = queries
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int qi = (r & 3) + 8 * (r >> 2) + 4 * lh;
+    const float iq = __shfl(inv, qi, 64);
+    const int q = q0 + qi;
+    if (q < L) {
+      float* op = out + ((long long)b * L + q) * width + h * HD;
+      op[lr] = o[0][r] * iq;
+      op[32 + lr] = o[1][r] * iq;
+    }
+  }
+}
+
+static dim3 grid_for(long long n, int block) {
+  long long g = (n + block - 1) / block;
+  if (g > 256 * 16) g = 256 * 16;
+  if (g < 1) g = 1;
+  return dim3((unsigned)g);
+}
+
+template <int NC>
+static hipError_t launch_attn(const float* qkv, int B, int L, int NH, float* out, hipStream_t s) {
+  const size_t lds = (size_t)2 * NC * 32 * 64 * 4;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)attention_kernel<NC>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL(attention_kernel<NC>, dim3((unsigned)(B * NH)), dim3(64 * NC), lds, s, qkv, B, L, NH, out);
+  return hipGetLastError();
+}
+
+}  // namespace rr
+
+using namespace rr;
+
+extern "C" int rr_layernorm(rr_handle_t h, const float* x, long long ldx, int m, int d, const float* gamma,
+                            const float* beta, float eps, float* y, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !y || !gamma || !beta || m < 0 || d <= 0 || d > 4096 || ldx < d)
+    return set_error(h, RR_EINVAL, "rr_layernorm: bad argument (d <= 4096, ldx >= d)");
+  if (m == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  const dim3 grid((unsigned)(((long long)m * 64 + 255) / 256));
+  const int per = (d + 63) / 64;
+  if (per <= 4)
+    hipLaunchKernelGGL(layernorm_kernel<4>, grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
+  else if (per <= 12)
+    hipLaunchKernelGGL(layernorm_kernel<12>, grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
+  else if (per <= 16)
+    hipLaunchKernelGGL(layernorm_kernel<16>, grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<64>, grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
+  return check_hip(h, hipGetLastError(), "layernorm launch");
+}
+
+extern "C" int rr_patchify(rr_handle_t h, const float* x, int b, int hgt, int wid, int c, int patch, float* y,
+                           void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !y || b < 0 || c <= 0 || patch <= 0 || hgt % patch || wid % patch)
+    return set_error(h, RR_EINVAL, "rr_patchify: bad argument (H, W must be multiples of the patch)");
+  const long long total = (long long)b * hgt * wid * c;
+  if (total == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  hipLaunchKernelGGL(patchify_kernel, grid_for(total, 256), dim3(256), 0, s, x, b, hgt, wid, c, patch, y);
+  return check_hip(h, hipGetLastError(), "patchify launch");
+}
+
+extern "C" int rr_vit_tokens(rr_handle_t h, const float* patches, int b, int npatch, int width, const float* cls,
+                             const float* pos, float* y, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!patches || !cls || !pos || !y || b < 0 || npatch <= 0 || width <= 0)
+    return set_error(h, RR_EINVAL, "rr_vit_tokens: bad argument");
+  const long long total = (long long)b * (npatch + 1) * width;
+  if (total == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  hipLaunchKernelGGL(vit_tokens_kernel, grid_for(total, 256), dim3(256), 0, s, patches, b, npatch, width, cls, pos,
+                     y);
+  return check_hip(h, hipGetLastError(), "vit_tokens launch");
+}
+
+extern "C" int rr_attention(rr_handle_t h, const float* qkv, int b, int seq, int heads, int head_dim, float* out,
+                            void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!qkv || !out || b < 0 || heads <= 0 || head_dim != 64 || seq <= 0 || seq > 256)
+    return set_error(h, RR_EINVAL, "rr_attention: supports head_dim == 64, 1 <= seq <= 256");
+  if (b == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeAttn, s);
+  const int nc = (seq + 31) / 32;
+  hipError_t e;
+  switch (nc) {
+    case 1: e = launch_attn<1>(qkv, b, seq, heads, out, s); break;
+    case 2: e = launch_attn<2>(qkv, b, seq, heads, out, s); break;
+    case 3: e = launch_attn<3>(qkv, b, seq, heads, out, s); break;
+    case 4: e = launch_attn<4>(qkv, b, seq, heads, out, s); break;
+    case 5: e = launch_attn<5>(qkv, b, seq, heads, out, s); break;
+    case 6: e = launch_attn<6>(qkv, b, seq, heads, out, s); break;
+    case 7: e = launch_attn<7>(qkv, b, seq, heads, out, s); break;
+    default: e = launch_attn<8>(qkv, b, seq, heads, out, s); break;
+  }
+  return check_hip(h, e, "attention launch");
+}

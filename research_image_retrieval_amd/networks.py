@@ -192,3 +192,72 @@ class GeMPCAw(_Extractor):
         f = self.net.forward_test_nhwc(x_nhwc)
         f = self.pcaw(f)
         return ops.l2_normalize(f, EPS_L2, out=f)
+
+
+class VisionTransformer(_Extractor):
+    """CLIP-style ViT image tower (networks/model.py:206-243) on librr.
+
+    forward(x) returns ``ln_post(x[:, 0]) @ proj`` as the reference does;
+    forward_test(x) additionally L2-normalises (the extractor contract).
+    Weights: a CLIP-layout state dict (conv1.weight, class_embedding,
+    positional_embedding, ln_pre.*, transformer.resblocks.{i}.{attn.in_proj_*,
+    attn.out_proj.*, ln_1.*, mlp.c_fc.*, mlp.c_proj.*, ln_2.*}, ln_post.*,
+    proj).  LayerNorm eps 1e-5 (nn.LayerNorm default)."""
+
+    def __init__(self, input_resolution=224, patch_size=16, width=768, layers=12, heads=12, output_dim=512,
+                 state_dict=None, device="cuda"):
+        if width % heads or width // heads != 64:
+            raise ValueError("VisionTransformer: librr's fused attention needs head_dim == 64")
+        if state_dict is None:
+            raise ValueError("VisionTransformer needs a state_dict (no pretrained download offline)")
+        self.device = torch.device(device)
+        self.res, self.patch, self.width, self.layers, self.heads = input_resolution, patch_size, width, layers, heads
+        self.output_dim = self.outputdim = output_dim
+        self.seq = (input_resolution // patch_size) ** 2 + 1
+        if self.seq > 256:
+            raise ValueError("VisionTransformer: sequence longer than 256 tokens")
+        t = lambda k: state_dict[k].float().contiguous().to(self.device)  # noqa: E731
+        # patch conv [width, 3, p, p] -> [width][p][p][3] to match patchify's (kh, kw, c) rows
+        self.conv_w = state_dict["conv1.weight"].float().permute(0, 2, 3, 1).reshape(width, -1).contiguous().to(
+            self.device)
+        self.cls = t("class_embedding")
+        self.pos = t("positional_embedding")
+        self.ln_pre = (t("ln_pre.weight"), t("ln_pre.bias"))
+        self.blocks = []
+        for i in range(layers):
+            p = f"transformer.resblocks.{i}."
+            self.blocks.append({k: t(p + k) for k in (
+                "attn.in_proj_weight", "attn.in_proj_bias", "attn.out_proj.weight", "attn.out_proj.bias",
+                "ln_1.weight", "ln_1.bias", "mlp.c_fc.weight", "mlp.c_fc.bias", "mlp.c_proj.weight",
+                "mlp.c_proj.bias", "ln_2.weight", "ln_2.bias")})
+        self.ln_post = (t("ln_post.weight"), t("ln_post.bias"))
+        self.proj_t = state_dict["proj"].float().t().contiguous().to(self.device)  # [out, width]
+
+    def forward_nhwc(self, x_nhwc):
+        b, h, w, _ = x_nhwc.shape
+        if h != self.res or w != self.res:
+            raise ValueError(f"VisionTransformer: fixed {self.res}x{self.res} input (positional embedding has "
+                             f"{self.seq} tokens; networks/model.py:228)")
+        x = ops.linear(ops.patchify(x_nhwc, self.patch), self.conv_w)
+        x = ops.vit_tokens(x, b, self.cls, self.pos)
+        x = ops.layernorm(x, *self.ln_pre)
+        for blk in self.blocks:
+            y = ops.layernorm(x, blk["ln_1.weight"], blk["ln_1.bias"])
+            qkv = ops.linear(y, blk["attn.in_proj_weight"], blk["attn.in_proj_bias"])
+            a = ops.attention(qkv, b, self.seq, self.heads)
+            x = ops.linear_ex(a, blk["attn.out_proj.weight"], blk["attn.out_proj.bias"], residual=x)
+            y = ops.layernorm(x, blk["ln_2.weight"], blk["ln_2.bias"])
+            y = ops.linear_ex(y, blk["mlp.c_fc.weight"], blk["mlp.c_fc.bias"], act=2)
+            x = ops.linear_ex(y, blk["mlp.c_proj.weight"], blk["mlp.c_proj.bias"], residual=x)
+        cls = ops.layernorm(x, *self.ln_post, rows=b, row_stride=self.seq * self.width)
+        return ops.linear(cls, self.proj_t)
+
+    @torch.no_grad()
+    def forward(self, x):
+        return self.forward_nhwc(self._input(x))
+
+    __call__ = forward
+
+    def forward_test_nhwc(self, x_nhwc):
+        f = self.forward_nhwc(x_nhwc)
+        return ops.l2_normalize(f, EPS_L2, out=f)

@@ -220,3 +220,68 @@ class KernelTimer:
         _lib.check(_lib.lib().rr_timing_collect(self.h, cls, ctypes.byref(ms), ctypes.byref(n)), self.h,
                    "rr_timing_collect")
         return ms.value, n.value
+
+
+def linear_ex(x, w, bias=None, residual=None, act=0):
+    """y = act(x @ w.T + bias + residual); act 0 none, 1 ReLU, 2 QuickGELU."""
+    _f32(x, "linear_ex x")
+    _f32(w, "linear_ex w")
+    dev = _dev(x)
+    m, k = x.shape
+    n = w.shape[0]
+    y = torch.empty((m, n), dtype=torch.float32, device=x.device)
+    if residual is not None:
+        _f32(residual, "linear_ex residual")
+        if tuple(residual.shape) != (m, n):
+            raise ValueError("linear_ex: residual shape mismatch")
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_linear_ex(hd, _ptr(x), m, k, _ptr(w), _ptr(bias), n, _ptr(residual), int(act), _ptr(y),
+                                       _stream(dev)), hd, "rr_linear_ex")
+    return y
+
+
+def layernorm(x, gamma, beta, eps=1e-5, rows=None, row_stride=None):
+    """LayerNorm over the last dim of x [..., D]; with rows/row_stride, LN of
+    ``rows`` rows spaced ``row_stride`` floats apart (e.g. the CLS tokens)."""
+    _f32(x, "layernorm")
+    dev = _dev(x)
+    d = x.shape[-1]
+    m = x.numel() // d if rows is None else int(rows)
+    ld = d if row_stride is None else int(row_stride)
+    y = torch.empty((m, d), dtype=torch.float32, device=x.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_layernorm(hd, _ptr(x), ld, m, d, _ptr(gamma), _ptr(beta), float(eps), _ptr(y),
+                                       _stream(dev)), hd, "rr_layernorm")
+    return y
+
+
+def patchify(x_nhwc, patch):
+    _f32(x_nhwc, "patchify")
+    dev = _dev(x_nhwc)
+    b, h, w, c = x_nhwc.shape
+    y = torch.empty((b * (h // patch) * (w // patch), patch * patch * c), dtype=torch.float32, device=x_nhwc.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_patchify(hd, _ptr(x_nhwc), b, h, w, c, patch, _ptr(y), _stream(dev)), hd, "rr_patchify")
+    return y
+
+
+def vit_tokens(patches, b, cls, pos):
+    _f32(patches, "vit_tokens")
+    dev = _dev(patches)
+    width = patches.shape[1]
+    npatch = patches.shape[0] // b
+    y = torch.empty((b * (npatch + 1), width), dtype=torch.float32, device=patches.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_vit_tokens(hd, _ptr(patches), b, npatch, width, _ptr(cls), _ptr(pos), _ptr(y),
+                                        _stream(dev)), hd, "rr_vit_tokens")
+    return y
+
+
+def attention(qkv, b, seq, heads, head_dim=64):
+    _f32(qkv, "attention")
+    dev = _dev(qkv)
+    out = torch.empty((b * seq, heads * head_dim), dtype=torch.float32, device=qkv.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_attention(hd, _ptr(qkv), b, seq, heads, head_dim, _ptr(out), _stream(dev)), hd,
+               "rr_attention")
+    return out

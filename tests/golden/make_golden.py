@@ -127,7 +127,7 @@ def main():
 
     # (vii) CLIP ViT (networks/model.py:206-243): tiny config and ViT-B/16, seeded weights
     out = {}
-    for tag, cfg in {"tiny": dict(res=32, patch=8, width=64, layers=2, heads=4, out_dim=32, seed=51),
+    for tag, cfg in {"tiny": dict(res=32, patch=8, width=128, layers=2, heads=2, out_dim=32, seed=51),
                      "b16": dict(res=224, patch=16, width=768, layers=12, heads=12, out_dim=512, seed=52)}.items():
         vit = VisionTransformer(cfg["res"], cfg["patch"], cfg["width"], cfg["layers"], cfg["heads"], cfg["out_dim"])
         sd = I.vit_state_dict(cfg["seed"], cfg["width"], cfg["layers"], cfg["heads"], cfg["patch"], cfg["res"],

@@ -1,0 +1,63 @@
+"""GPU parity of the ViT extractor (networks.VisionTransformer on librr)
+against the reference's own VisionTransformer outputs (golden fixture) and the
+oracle's functional restatement."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import embed_ref
+from research_image_retrieval_amd import ops
+from research_image_retrieval_amd.networks import VisionTransformer
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+sys.path.insert(0, GOLD)
+import inputs as I  # noqa: E402
+
+
+@pytest.mark.parametrize("tag", ["tiny", "b16"])
+def test_vit_vs_reference_fixture(cuda, tag):
+    fx = np.load(os.path.join(GOLD, "vit.npz"))
+    res, patch, width, layers, heads, out_dim, seed = (int(v) for v in fx[tag + "_cfg"])
+    sd = I.vit_state_dict(seed, width, layers, heads, patch, res, out_dim)
+    net = VisionTransformer(res, patch, width, layers, heads, out_dim, state_dict=sd, device=cuda)
+    rsx = np.random.RandomState(seed + 100)
+    x = torch.from_numpy(rsx.standard_normal((2, 3, res, res)).astype(np.float32))
+    got = net(x.to(cuda)).cpu().numpy()
+    ref = fx[tag]
+    err = np.abs(got - ref).max() / max(1.0, np.abs(ref).max())
+    print(tag, "rel max err", err)
+    assert err < 2e-4
+    d = net.forward_test(x.to(cuda)).cpu().numpy()
+    np.testing.assert_allclose(np.linalg.norm(d, axis=1), 1.0, rtol=1e-5)
+
+
+@pytest.mark.parametrize("seq", [17, 197, 256, 40])
+def test_attention_kernel_vs_torch(cuda, seq):
+    b, heads = 3, 2
+    g = torch.Generator().manual_seed(seq)
+    qkv = torch.randn(b * seq, 3 * heads * 64, generator=g)
+    out = ops.attention(qkv.to(cuda), b, seq, heads).cpu()
+    q, k, v = qkv.view(b, seq, 3, heads, 64).permute(2, 0, 3, 1, 4).double()
+    ref = torch.softmax(q @ k.transpose(-2, -1) / 8.0, dim=-1) @ v
+    ref = ref.permute(0, 2, 1, 3).reshape(b * seq, heads * 64).float()
+    torch.testing.assert_close(out, ref, rtol=1e-5, atol=1e-5)
+
+
+def test_layernorm_and_quickgelu(cuda):
+    x = torch.randn(37, 768)
+    w, bb = torch.randn(768), torch.randn(768)
+    ref = torch.nn.functional.layer_norm(x.double(), (768,), w.double(), bb.double(), 1e-5).float()
+    torch.testing.assert_close(ops.layernorm(x.to(cuda), w.to(cuda), bb.to(cuda)).cpu(), ref, rtol=1e-5, atol=1e-5)
+    cls = ops.layernorm(x.to(cuda), w.to(cuda), bb.to(cuda), rows=3, row_stride=12 * 768).cpu()
+    torch.testing.assert_close(cls, ref[::12][:3], rtol=1e-5, atol=1e-5)
+    a = torch.randn(19, 64)
+    wt = torch.randn(96, 64) * 0.1
+    b2 = torch.randn(96)
+    z = torch.nn.functional.linear(a.double(), wt.double(), b2.double())
+    refg = (z * torch.sigmoid(1.702 * z)).float()
+    torch.testing.assert_close(ops.linear_ex(a.to(cuda), wt.to(cuda), b2.to(cuda), act=2).cpu(), refg,
+                               rtol=1e-5, atol=1e-5)

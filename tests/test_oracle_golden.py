@@ -134,3 +134,16 @@ def test_oracle_merge_and_topk_rows_consistent():
     ms, mi = oracle.topk_merge(np.stack([p0s, p1s]), np.stack([p0i, p1i]), 50)
     np.testing.assert_array_equal(mi, ti)
     np.testing.assert_array_equal(ms, ts)
+
+
+@pytest.mark.parametrize("tag", ["tiny", "b16"])
+def test_oracle_vit_vs_reference(tag):
+    fx = load("vit")
+    res, patch, width, layers, heads, out_dim, seed = (int(v) for v in fx[tag + "_cfg"])
+    sd = I.vit_state_dict(seed, width, layers, heads, patch, res, out_dim)
+    rsx = np.random.RandomState(seed + 100)
+    x = torch.from_numpy(rsx.standard_normal((2, 3, res, res)).astype(np.float32))
+    with torch.no_grad():
+        out = embed_ref.vit_forward(x, sd, patch, width, layers, heads).numpy()
+    ref = fx[tag]
+    assert np.abs(out - ref).max() < 1e-4 * max(1.0, np.abs(ref).max())
