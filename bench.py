@@ -32,7 +32,7 @@ sys.path.insert(0, ROOT)
 from research_image_retrieval_amd import _lib, ops  # noqa: E402
 from research_image_retrieval_amd import weights as W  # noqa: E402
 from research_image_retrieval_amd.distributed import ShardedGallery, shard_bounds  # noqa: E402
-from research_image_retrieval_amd.networks import GeM, ConvDimReduction, GeMPCAw  # noqa: E402
+from research_image_retrieval_amd.networks import GeM, ConvDimReduction, GeMPCAw, VisionTransformer  # noqa: E402
 
 METRIC = "images embedded+ranked/sec on 1.6M×2048 gallery; mAP on ROxf/RPar"
 PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
@@ -145,23 +145,51 @@ def main():
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--arch", default="resnet101")
+    ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
+                    help="c3: ResNet101-GeM 2048-d + PCA-w (BASELINE metric config); "
+                         "c4: ViT-B/16 CLS 512-d (fp32 here; bf16 is the next row)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
+    if a.workload == "c4":
+        if a.dim == 2048:
+            a.dim = 512
+        a.arch = "vit_b16"
 
+    if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # started bare with --gpus N: run ourselves under torch.distributed.run
+        # as a child (nothing has touched the GPU yet in this process)
+        import socket
+        import subprocess
+        sock = socket.socket()
+        sock.bind(("127.0.0.1", 0))
+        port = sock.getsockname()[1]
+        sock.close()
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={a.gpus}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+        sys.exit(subprocess.run(cmd).returncode)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         log(f"note: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    # one process per GPU; ranks beyond the visible devices share them (rehearsal)
+    dev = torch.device("cuda", local % torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        backend = os.environ.get("RR_DIST_BACKEND", "nccl")  # "gloo" only for 1-GPU rehearsals
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
 
     t_setup = time.time()
     lo, hi = shard_bounds(a.gallery, world, rank)
     gallery = make_gallery(a.gallery, a.dim, lo, hi, dev)
-    net = build_extractor(a.arch, dev)
+    if a.workload == "c4":
+        net = VisionTransformer(224, 16, 768, 12, 12, a.dim,
+                                state_dict=W.synthetic_vit_state_dict(out_dim=a.dim, seed=0), device=dev)
+    else:
+        net = build_extractor(a.arch, dev)
     rs = np.random.RandomState(1234 + rank)
     imgs = torch.from_numpy(rs.randint(0, 256, size=(a.batch, 224, 224, 3), dtype=np.uint8)).to(dev)
     q_total = a.batch * world
@@ -183,7 +211,7 @@ def main():
     chk_s, chk_i = ops.cosine_topk(gallery[:2].contiguous(), gallery, 1, idx_offset=lo, workspace=ws)
     assert chk_i[:, 0].tolist() == [lo, lo + 1], chk_i
 
-    timer = ops.KernelTimer(local)
+    timer = ops.KernelTimer(dev.index)
     timer.enable(True)
     if world > 1:
         dist.barrier()
@@ -197,10 +225,12 @@ def main():
     elapsed = time.perf_counter() - t0
     cls = {name: timer.collect(c) for name, c in (("cosine_filter", _lib.TIME_COSINE), ("conv_gemm", _lib.TIME_GEMM),
                                                    ("select", _lib.TIME_SELECT), ("elementwise", _lib.TIME_ELEM),
-                                                   ("cosine_seed", _lib.TIME_COSINE_SEED))}
+                                                   ("cosine_seed", _lib.TIME_COSINE_SEED),
+                                                   ("attention", _lib.TIME_ATTN))}
     timer.enable(False)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64,
+                         device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = world * a.batch * a.steps / elapsed
@@ -209,11 +239,15 @@ def main():
     s_rows = min(hi - lo, max(32768, a.k))
     flop_filter = 2.0 * q_total * max(0, (hi - lo) - s_rows) * a.dim  # per filter launch (one per step)
     flop_seed = 2.0 * q_total * s_rows * a.dim
-    conv_flops_img = sum(W.resnet_conv_flops(a.arch, 224, 224).values()) + 2 * 2 * 2048 * 2048  # + whiten + PCA-w
+    attn_flops_img = 0
+    if a.workload == "c4":
+        conv_flops_img, attn_flops_img = W.vit_flops(out_dim=a.dim)
+    else:
+        conv_flops_img = sum(W.resnet_conv_flops(a.arch, 224, 224).values()) + 2 * 2 * 2048 * 2048  # + whiten, PCA-w
     traffic = load_traffic()
     rk = {}
     for name, fl in (("cosine_filter", flop_filter * a.steps), ("conv_gemm", conv_flops_img * a.batch * a.steps),
-                     ("cosine_seed", flop_seed * a.steps)):
+                     ("cosine_seed", flop_seed * a.steps), ("attention", attn_flops_img * a.batch * a.steps)):
         ms, n = cls[name]
         if n == 0 or ms <= 0:
             continue
@@ -234,12 +268,14 @@ def main():
            "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
            "data": "synthetic: uint8 224x224x3 images RandomState(1234+rank); seeded Gaussian L2-normalised "
                    "gallery; seeded ResNet/whiten/PCA-w weights (no pretrained weights offline)",
-           "config": {"workload": f"C3: {a.arch}-GeM 2048-d + PCA-whiten, embed + exact top-{a.k} against a "
-                                  f"{a.gallery}x{a.dim} gallery", "global_batch": q_total,
+           "config": {"workload": (f"C3: {a.arch}-GeM 2048-d + PCA-whiten" if a.workload == "c3" else
+                                   f"C4 (fp32): ViT-B/16 CLS {a.dim}-d") +
+                                  f", embed + exact top-{a.k} against a {a.gallery}x{a.dim} gallery",
+                      "global_batch": q_total,
                       "images_per_gpu_per_step": a.batch, "gallery_rows": a.gallery, "dim": a.dim, "k": a.k,
                       "parallelism": f"query-dp{world} + gallery-shard{world}"},
            "roofline": roof, "roofline_by_kernel": rk}
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+    if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "c3":
         t = time.time()
         res["cpu_baseline"] = cpu_baseline(a.arch, a.gallery, a.dim, a.k)
         log(f"cpu baseline {time.time() - t:.1f}s")

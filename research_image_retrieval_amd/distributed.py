@@ -31,9 +31,19 @@ def shard_bounds(n, world, rank):
     return lo, lo + base + (1 if rank < extra else 0)
 
 
+def _host_staged(group):
+    """gloo has no all_gather / all_to_all for device tensors: rehearsal runs
+    of the sharded path (several ranks on one GPU, gloo transport) stage the
+    collectives through host memory.  RCCL ("nccl") moves device tensors."""
+    return dist.get_backend(group) == "gloo"
+
+
 def _all_gather_var(t, group):
     """all_gather of tensors whose first dim may differ across ranks."""
     world = dist.get_world_size(group)
+    dev = t.device
+    if _host_staged(group):
+        t = t.cpu()
     n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
     sizes = [torch.zeros_like(n) for _ in range(world)]
     dist.all_gather(sizes, n, group=group)
@@ -43,7 +53,7 @@ def _all_gather_var(t, group):
     pad[: t.shape[0]] = t
     outs = [torch.empty_like(pad) for _ in range(world)]
     dist.all_gather(outs, pad, group=group)
-    return [o[:s] for o, s in zip(outs, sizes)], sizes
+    return [o[:s].to(dev) for o, s in zip(outs, sizes)], sizes
 
 
 class ShardedGallery:
@@ -81,8 +91,12 @@ class ShardedGallery:
         # each rank needs only its own queries' partial lists: all-to-all
         # (B_r * W * k * 12 bytes in per rank instead of Q * W * k * 12)
         mine = sizes[rank]
+        dev = s.device
+        if _host_staged(group):
+            s, i = s.cpu(), i.cpu()
         rs = s.new_empty((world * mine, k))
         ri = i.new_empty((world * mine, k))
         dist.all_to_all_single(rs, s.contiguous(), [mine] * world, sizes, group=group)
         dist.all_to_all_single(ri, i.contiguous(), [mine] * world, sizes, group=group)
+        rs, ri = rs.to(dev), ri.to(dev)
         return self._merge_parts(rs.view(world, mine, k).contiguous(), ri.view(world, mine, k).contiguous(), k)

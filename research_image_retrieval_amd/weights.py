@@ -170,3 +170,40 @@ def resnet_conv_flops(arch, h, w):
             flops[p + ".conv3"] = 2 * Ho * Wo * planes * 4 * planes
             H, Wd, inplanes = Ho, Wo, planes * 4
     return flops
+
+
+def synthetic_vit_state_dict(width=768, layers=12, heads=12, patch=16, res=224, out_dim=512, seed=0):
+    """Seeded CLIP-layout ViT weights (networks/model.py:206-243 key names)."""
+    rs = np.random.RandomState(seed)
+    sc = width ** -0.5
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))  # noqa: E731
+    sd = collections.OrderedDict()
+    sd["conv1.weight"] = t(rs.standard_normal((width, 3, patch, patch)) / np.sqrt(3 * patch * patch))
+    sd["class_embedding"] = t(rs.standard_normal(width) * sc)
+    sd["positional_embedding"] = t(rs.standard_normal(((res // patch) ** 2 + 1, width)) * sc)
+    sd["ln_pre.weight"], sd["ln_pre.bias"] = t(np.ones(width)), t(np.zeros(width))
+    for i in range(layers):
+        p = f"transformer.resblocks.{i}."
+        sd[p + "attn.in_proj_weight"] = t(rs.standard_normal((3 * width, width)) * sc)
+        sd[p + "attn.in_proj_bias"] = t(np.zeros(3 * width))
+        sd[p + "attn.out_proj.weight"] = t(rs.standard_normal((width, width)) * sc)
+        sd[p + "attn.out_proj.bias"] = t(np.zeros(width))
+        sd[p + "ln_1.weight"], sd[p + "ln_1.bias"] = t(np.ones(width)), t(np.zeros(width))
+        sd[p + "mlp.c_fc.weight"] = t(rs.standard_normal((4 * width, width)) * sc)
+        sd[p + "mlp.c_fc.bias"] = t(np.zeros(4 * width))
+        sd[p + "mlp.c_proj.weight"] = t(rs.standard_normal((width, 4 * width)) * (0.5 / np.sqrt(4 * width)))
+        sd[p + "mlp.c_proj.bias"] = t(np.zeros(width))
+        sd[p + "ln_2.weight"], sd[p + "ln_2.bias"] = t(np.ones(width)), t(np.zeros(width))
+    sd["ln_post.weight"], sd["ln_post.bias"] = t(np.ones(width)), t(np.zeros(width))
+    sd["proj"] = t(rs.standard_normal((width, out_dim)) * sc)
+    return sd
+
+
+def vit_flops(width=768, layers=12, heads=12, patch=16, res=224, out_dim=512):
+    """Algorithmic FLOPs per image: (GEMM FLOPs, attention FLOPs)."""
+    L = (res // patch) ** 2 + 1
+    gemm = 2 * (L - 1) * width * 3 * patch * patch
+    gemm += layers * 2 * L * width * (3 * width + width + 4 * width + 4 * width)
+    gemm += 2 * width * out_dim
+    attn = layers * heads * 2 * (2 * L * L * (width // heads))
+    return gemm, attn
