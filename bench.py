@@ -210,6 +210,9 @@ def main():
     # sanity: a gallery row used as a query must come back first
     chk_s, chk_i = ops.cosine_topk(gallery[:2].contiguous(), gallery, 1, idx_offset=lo, workspace=ws)
     assert chk_i[:, 0].tolist() == [lo, lo + 1], chk_i
+    if sharded is not None:  # the full sharded path: all-gather -> shard top-k -> all-to-all -> merge
+        ss, si = sharded.search(gallery[:2].contiguous(), a.k)
+        assert si[:, 0].tolist() == [lo, lo + 1], si[:, :3]
 
     timer = ops.KernelTimer(dev.index)
     timer.enable(True)
