@@ -290,16 +290,32 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
         }
     __syncthreads();
     constexpr int C4 = BN / 4;
+    constexpr int ITERS = BM * C4 / NT;
+    static_assert(ITERS * NT == BM * C4, "epilogue tiling");
     const bool vec_ok = ((g.N & 3) == 0) && ((g.ldc & 3) == 0);
-    for (int idx = tid; idx < BM * C4; idx += NT) {
-      const int row = idx / C4, c4 = idx - row * C4;
-      const int m = m0 + row, n = n0 + c4 * 4;
-      if (m >= g.M || n >= g.N) continue;
-      f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
-      const long long o = (long long)m * g.ldc + n;
-      if (vec_ok) {
+    if (vec_ok) {
+      // all residual loads in flight before the first use (one HBM round trip
+      // per tile instead of one per row group)
+      f32x4 res[ITERS];
+      if (g.residual != nullptr) {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+          const int idx = tid + it * NT;
+          const int row = idx / C4, c4 = idx - row * C4;
+          const int m = m0 + row, n = n0 + c4 * 4;
+          if (m < g.M && n < g.N)
+            res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int idx = tid + it * NT;
+        const int row = idx / C4, c4 = idx - row * C4;
+        const int m = m0 + row, n = n0 + c4 * 4;
+        if (m >= g.M || n >= g.N) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
         if (g.bias != nullptr) v += *reinterpret_cast<const f32x4*>(g.bias + n);
-        if (g.residual != nullptr) v += *reinterpret_cast<const f32x4*>(g.residual + o);
+        if (g.residual != nullptr) v += res[it];
         if (g.relu == 1) {
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -307,8 +323,15 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
 #pragma unroll
           for (int e = 0; e < 4; ++e) v[e] = quick_gelu(v[e]);
         }
-        *reinterpret_cast<f32x4*>(g.C + o) = v;
-      } else {
+        *reinterpret_cast<f32x4*>(g.C + (long long)m * g.ldc + n) = v;
+      }
+    } else {
+      for (int idx = tid; idx < BM * C4; idx += NT) {
+        const int row = idx / C4, c4 = idx - row * C4;
+        const int m = m0 + row, n = n0 + c4 * 4;
+        if (m >= g.M || n >= g.N) continue;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
+        const long long o = (long long)m * g.ldc + n;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           if (n + e >= g.N) break;
