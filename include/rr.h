@@ -100,9 +100,18 @@ int rr_preprocess_u8(rr_handle_t h, const uint8_t* img_nhwc, int b, int hgt,
                      int wid, const float* mean3, const float* std3,
                      float* out_nhwc, void* stream);
 
+/* Same with out_c in {3, 4}: out_c == 4 writes NHWC4 pixels with a zero
+ * 4th channel, the stem conv's 16-byte tap layout (see rr_conv2d).          */
+int rr_preprocess_u8_ex(rr_handle_t h, const uint8_t* img_nhwc, int b, int hgt,
+                        int wid, const float* mean3, const float* std3,
+                        int out_c, float* out_nhwc, void* stream);
+
 /* fp32 NCHW -> NHWC relayout (the reference's forward_test input is NCHW). */
 int rr_nchw_to_nhwc(rr_handle_t h, const float* in, int b, int c, int hgt,
                     int wid, float* out, void* stream);
+/* Same, zero-padding the channel dim to out_c >= c.                       */
+int rr_nchw_to_nhwc_ex(rr_handle_t h, const float* in, int b, int c, int hgt,
+                       int wid, int out_c, float* out, void* stream);
 
 /* 2-D convolution, NHWC, implicit GEMM on fp32 MFMA with a fused epilogue:
  * y = relu?( conv(x, w) + bias[co] + residual? ).  Weights [cout][kh][kw][cin]
@@ -110,7 +119,10 @@ int rr_nchw_to_nhwc(rr_handle_t h, const float* in, int b, int c, int hgt,
  * Replaces the torchvision ResNet conv/BN/ReLU/residual ops behind
  * networks/backbone.py:103-109 and models/gem_pooling.py:44,61.
  * residual may be NULL; output is [b][oh][ow][cout].
- * Constraints: cin % 4 == 0 or cin < 32 (generic gather path).             */
+ * A-operand paths: 1x1/s1 = dense rows; cin % 32 == 0 = im2col with one
+ * filter tap per 32-deep k-tile; cin == 4 = one tap per float4 (the stem on
+ * NHWC4 input, zero 4th channel and zero 4th weight channel); other cin =
+ * per-element gather.                                                      */
 int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin,
               const float* w, const float* bias, int cout, int kh, int kw,
               int stride, int pad, const float* residual, int relu, float* y,

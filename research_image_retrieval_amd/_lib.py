@@ -43,6 +43,8 @@ SIGNATURES = {
     "rr_topk_merge": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
     "rr_preprocess_u8": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
     "rr_nchw_to_nhwc": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "rr_preprocess_u8_ex": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp]),
+    "rr_nchw_to_nhwc_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "rr_conv2d": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
     "rr_resize_bilinear": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _f, _f, _vp, _vp]),
     "rr_maxpool2d": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
@@ -79,6 +81,8 @@ def lib():
                     "(there is deliberately no CPU/eager fallback)")
             L = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in SIGNATURES.items():
+                if os.environ.get("RR_LIB_PATH") and not hasattr(L, name):
+                    continue  # A/B against an older build: bind what it has
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args

@@ -9,27 +9,36 @@ namespace rr {
 // (x/255 - mean[c]) / std[c]; same op order and IEEE division as
 // torchvision ToTensor().div(255) + Normalize().sub_(mean).div_(std)
 // (dataset/configdataset.py:417,430-436).
+// out_c == 4 appends a zero channel (16-B pixels for the stem conv's tap loads).
 __global__ void preprocess_u8_kernel(const uint8_t* __restrict__ in, long long n_px, float m0, float m1, float m2,
-                                     float s0, float s1, float s2, float* __restrict__ out) {
+                                     float s0, float s1, float s2, int out_c, float* __restrict__ out) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long p = (long long)blockIdx.x * blockDim.x + threadIdx.x; p < n_px; p += stride) {
     const uint8_t* px = in + p * 3;
-    float* o = out + p * 3;
-    o[0] = ((float)px[0] / 255.0f - m0) / s0;
-    o[1] = ((float)px[1] / 255.0f - m1) / s1;
-    o[2] = ((float)px[2] / 255.0f - m2) / s2;
+    const float r = ((float)px[0] / 255.0f - m0) / s0;
+    const float g = ((float)px[1] / 255.0f - m1) / s1;
+    const float b = ((float)px[2] / 255.0f - m2) / s2;
+    if (out_c == 4) {
+      *reinterpret_cast<float4*>(out + p * 4) = make_float4(r, g, b, 0.f);
+    } else {
+      float* o = out + p * 3;
+      o[0] = r;
+      o[1] = g;
+      o[2] = b;
+    }
   }
 }
 
-__global__ void nchw_to_nhwc_kernel(const float* __restrict__ in, int C, long long HW, long long total,
+// out[b][hw][c'] = in[b][c'][hw] for c' < C, 0 for C <= c' < CO (channel pad)
+__global__ void nchw_to_nhwc_kernel(const float* __restrict__ in, int C, int CO, long long HW, long long total,
                                     float* __restrict__ out) {
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += stride) {
-    const int c = (int)(o % C);
-    const long long t = o / C;
+    const int c = (int)(o % CO);
+    const long long t = o / CO;
     const long long hw = t % HW;
     const long long b = t / HW;
-    out[o] = in[(b * C + c) * HW + hw];
+    out[o] = c < C ? in[(b * C + c) * HW + hw] : 0.f;
   }
 }
 
@@ -57,6 +66,37 @@ __global__ void resize_bilinear_kernel(const float* __restrict__ x, int B, int H
     const float v00 = xb[((long long)h0 * W + w0) * C], v01 = xb[((long long)h0 * W + w1) * C];
     const float v10 = xb[((long long)h1 * W + w0) * C], v11 = xb[((long long)h1 * W + w1) * C];
     y[o] = (v00 * lw0 + v01 * lw1) * lh0 + (v10 * lw0 + v11 * lw1) * lh1;
+  }
+}
+
+// max pool, NHWC, 4 channels per thread (C % 4 == 0); padding taps are -inf.
+__global__ void maxpool4_kernel(const float* __restrict__ x, int B, int H, int W, int C, int k, int stride, int pad,
+                                int OH, int OW, float* __restrict__ y) {
+  const int C4 = C >> 2;
+  const long long total = (long long)B * OH * OW * C4;
+  const long long gstride = (long long)gridDim.x * blockDim.x;
+  for (long long o = (long long)blockIdx.x * blockDim.x + threadIdx.x; o < total; o += gstride) {
+    const int c4 = (int)(o % C4);
+    long long t = o / C4;
+    const int ow = (int)(t % OW);
+    t /= OW;
+    const int oh = (int)(t % OH);
+    const int b = (int)(t / OH);
+    float4 m = make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff());
+    for (int dh = 0; dh < k; ++dh) {
+      const int ih = oh * stride - pad + dh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      for (int dw = 0; dw < k; ++dw) {
+        const int iw = ow * stride - pad + dw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const float4 v = *reinterpret_cast<const float4*>(x + (((long long)b * H + ih) * W + iw) * C + c4 * 4);
+        m.x = fmaxf(m.x, v.x);
+        m.y = fmaxf(m.y, v.y);
+        m.z = fmaxf(m.z, v.z);
+        m.w = fmaxf(m.w, v.w);
+      }
+    }
+    *reinterpret_cast<float4*>(y + o * 4) = m;
   }
 }
 
@@ -136,28 +176,40 @@ using namespace rr;
 
 extern "C" int rr_preprocess_u8(rr_handle_t h, const uint8_t* img, int b, int hgt, int wid, const float* mean3,
                                 const float* std3, float* out, void* stream) {
+  return rr_preprocess_u8_ex(h, img, b, hgt, wid, mean3, std3, 3, out, stream);
+}
+
+extern "C" int rr_preprocess_u8_ex(rr_handle_t h, const uint8_t* img, int b, int hgt, int wid, const float* mean3,
+                                   const float* std3, int out_c, float* out, void* stream) {
   if (!h) return RR_EINVAL;
-  if (!img || !out || !mean3 || !std3 || b < 0 || hgt < 0 || wid < 0)
-    return set_error(h, RR_EINVAL, "rr_preprocess_u8: bad argument");
+  if (!img || !out || !mean3 || !std3 || b < 0 || hgt < 0 || wid < 0 || (out_c != 3 && out_c != 4) ||
+      (out_c == 4 && ((uintptr_t)out & 15)))
+    return set_error(h, RR_EINVAL, "rr_preprocess_u8: bad argument (out_c 3 or 4, 16-B aligned out)");
   const long long npx = (long long)b * hgt * wid;
   if (npx == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeElem, s);
   hipLaunchKernelGGL(preprocess_u8_kernel, grid_for(npx, 256), dim3(256), 0, s, img, npx, mean3[0], mean3[1],
-                     mean3[2], std3[0], std3[1], std3[2], out);
+                     mean3[2], std3[0], std3[1], std3[2], out_c, out);
   return check_hip(h, hipGetLastError(), "preprocess launch");
 }
 
 extern "C" int rr_nchw_to_nhwc(rr_handle_t h, const float* in, int b, int c, int hgt, int wid, float* out,
                                void* stream) {
+  return rr_nchw_to_nhwc_ex(h, in, b, c, hgt, wid, c, out, stream);
+}
+
+extern "C" int rr_nchw_to_nhwc_ex(rr_handle_t h, const float* in, int b, int c, int hgt, int wid, int out_c,
+                                  float* out, void* stream) {
   if (!h) return RR_EINVAL;
-  if (!in || !out || b < 0 || c <= 0 || hgt < 0 || wid < 0) return set_error(h, RR_EINVAL, "rr_nchw_to_nhwc: bad argument");
-  const long long total = (long long)b * c * hgt * wid;
+  if (!in || !out || b < 0 || c <= 0 || hgt < 0 || wid < 0 || out_c < c)
+    return set_error(h, RR_EINVAL, "rr_nchw_to_nhwc: bad argument");
+  const long long total = (long long)b * out_c * hgt * wid;
   if (total == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeElem, s);
-  hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid_for(total, 256), dim3(256), 0, s, in, c, (long long)hgt * wid, total,
-                     out);
+  hipLaunchKernelGGL(nchw_to_nhwc_kernel, grid_for(total, 256), dim3(256), 0, s, in, c, out_c, (long long)hgt * wid,
+                     total, out);
   return check_hip(h, hipGetLastError(), "nchw_to_nhwc launch");
 }
 
@@ -172,8 +224,12 @@ extern "C" int rr_maxpool2d(rr_handle_t h, const float* x, int b, int hgt, int w
   if (total == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeElem, s);
-  hipLaunchKernelGGL(maxpool_kernel, grid_for(total, 256), dim3(256), 0, s, x, b, hgt, wid, c, k, stride, pad, oh, ow,
-                     y);
+  if ((c & 3) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0)
+    hipLaunchKernelGGL(maxpool4_kernel, grid_for(total / 4, 256), dim3(256), 0, s, x, b, hgt, wid, c, k, stride, pad,
+                       oh, ow, y);
+  else
+    hipLaunchKernelGGL(maxpool_kernel, grid_for(total, 256), dim3(256), 0, s, x, b, hgt, wid, c, k, stride, pad, oh,
+                       ow, y);
   return check_hip(h, hipGetLastError(), "maxpool launch");
 }
 

@@ -126,8 +126,19 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
         ra[i] = ok ? *reinterpret_cast<const f32x4*>(a_ptr[i] + ((long long)ih * g.W + iw) * g.Cin + cin0 + slot * 4)
                    : f32x4{0.f, 0.f, 0.f, 0.f};
       }
+    } else if constexpr (AMODE == A_CONV_C4) {
+      // Cin == 4 (RGB + zero pad channel): each float4 is one filter tap
+      const int tap = k >> 2;
+      const int kh = tap / g.KW;
+      const int kw = tap - kh * g.KW;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+        const bool ok = a_ok[i] && kok && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        ra[i] = ok ? *reinterpret_cast<const f32x4*>(a_ptr[i] + ((long long)ih * g.W + iw) * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
     } else {
-      // generic gather (small / odd Cin, e.g. the 7x7 stem with Cin = 3)
+      // generic gather (small / odd Cin)
       const int kwc = g.KW * g.Cin;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
@@ -401,6 +412,7 @@ int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStre
     else if (amode == A_DENSE && emode == E_FILTER) e = launch_cfg<A_DENSE, E_FILTER>(g, s);
     else if (amode == A_CONV && emode == E_STORE) e = launch_cfg<A_CONV, E_STORE>(g, s);
     else if (amode == A_CONV_GENERIC && emode == E_STORE) e = launch_cfg<A_CONV_GENERIC, E_STORE>(g, s);
+    else if (amode == A_CONV_C4 && emode == E_STORE) e = launch_cfg<A_CONV_C4, E_STORE>(g, s);
     else return set_error(h, RR_EINVAL, "gemm: unsupported mode combination");
   }
   return check_hip(h, e, "gemm launch");

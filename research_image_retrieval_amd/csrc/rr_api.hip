@@ -273,6 +273,8 @@ int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, c
     g.lda = cin;
   } else if (cin % 32 == 0) {
     amode = A_CONV;
+  } else if (cin == 4) {
+    amode = A_CONV_C4;
   } else {
     amode = A_CONV_GENERIC;
   }

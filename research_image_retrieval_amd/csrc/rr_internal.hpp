@@ -67,7 +67,7 @@ __host__ __device__ inline float key_score(unsigned long long k) {
 }
 
 // ---- GEMM core launchers (gemm_f32.hip) ---------------------------------
-enum AMode { A_DENSE = 0, A_CONV = 1, A_CONV_GENERIC = 2 };
+enum AMode { A_DENSE = 0, A_CONV = 1, A_CONV_GENERIC = 2, A_CONV_C4 = 3 };
 enum EMode { E_STORE = 0, E_SCORES_T = 1, E_FILTER = 2 };
 
 struct GemmArgs {

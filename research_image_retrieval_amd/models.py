@@ -31,6 +31,8 @@ class GeMModel(_Extractor):
     """resnet trunk -> GeMPooling -> feature_proj Linear(2048, feature_dim)
     (models/gem_pooling.py:26-92); extract_descriptor adds F.normalize(p=2, dim=1)."""
 
+    in_channels = 4
+
     def __init__(self, backbone="resnet50", pretrained=False, num_classes=1000, feature_dim=2048, gem_p=3.0,
                  state_dict=None, seed=0, device="cuda"):
         if pretrained:
@@ -88,6 +90,8 @@ def _from_sd(sd, name):
 
 class GeMWrapper(_Extractor):
     """models/gem_pooling.py:95-119: training-loop facade over GeMModel."""
+
+    in_channels = 4
 
     def __init__(self, num_classes, backbone="resnet50", feature_dim=2048, gem_p=3.0, **kw):
         self.backbone = GeMModel(backbone=backbone, num_classes=num_classes, feature_dim=feature_dim, gem_p=gem_p,

@@ -32,6 +32,9 @@ class ResNet:
         sd = W.synthetic_resnet_state_dict(name, seed) if state_dict is None else W.to_torchvision_keys(state_dict)
         self.device = torch.device(device)
         folded = W.folded_resnet(sd, name)
+        # stem weights padded to 4 input channels (zero) for the NHWC4 tap path
+        w1, b1 = folded["conv1"]
+        folded["conv1"] = (torch.nn.functional.pad(w1, (0, 1)).contiguous(), b1)
         self.convs = {k: (w.to(self.device), b.to(self.device)) for k, (w, b) in folded.items()}
         self.layers = W.RESNET_LAYERS[name]
 
@@ -40,6 +43,9 @@ class ResNet:
         return ops.conv2d(x, w, b, stride, pad, residual, relu)
 
     def forward(self, x):
+        """x: NHWC fp32 with 3 channels or 4 (zero 4th channel, preferred)."""
+        if x.shape[-1] == 3:
+            x = torch.nn.functional.pad(x, (0, 1))
         x = self._conv(x, "conv1", 2, 3, True)
         x = ops.maxpool2d(x, 3, 2, 1)
         for li, nb in enumerate(self.layers):
@@ -78,11 +84,13 @@ class _Extractor:
     def to(self, *_a, **_k):
         return self
 
+    in_channels = 3  # NHWC channel count the first layer consumes (4 = RGB + zero pad)
+
     def _input(self, x):
         if not isinstance(x, torch.Tensor) or not x.is_cuda:
             raise ValueError("forward_test expects a float32 [B,3,H,W] tensor on a ROCm device")
         x = x.float() if x.dtype != torch.float32 else x
-        return ops.nchw_to_nhwc(x.contiguous())
+        return ops.nchw_to_nhwc(x.contiguous(), out_c=self.in_channels)
 
     def forward_test_nhwc(self, x_nhwc):
         raise NotImplementedError
@@ -95,7 +103,7 @@ class _Extractor:
     def forward_test_u8(self, img_nhwc_u8):
         """uint8 [B,H,W,3] pixels -> descriptors, with ToTensor+Normalize fused
         into the first kernel (dataset/configdataset.py:417)."""
-        return self.forward_test_nhwc(ops.preprocess_u8(img_nhwc_u8))
+        return self.forward_test_nhwc(ops.preprocess_u8(img_nhwc_u8, out_c=self.in_channels))
 
 
 class GeM(_Extractor):
@@ -104,6 +112,8 @@ class GeM(_Extractor):
 
     As in the reference, the whitening conv takes ``outputdim`` input channels,
     so the network is only well-formed for outputdim == 2048 (:332)."""
+
+    in_channels = 4
 
     def __init__(self, outputdim=2048, backbone="resnet101", state_dict=None, whiten=None, seed=0, device="cuda"):
         if outputdim != 2048:
@@ -184,6 +194,7 @@ class GeMPCAw(_Extractor):
     whiten -> normalise."""
 
     def __init__(self, net, pcaw):
+        self.in_channels = net.in_channels
         self.net = net
         self.pcaw = pcaw
         self.outputdim = pcaw.dim

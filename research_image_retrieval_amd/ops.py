@@ -35,30 +35,33 @@ def _f32(t, name):
     return t
 
 
-def preprocess_u8(img_nhwc, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225)):
-    """uint8 [B,H,W,3] -> fp32 NHWC normalised (ToTensor + Normalize)."""
+def preprocess_u8(img_nhwc, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225), out_c=3):
+    """uint8 [B,H,W,3] -> fp32 NHWC normalised (ToTensor + Normalize); out_c=4
+    appends a zero channel (stem-conv tap layout)."""
     if img_nhwc.dtype != torch.uint8 or img_nhwc.dim() != 4 or img_nhwc.shape[3] != 3:
         raise ValueError("preprocess_u8: expected uint8 [B,H,W,3]")
     img_nhwc = img_nhwc.contiguous()
     dev = _dev(img_nhwc)
     b, h, w, _ = img_nhwc.shape
-    out = torch.empty((b, h, w, 3), dtype=torch.float32, device=img_nhwc.device)
+    out = torch.empty((b, h, w, out_c), dtype=torch.float32, device=img_nhwc.device)
     m = (ctypes.c_float * 3)(*mean)
     s = (ctypes.c_float * 3)(*std)
     hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_preprocess_u8(hd, _ptr(img_nhwc), b, h, w, ctypes.cast(m, ctypes.c_void_p),
-                                           ctypes.cast(s, ctypes.c_void_p), _ptr(out), _stream(dev)), hd,
-               "rr_preprocess_u8")
+    _lib.check(_lib.lib().rr_preprocess_u8_ex(hd, _ptr(img_nhwc), b, h, w, ctypes.cast(m, ctypes.c_void_p),
+                                              ctypes.cast(s, ctypes.c_void_p), int(out_c), _ptr(out), _stream(dev)),
+               hd, "rr_preprocess_u8")
     return out
 
 
-def nchw_to_nhwc(x):
+def nchw_to_nhwc(x, out_c=None):
     x = _f32(x.contiguous(), "nchw_to_nhwc")
     dev = _dev(x)
     b, c, h, w = x.shape
-    out = torch.empty((b, h, w, c), dtype=torch.float32, device=x.device)
+    oc = c if out_c is None else int(out_c)
+    out = torch.empty((b, h, w, oc), dtype=torch.float32, device=x.device)
     hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_nchw_to_nhwc(hd, _ptr(x), b, c, h, w, _ptr(out), _stream(dev)), hd, "rr_nchw_to_nhwc")
+    _lib.check(_lib.lib().rr_nchw_to_nhwc_ex(hd, _ptr(x), b, c, h, w, oc, _ptr(out), _stream(dev)), hd,
+               "rr_nchw_to_nhwc")
     return out
 
 

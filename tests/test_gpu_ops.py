@@ -29,6 +29,8 @@ def _conv_ref(x_nhwc, w_okkc, b, stride, pad, res=None, relu=False):
     (3, 7, 7, 512, 2048, 1, 1, 0, True, True),
     (2, 16, 16, 256, 512, 1, 2, 0, False, False),
     (2, 33, 35, 3, 64, 7, 2, 3, False, True),     # stem (generic gather)
+    (2, 33, 35, 4, 64, 7, 2, 3, False, True),     # stem on NHWC4 (one tap per float4)
+    (3, 224, 224, 4, 64, 7, 2, 3, False, True),   # full-size stem
     (1, 9, 9, 64, 96, 1, 1, 0, False, False),
 ])
 def test_conv2d(cuda, b, h, w, cin, cout, k, s, p, res, relu):
@@ -83,3 +85,19 @@ def test_preprocess_bitexact(cuda):
 def test_nchw_to_nhwc(cuda):
     x = torch.randn(2, 3, 11, 13)
     assert torch.equal(ops.nchw_to_nhwc(x.to(cuda)).cpu(), x.permute(0, 2, 3, 1))
+    y4 = ops.nchw_to_nhwc(x.to(cuda), out_c=4).cpu()
+    assert torch.equal(y4[..., :3], x.permute(0, 2, 3, 1)) and (y4[..., 3] == 0).all()
+
+
+def test_preprocess_pad4(cuda):
+    rng = np.random.RandomState(7)
+    t = torch.from_numpy(rng.randint(0, 256, size=(2, 9, 7, 3), dtype=np.uint8)).to(cuda)
+    a = ops.preprocess_u8(t).cpu()
+    b = ops.preprocess_u8(t, out_c=4).cpu()
+    assert torch.equal(b[..., :3], a) and (b[..., 3] == 0).all()
+
+
+def test_maxpool_scalar_path(cuda):
+    x = torch.randn(2, 9, 8, 6)  # C % 4 != 0 -> scalar kernel
+    ref = F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
+    assert torch.equal(ops.maxpool2d(x.to(cuda), 3, 2, 1).cpu(), ref)

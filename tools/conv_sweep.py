@@ -17,7 +17,7 @@ def conv_launches(arch, b, h=224, w=224):
     out = lambda x, k, s, p: (x + 2 * p - k) // s + 1  # noqa: E731
     L = collections.Counter()
     H, Wd = h, w
-    L[(b, H, Wd, 3, 64, 7, 2, 3, False, True)] += 1
+    L[(b, H, Wd, 4, 64, 7, 2, 3, False, True)] += 1  # stem on NHWC4
     H, Wd = out(out(H, 7, 2, 3), 3, 2, 1), out(out(Wd, 7, 2, 3), 3, 2, 1)
     inpl = 64
     for li, nb in enumerate(W.RESNET_LAYERS[arch]):
