@@ -33,22 +33,30 @@ namespace rr {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int BK = 32;
-
-__device__ __forceinline__ int swz(int row, int slot) { return slot ^ ((row >> 1) & 7); }
+// 16-byte-slot XOR swizzle of a [rows][BK] fp32 LDS image, conflict-free for
+// the fragment ds_read_b128 (16 lanes = 16 rows distinct mod 16, one slot):
+// BK = 32 (8 slots per 128-B row): slot ^ ((row >> 1) & 7);
+// BK = 16 (4 slots per 64-B row):  slot ^ ((row >> 2) & 3).
+template <int BK>
+__device__ __forceinline__ int swz(int row, int slot) {
+  if constexpr (BK == 32) return slot ^ ((row >> 1) & 7);
+  else return slot ^ ((row >> 2) & 3);
+}
 
 // QuickGELU, x * sigmoid(1.702 x) (networks/model.py:166-168)
 __device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f + expf(-(1.702f * x)))); }
 
-template <int WM, int WN, int AMODE, int EMODE>
-__global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int tiles_n) {
+// BK = 32: 64 KB LDS per 128x128 block, 2 blocks (2 waves/SIMD) per CU.
+// BK = 16: 32 KB, 3 blocks (3 waves/SIMD) per CU, twice the barriers.
+template <int WM, int WN, int AMODE, int EMODE, int BK>
+__global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(GemmArgs g, int tiles_n) {
   constexpr int NT = 64 * WM * WN;
   constexpr int BM = 64 * WM, BN = 64 * WN;
-  constexpr int ROWS_PER_PASS = NT / 8;
+  constexpr int SLOTS = BK / 4;
+  constexpr int ROWS_PER_PASS = NT / SLOTS;
   constexpr int A_CH = BM / ROWS_PER_PASS;
   constexpr int B_CH = BN / ROWS_PER_PASS;
   static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for block");
-  static_assert(BM * BN <= 2 * (BM + BN) * 32, "C tile must fit the LDS staging buffers");
   constexpr int BUF = (BM + BN) * BK;  // floats per LDS buffer
   __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
 
@@ -64,8 +72,8 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
   const int tn = wgid % tiles_n, tm = wgid / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
 
-  const int slot = tid & 7;
-  const int crow = tid >> 3;
+  const int slot = tid % SLOTS;
+  const int crow = tid / SLOTS;
   const int K = g.K;
   const int nk = (K + BK - 1) / BK;
 
@@ -183,12 +191,12 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       const int row = crow + i * ROWS_PER_PASS;
-      *reinterpret_cast<f32x4*>(la + row * BK + swz(row, slot) * 4) = ra[i];
+      *reinterpret_cast<f32x4*>(la + row * BK + swz<BK>(row, slot) * 4) = ra[i];
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
       const int row = crow + i * ROWS_PER_PASS;
-      *reinterpret_cast<f32x4*>(lb + row * BK + swz(row, slot) * 4) = rb[i];
+      *reinterpret_cast<f32x4*>(lb + row * BK + swz<BK>(row, slot) * 4) = rb[i];
     }
   };
 
@@ -212,20 +220,20 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
     const float* la = lds + cur * BUF;
     const float* lb = la + BM * BK;
 #pragma unroll
-    for (int c2 = 0; c2 < 2; ++c2) {
+    for (int c2 = 0; c2 < BK / 16; ++c2) {
       f32x4 af[2][2], bf[2][2];
       const int s0 = c2 * 4 + 2 * lh;
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
         const int row = wm * 64 + i * 32 + lr;
-        af[i][0] = *reinterpret_cast<const f32x4*>(la + row * BK + swz(row, s0) * 4);
-        af[i][1] = *reinterpret_cast<const f32x4*>(la + row * BK + swz(row, s0 + 1) * 4);
+        af[i][0] = *reinterpret_cast<const f32x4*>(la + row * BK + swz<BK>(row, s0) * 4);
+        af[i][1] = *reinterpret_cast<const f32x4*>(la + row * BK + swz<BK>(row, s0 + 1) * 4);
       }
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int row = wn * 64 + j * 32 + lr;
-        bf[j][0] = *reinterpret_cast<const f32x4*>(lb + row * BK + swz(row, s0) * 4);
-        bf[j][1] = *reinterpret_cast<const f32x4*>(lb + row * BK + swz(row, s0 + 1) * 4);
+        bf[j][0] = *reinterpret_cast<const f32x4*>(lb + row * BK + swz<BK>(row, s0) * 4);
+        bf[j][1] = *reinterpret_cast<const f32x4*>(lb + row * BK + swz<BK>(row, s0 + 1) * 4);
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
@@ -287,78 +295,90 @@ __global__ __launch_bounds__(64 * WM * WN, 2) void gemm_kernel(GemmArgs g, int t
   if constexpr (EMODE == E_STORE) {
     // Stage the BMxBN accumulator tile through LDS (free after the last
     // barrier of the k-loop), then write whole rows: each lane moves 16 B,
-    // 32 lanes cover a 512-B row run, residual read the same way.
-    float* ct = lds;  // [BM][BN] row-major (BM*BN <= 2*BUF floats)
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-          const int col = wn * 64 + j * 32 + lr;
-          ct[row * BN + col] = acc[i][j][r];
-        }
-    __syncthreads();
+    // 32 lanes cover a 512-B row run, residual read the same way.  When the
+    // tile exceeds the LDS image (BK = 16) it goes in P row slabs.
+    constexpr int CAP = 2 * BUF;
+    constexpr int P = (BM * BN + CAP - 1) / CAP;
+    static_assert(WM % P == 0, "row slabs must align with wave rows");
+    constexpr int SLAB = BM / P;
     constexpr int C4 = BN / 4;
-    constexpr int ITERS = BM * C4 / NT;
-    static_assert(ITERS * NT == BM * C4, "epilogue tiling");
+    constexpr int ITERS = SLAB * C4 / NT;
+    static_assert(ITERS * NT == SLAB * C4, "epilogue tiling");
+    float* ct = lds;  // [SLAB][BN] row-major
     const bool vec_ok = ((g.N & 3) == 0) && ((g.ldc & 3) == 0);
-    if (vec_ok) {
-      // all residual loads in flight before the first use (one HBM round trip
-      // per tile instead of one per row group)
-      f32x4 res[ITERS];
-      if (g.residual != nullptr) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      if (p > 0) __syncthreads();
+      if (wm / (WM / P) == p) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh - p * SLAB;
+              const int col = wn * 64 + j * 32 + lr;
+              ct[row * BN + col] = acc[i][j][r];
+            }
+      }
+      __syncthreads();
+      const int rbase = p * SLAB;
+      if (vec_ok) {
+        // all residual loads in flight before the first use (one HBM round
+        // trip per slab instead of one per row group)
+        f32x4 res[ITERS];
+        if (g.residual != nullptr) {
+#pragma unroll
+          for (int it = 0; it < ITERS; ++it) {
+            const int idx = tid + it * NT;
+            const int row = idx / C4, c4 = idx - row * C4;
+            const int m = m0 + rbase + row, n = n0 + c4 * 4;
+            if (m < g.M && n < g.N)
+              res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
+          }
+        }
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
           const int idx = tid + it * NT;
           const int row = idx / C4, c4 = idx - row * C4;
-          const int m = m0 + row, n = n0 + c4 * 4;
-          if (m < g.M && n < g.N)
-            res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
+          const int m = m0 + rbase + row, n = n0 + c4 * 4;
+          if (m >= g.M || n >= g.N) continue;
+          f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
+          if (g.bias != nullptr) v += *reinterpret_cast<const f32x4*>(g.bias + n);
+          if (g.residual != nullptr) v += res[it];
+          if (g.relu == 1) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+          } else if (g.relu == 2) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = quick_gelu(v[e]);
+          }
+          *reinterpret_cast<f32x4*>(g.C + (long long)m * g.ldc + n) = v;
         }
-      }
+      } else {
+        for (int idx = tid; idx < SLAB * C4; idx += NT) {
+          const int row = idx / C4, c4 = idx - row * C4;
+          const int m = m0 + rbase + row, n = n0 + c4 * 4;
+          if (m >= g.M || n >= g.N) continue;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
+          const long long o = (long long)m * g.ldc + n;
 #pragma unroll
-      for (int it = 0; it < ITERS; ++it) {
-        const int idx = tid + it * NT;
-        const int row = idx / C4, c4 = idx - row * C4;
-        const int m = m0 + row, n = n0 + c4 * 4;
-        if (m >= g.M || n >= g.N) continue;
-        f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
-        if (g.bias != nullptr) v += *reinterpret_cast<const f32x4*>(g.bias + n);
-        if (g.residual != nullptr) v += res[it];
-        if (g.relu == 1) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        } else if (g.relu == 2) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = quick_gelu(v[e]);
-        }
-        *reinterpret_cast<f32x4*>(g.C + (long long)m * g.ldc + n) = v;
-      }
-    } else {
-      for (int idx = tid; idx < BM * C4; idx += NT) {
-        const int row = idx / C4, c4 = idx - row * C4;
-        const int m = m0 + row, n = n0 + c4 * 4;
-        if (m >= g.M || n >= g.N) continue;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
-        const long long o = (long long)m * g.ldc + n;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (n + e >= g.N) break;
-          float x = v[e];
-          if (g.bias != nullptr) x += g.bias[n + e];
-          if (g.residual != nullptr) x += g.residual[o + e];
-          if (g.relu == 1) x = fmaxf(x, 0.f);
-          else if (g.relu == 2) x = quick_gelu(x);
-          g.C[o + e] = x;
+          for (int e = 0; e < 4; ++e) {
+            if (n + e >= g.N) break;
+            float x = v[e];
+            if (g.bias != nullptr) x += g.bias[n + e];
+            if (g.residual != nullptr) x += g.residual[o + e];
+            if (g.relu == 1) x = fmaxf(x, 0.f);
+            else if (g.relu == 2) x = quick_gelu(x);
+            g.C[o + e] = x;
+          }
         }
       }
     }
   }
 }
 
-template <int WM, int WN, int AM, int EM>
+template <int WM, int WN, int AM, int EM, int BK>
 static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   const long long tiles_m = (g.M + BM - 1) / BM;
@@ -366,9 +386,21 @@ static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, AM, EM>), dim3((unsigned)nblk), dim3(64 * WM * WN), 0, s, g,
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, AM, EM, BK>), dim3((unsigned)nblk), dim3(64 * WM * WN), 0, s, g,
                      (int)tiles_n);
   return hipGetLastError();
+}
+
+// k-tile depth.  Measured on MI355X (same device, interleaved A/B): BK = 16
+// (3 blocks per CU) is +2.5 % on the long-K, huge-grid cosine GEMM, BK = 32
+// (2 blocks per CU) is +4.8 % on the ResNet convs.  RR_GEMM_BK=16|32 forces.
+static int pick_bk(int emode) {
+  static const int forced = [] {
+    const char* e = getenv("RR_GEMM_BK");
+    return e ? atoi(e) : 0;
+  }();
+  if (forced == 16 || forced == 32) return forced;
+  return emode == E_STORE ? 32 : 16;
 }
 
 // Tile choice: both configs run 4 waves and 2 workgroups per CU (512 slots
@@ -376,13 +408,13 @@ static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
 // 512): this charges both the padding of N (e.g. 320 queries on 128-wide
 // tiles) and the last partially-filled round (wave quantization).
 // RR_GEMM_CFG=22|41 forces a config (tuning experiments).
-static int pick_cfg(const GemmArgs& g) {
+static int pick_cfg(const GemmArgs& g, int emode) {
   static const int forced = [] {
     const char* e = getenv("RR_GEMM_CFG");
     return e ? atoi(e) : 0;
   }();
   if (forced == 22 || forced == 41) return forced;
-  const long long slots = 512;
+  const long long slots = pick_bk(emode) == 16 ? 768 : 512;
   const long long t22 = ((g.M + 127) / 128) * ((g.N + 127) / 128);
   const long long t41 = ((g.M + 255) / 256) * ((g.N + 63) / 64);
   const long long c22 = ((t22 + slots - 1) / slots) * 128 * 128;
@@ -392,8 +424,13 @@ static int pick_cfg(const GemmArgs& g) {
 
 template <int AM, int EM>
 static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
-  if (pick_cfg(g) == 41) return launch_t<4, 1, AM, EM>(g, s);
-  return launch_t<2, 2, AM, EM>(g, s);
+  const int cfg = pick_cfg(g, EM);
+  if (pick_bk(EM) == 16) {
+    if (cfg == 41) return launch_t<4, 1, AM, EM, 16>(g, s);
+    return launch_t<2, 2, AM, EM, 16>(g, s);
+  }
+  if (cfg == 41) return launch_t<4, 1, AM, EM, 32>(g, s);
+  return launch_t<2, 2, AM, EM, 32>(g, s);
 }
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStream_t s, int timer_cls) {
@@ -402,7 +439,7 @@ int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStre
   if (amode == A_DENSE && (g.lda & 3)) return set_error(h, RR_EINVAL, "gemm: lda must be a multiple of 4");
   if (amode != A_CONV_GENERIC && (g.ldb & 3) != 0) return set_error(h, RR_EINVAL, "gemm: ldb must be a multiple of 4");
   if (emode == E_SCORES_T && (g.ldc & 3)) return set_error(h, RR_EINVAL, "gemm: ldc must be a multiple of 4");
-  if (amode == A_CONV && (g.Cin % BK) != 0) return set_error(h, RR_EINVAL, "gemm: A_CONV needs Cin % 32 == 0");
+  if (amode == A_CONV && (g.Cin % 32) != 0) return set_error(h, RR_EINVAL, "gemm: A_CONV needs Cin % 32 == 0");
   if (g.M == 0 || g.N == 0) return RR_OK;
   hipError_t e = hipSuccess;
   {
