@@ -92,6 +92,23 @@ int rr_topk_merge(rr_handle_t h, const float* part_scores,
                   int k_out, float* out_scores, long long* out_idx,
                   void* stream);
 
+/* ---- low-precision search (configs C4 bf16, C5 fp8) ---------------------
+ * dtype: 1 = bf16 (RNE), 2 = fp8 OCP e4m3 with one fp32 scale per row.
+ * rr_quantize_rows: x [rows][d] fp32 -> y [rows][d] (2 or 1 bytes/elem);
+ * fp8 writes row_scale[r] = amax(row)/448 (x ~= q * scale).              */
+int rr_quantize_rows(rr_handle_t h, const float* x, long long rows, int d,
+                     int dtype, void* y, float* row_scale, void* stream);
+
+/* rr_cosine_topk on bf16 / fp8 rows (fp32 accumulate, scores dequantised
+ * by q_scale[i] * g_scale[j] when given; required for fp8).  Same workspace
+ * and output contract as rr_cosine_topk; scores are the low-precision
+ * ones, so parity vs fp32 is recall@k, not index equality.  d*size % 16 == 0. */
+int rr_cosine_topk_lp(rr_handle_t h, const void* queries, const float* q_scale,
+                      int nq, const void* gallery, const float* g_scale,
+                      long long n, int d, int dtype, int k, long long idx_offset,
+                      float* out_scores, long long* out_idx, void* workspace,
+                      size_t workspace_bytes, void* stream);
+
 /* ---- embed (extractor) ---------------------------------------------------
  * uint8 HWC pixels -> fp32 NHWC, (x/255 - mean[c]) / std[c].
  * Replaces transforms.ToTensor + Normalize(mean=[.485,.456,.406],
@@ -162,6 +179,12 @@ int rr_linear_ex(rr_handle_t h, const float* x, int m, int k, const float* w,
                  const float* bias, int n, const float* residual, int act,
                  float* y, void* stream);
 
+/* bf16 x [m][k] . bf16 w [n][k]^T, fp32 accumulate, fp32 bias / residual,
+ * act as rr_linear_ex; y fp32 or (out_bf16) bf16.  The C4 (ViT bf16) GEMMs. */
+int rr_linear_bf16(rr_handle_t h, const void* x, int m, int k, const void* w,
+                   const float* bias, int n, const float* residual, int act,
+                   int out_bf16, void* y, void* stream);
+
 /* ---- ViT-B/16 (networks/model.py:206-243) ------------------------------ */
 /* LayerNorm over the last dim (fp32, biased variance), rows x + i*ldx ->
  * dense y [m][d].  Replaces LayerNorm (:157-163): ln_pre, ln_1, ln_2, and
@@ -169,6 +192,11 @@ int rr_linear_ex(rr_handle_t h, const float* x, int m, int k, const float* w,
 int rr_layernorm(rr_handle_t h, const float* x, long long ldx, int m, int d,
                  const float* gamma, const float* beta, float eps, float* y,
                  void* stream);
+
+/* Same, output dtype 0 = fp32, 1 = bf16 (feeds rr_linear_bf16).           */
+int rr_layernorm_ex(rr_handle_t h, const float* x, long long ldx, int m, int d,
+                    const float* gamma, const float* beta, float eps,
+                    int out_dtype, void* y, void* stream);
 
 /* NHWC image -> non-overlapping patch rows [b*(H/p)*(W/p)][p*p*c], (kh,kw,c)
  * order: with weights [width][p][p][c] the patch conv (:223, stride = kernel
@@ -189,6 +217,9 @@ int rr_vit_tokens(rr_handle_t h, const float* patches, int b, int npatch,
  * CU.                                                                      */
 int rr_attention(rr_handle_t h, const float* qkv, int b, int seq, int heads,
                  int head_dim, float* out, void* stream);
+/* Same, output dtype 0 = fp32, 1 = bf16.                                   */
+int rr_attention_ex(rr_handle_t h, const float* qkv, int b, int seq, int heads,
+                    int head_dim, int out_dtype, void* out, void* stream);
 
 /* Row-wise L2 normalisation x / max(||x||_2, eps), in place allowed.
  * Replaces F.normalize (networks/RetrievalNet.py:343, models/gem_pooling.py:91,

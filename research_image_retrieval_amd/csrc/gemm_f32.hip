@@ -32,6 +32,15 @@ namespace rr {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// input element type of A/B: DT_F32 (v_mfma_f32_32x32x2_f32), DT_BF16
+// (v_mfma_f32_32x32x16_bf16), DT_FP8 (OCP e4m3, v_mfma_f32_32x32x16_fp8_fp8).
+// LDS rows are 128 B for all three (32 fp32 / 64 bf16 / 128 fp8 per k-tile),
+// so staging, swizzle and epilogues are shared.
+template <int DT> struct ElemT { using T = float; };
+template <> struct ElemT<DT_BF16> { using T = uint16_t; };
+template <> struct ElemT<DT_FP8> { using T = uint8_t; };
 
 // 16-byte-slot XOR swizzle of a [rows][BK] fp32 LDS image, conflict-free for
 // the fragment ds_read_b128 (16 lanes = 16 rows distinct mod 16, one slot):
@@ -48,8 +57,13 @@ __device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f 
 
 // BK = 32: 64 KB LDS per 128x128 block, 2 blocks (2 waves/SIMD) per CU.
 // BK = 16: 32 KB, 3 blocks (3 waves/SIMD) per CU, twice the barriers.
-template <int WM, int WN, int AMODE, int EMODE, int BK>
+template <int WM, int WN, int AMODE, int EMODE, int BK, int DT>
 __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(GemmArgs g, int tiles_n) {
+  using ET = typename ElemT<DT>::T;
+  static_assert(DT == DT_F32 || (AMODE == A_DENSE && BK == 32), "low-precision GEMM: dense A, 128-B rows");
+  constexpr int ES = (int)sizeof(ET);
+  constexpr int EPR = BK * 4 / ES;  // elements per LDS row (= k per k-tile)
+  constexpr int CH = 16 / ES;       // elements per 16-byte staging chunk
   constexpr int NT = 64 * WM * WN;
   constexpr int BM = 64 * WM, BN = 64 * WN;
   constexpr int SLOTS = BK / 4;
@@ -75,10 +89,10 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
   const int slot = tid % SLOTS;
   const int crow = tid / SLOTS;
   const int K = g.K;
-  const int nk = (K + BK - 1) / BK;
+  const int nk = (K + EPR - 1) / EPR;
 
   // ---- per-chunk A row state ----
-  const float* a_ptr[A_CH];
+  const ET* a_ptr[A_CH];
   int a_ih0[A_CH], a_iw0[A_CH];
   bool a_ok[A_CH];
 #pragma unroll
@@ -86,7 +100,7 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
     const int m = m0 + crow + i * ROWS_PER_PASS;
     a_ok[i] = m < g.M;
     if constexpr (AMODE == A_DENSE) {
-      a_ptr[i] = g.A + (long long)(a_ok[i] ? m : 0) * g.lda;
+      a_ptr[i] = reinterpret_cast<const ET*>(g.A) + (long long)(a_ok[i] ? m : 0) * g.lda;
       a_ih0[i] = 0;
       a_iw0[i] = 0;
     } else {
@@ -96,24 +110,24 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
       const int rem = mm - b * ohw;
       const int oh = rem / g.OW;
       const int ow = rem - oh * g.OW;
-      a_ptr[i] = g.A + (long long)b * g.H * g.W * g.Cin;
+      a_ptr[i] = reinterpret_cast<const ET*>(g.A) + (long long)b * g.H * g.W * g.Cin;
       a_ih0[i] = oh * g.stride - g.pad;
       a_iw0[i] = ow * g.stride - g.pad;
     }
   }
-  const float* b_ptr[B_CH];
+  const ET* b_ptr[B_CH];
   bool b_ok[B_CH];
 #pragma unroll
   for (int i = 0; i < B_CH; ++i) {
     const int n = n0 + crow + i * ROWS_PER_PASS;
     b_ok[i] = n < g.N;
-    b_ptr[i] = g.B + (long long)(b_ok[i] ? n : 0) * g.ldb;
+    b_ptr[i] = reinterpret_cast<const ET*>(g.B) + (long long)(b_ok[i] ? n : 0) * g.ldb;
   }
 
   f32x4 ra[A_CH], rb[B_CH];
 
   auto load_tile = [&](int kt) {
-    const int k = kt * BK + slot * 4;
+    const int k = kt * EPR + slot * CH;
     const bool kok = k < K;
     if constexpr (AMODE == A_DENSE) {
 #pragma unroll
@@ -219,6 +233,7 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
     if (kt + 1 < nk) load_tile(kt + 1);
     const float* la = lds + cur * BUF;
     const float* lb = la + BM * BK;
+    if constexpr (DT == DT_F32) {
 #pragma unroll
     for (int c2 = 0; c2 < BK / 16; ++c2) {
       f32x4 af[2][2], bf[2][2];
@@ -245,12 +260,70 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
                                                              acc[i][j], 0, 0, 0);
       }
     }
+    } else if constexpr (DT == DT_BF16) {
+      // 4 k-steps of 16; lane half h holds k = 16s + 8h .. +7 = 16-B slot 2s + h
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        bf16x8 af[2], bf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = wm * 64 + i * 32 + lr;
+          af[i] = *reinterpret_cast<const bf16x8*>(la + row * BK + swz<BK>(row, 2 * st + lh) * 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = wn * 64 + j * 32 + lr;
+          bf[j] = *reinterpret_cast<const bf16x8*>(lb + row * BK + swz<BK>(row, 2 * st + lh) * 4);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    } else {
+      // fp8: 8 k-steps of 16; lane half h holds bytes 8h..8h+7 of 16-B slot s
+#pragma unroll
+      for (int st = 0; st < 8; ++st) {
+        long af[2], bf[2];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const int row = wm * 64 + i * 32 + lr;
+          af[i] = *reinterpret_cast<const long*>(la + row * BK + swz<BK>(row, st) * 4 + 2 * lh);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          const int row = wn * 64 + j * 32 + lr;
+          bf[j] = *reinterpret_cast<const long*>(lb + row * BK + swz<BK>(row, st) * 4 + 2 * lh);
+        }
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(af[i], bf[j], acc[i][j], 0, 0, 0);
+      }
+    }
     if (kt + 1 < nk) store_tile(cur ^ 1);
     __syncthreads();
   }
 
   // ---- epilogue ----
   // 32x32 C/D map: col (N index) = lane & 31, row (M index) = (r&3) + 8(r>>2) + 4(lane>>5)
+  if (g.scale_a != nullptr || g.scale_b != nullptr) {  // per-row dequantisation (fp8)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n = n0 + wn * 64 + j * 32 + lr;
+      const float sb = (g.scale_b != nullptr && n < g.N) ? g.scale_b[n] : 1.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const float sa = (g.scale_a != nullptr && m < g.M) ? g.scale_a[m] : 1.f;
+          acc[i][j][r] = acc[i][j][r] * sa * sb;
+        }
+    }
+  }
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     const int n = n0 + wn * 64 + j * 32 + lr;
@@ -353,7 +426,13 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
 #pragma unroll
             for (int e = 0; e < 4; ++e) v[e] = quick_gelu(v[e]);
           }
-          *reinterpret_cast<f32x4*>(g.C + (long long)m * g.ldc + n) = v;
+          if (g.out_bf16) {
+            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+            const bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+            *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(g.C) + (long long)m * g.ldc + n) = o;
+          } else {
+            *reinterpret_cast<f32x4*>(g.C + (long long)m * g.ldc + n) = v;
+          }
         }
       } else {
         for (int idx = tid; idx < SLAB * C4; idx += NT) {
@@ -370,7 +449,12 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
             if (g.residual != nullptr) x += g.residual[o + e];
             if (g.relu == 1) x = fmaxf(x, 0.f);
             else if (g.relu == 2) x = quick_gelu(x);
-            g.C[o + e] = x;
+            if (g.out_bf16) {
+              const __bf16 xb = (__bf16)x;
+              reinterpret_cast<__bf16*>(g.C)[o + e] = xb;
+            } else {
+              g.C[o + e] = x;
+            }
           }
         }
       }
@@ -378,7 +462,7 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
   }
 }
 
-template <int WM, int WN, int AM, int EM, int BK>
+template <int WM, int WN, int AM, int EM, int BK, int DT>
 static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 64 * WM, BN = 64 * WN;
   const long long tiles_m = (g.M + BM - 1) / BM;
@@ -386,7 +470,7 @@ static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, AM, EM, BK>), dim3((unsigned)nblk), dim3(64 * WM * WN), 0, s, g,
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, AM, EM, BK, DT>), dim3((unsigned)nblk), dim3(64 * WM * WN), 0, s, g,
                      (int)tiles_n);
   return hipGetLastError();
 }
@@ -426,15 +510,47 @@ template <int AM, int EM>
 static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
   const int cfg = pick_cfg(g, EM);
   if (pick_bk(EM) == 16) {
-    if (cfg == 41) return launch_t<4, 1, AM, EM, 16>(g, s);
-    return launch_t<2, 2, AM, EM, 16>(g, s);
+    if (cfg == 41) return launch_t<4, 1, AM, EM, 16, DT_F32>(g, s);
+    return launch_t<2, 2, AM, EM, 16, DT_F32>(g, s);
   }
-  if (cfg == 41) return launch_t<4, 1, AM, EM, 32>(g, s);
-  return launch_t<2, 2, AM, EM, 32>(g, s);
+  if (cfg == 41) return launch_t<4, 1, AM, EM, 32, DT_F32>(g, s);
+  return launch_t<2, 2, AM, EM, 32, DT_F32>(g, s);
 }
 
-int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStream_t s, int timer_cls) {
+// low-precision (dense A only, 128-B LDS rows, 2 blocks per CU)
+template <int EM, int DT>
+static hipError_t launch_lp(const GemmArgs& g, hipStream_t s) {
+  const long long t22 = ((g.M + 127) / 128) * ((g.N + 127) / 128);
+  const long long t41 = ((g.M + 255) / 256) * ((g.N + 63) / 64);
+  const long long c22 = ((t22 + 511) / 512) * 128 * 128, c41 = ((t41 + 511) / 512) * 256 * 64;
+  if (c41 < c22) return launch_t<4, 1, A_DENSE, EM, 32, DT>(g, s);
+  return launch_t<2, 2, A_DENSE, EM, 32, DT>(g, s);
+}
+
+int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStream_t s, int timer_cls, int dt) {
   if (g.M < 0 || g.N < 0 || g.K <= 0) return set_error(h, RR_EINVAL, "gemm: bad shape");
+  if (dt != DT_F32) {
+    const int vec = dt == DT_BF16 ? 8 : 16;  // elements per 16-B staging load
+    if (amode != A_DENSE) return set_error(h, RR_EINVAL, "gemm: low-precision GEMM needs dense A");
+    if ((g.K % vec) || (g.lda % vec) || (g.ldb % vec))
+      return set_error(h, RR_EINVAL, "gemm: low-precision K / lda / ldb must be multiples of 16 bytes");
+    if (emode == E_SCORES_T && (g.ldc & 3)) return set_error(h, RR_EINVAL, "gemm: ldc must be a multiple of 4");
+    if (g.M == 0 || g.N == 0) return RR_OK;
+    hipError_t e = hipSuccess;
+    {
+      TimedLaunch tl(h, timer_cls, s);
+      if (dt == DT_BF16) {
+        if (emode == E_STORE) e = launch_lp<E_STORE, DT_BF16>(g, s);
+        else if (emode == E_SCORES_T) e = launch_lp<E_SCORES_T, DT_BF16>(g, s);
+        else e = launch_lp<E_FILTER, DT_BF16>(g, s);
+      } else {
+        if (emode == E_STORE) e = launch_lp<E_STORE, DT_FP8>(g, s);
+        else if (emode == E_SCORES_T) e = launch_lp<E_SCORES_T, DT_FP8>(g, s);
+        else e = launch_lp<E_FILTER, DT_FP8>(g, s);
+      }
+    }
+    return check_hip(h, e, "gemm launch");
+  }
   if (amode != A_CONV_GENERIC && (g.K & 3) != 0) return set_error(h, RR_EINVAL, "gemm: K must be a multiple of 4");
   if (amode == A_DENSE && (g.lda & 3)) return set_error(h, RR_EINVAL, "gemm: lda must be a multiple of 4");
   if (amode != A_CONV_GENERIC && (g.ldb & 3) != 0) return set_error(h, RR_EINVAL, "gemm: ldb must be a multiple of 4");

@@ -134,10 +134,14 @@ size_t rr_cosine_topk_workspace_size(int nq, long long n, int d, int k) {
   return topk_layout(nq, n > 0 ? n : 1, k).total;
 }
 
-int rr_cosine_topk(rr_handle_t h, const float* queries, int nq, const float* gallery, long long n, int d, int k,
-                   long long idx_offset, float* out_scores, long long* out_idx, void* workspace,
-                   size_t workspace_bytes, void* stream) {
-  if (!h) return RR_EINVAL;
+}  // extern "C"
+
+namespace rr {
+// Fused top-k over a gallery of any GEMM input dtype (fp32 / bf16 / fp8 with
+// per-row scales); see rr_cosine_topk for the algorithm.
+static int cosine_topk_impl(rr_handle_t h, const void* queries, const float* q_scale, int nq, const void* gallery,
+                            const float* g_scale, long long n, int d, int k, long long idx_offset, float* out_scores,
+                            long long* out_idx, void* workspace, size_t workspace_bytes, hipStream_t s, int dt) {
   if (nq < 0 || n < 0 || d <= 0 || (d & 3) || k < 1 || k > 16384)
     return set_error(h, RR_EINVAL, "rr_cosine_topk: need nq,n >= 0, d % 4 == 0, 1 <= k <= 16384");
   if (n >= 0xffffffffLL) return set_error(h, RR_EINVAL, "rr_cosine_topk: gallery shard must have < 2^32 rows");
@@ -146,17 +150,8 @@ int rr_cosine_topk(rr_handle_t h, const float* queries, int nq, const float* gal
     return set_error(h, RR_EINVAL, "rr_cosine_topk: null pointer");
   if (((uintptr_t)queries & 15) || ((uintptr_t)gallery & 15))
     return set_error(h, RR_EINVAL, "rr_cosine_topk: queries/gallery must be 16-byte aligned");
-  hipStream_t s = (hipStream_t)stream;
+  const int es = dt == DT_F32 ? 4 : (dt == DT_BF16 ? 2 : 1);
   const TopkWs L = topk_layout(nq, n > 0 ? n : 1, k);
-  if (n == 0) {
-    // nothing to rank: all padding
-    if (!workspace || workspace_bytes < L.total) return set_error(h, RR_EWORKSPACE, "rr_cosine_topk: workspace too small");
-    char* ws = (char*)workspace;
-    int* cnt = (int*)(ws + L.off_cnt);
-    if (int rc = check_hip(h, hipMemsetAsync(cnt, 0, (size_t)nq * 4, s), "memset")) return rc;
-    return launch_select_final(h, (unsigned long long*)(ws + L.off_cand), L.cap, cnt, nq, k, idx_offset, out_scores,
-                               out_idx, (int*)(ws + L.off_ovf), s);
-  }
   if (!workspace || workspace_bytes < L.total)
     return set_error(h, RR_EWORKSPACE, "rr_cosine_topk: workspace too small (query rr_cosine_topk_workspace_size)");
   char* ws = (char*)workspace;
@@ -165,47 +160,99 @@ int rr_cosine_topk(rr_handle_t h, const float* queries, int nq, const float* gal
   int* cnt = (int*)(ws + L.off_cnt);
   int* ovf = (int*)(ws + L.off_ovf);
   unsigned long long* cand = (unsigned long long*)(ws + L.off_cand);
-
+  if (n == 0) {  // nothing to rank: all padding
+    if (int rc = check_hip(h, hipMemsetAsync(cnt, 0, (size_t)nq * 4, s), "memset")) return rc;
+    return launch_select_final(h, cand, L.cap, cnt, nq, k, idx_offset, out_scores, out_idx, ovf, s);
+  }
   if (int rc = check_hip(h, hipMemsetAsync(ovf, 0, 4, s), "memset")) return rc;
-
   // 1. exact scores of the first s gallery rows (query-major)
   GemmArgs g;
-  g.A = gallery;
+  g.A = (const float*)gallery;
   g.lda = d;
   g.M = (int)L.s;
   g.K = d;
-  g.B = queries;
+  g.B = (const float*)queries;
   g.ldb = d;
   g.N = nq;
   g.C = scores_t;
   g.ldc = L.ld;
-  if (int rc = launch_gemm(h, A_DENSE, E_SCORES_T, g, s, kTimeCosineSeed)) return rc;
+  g.scale_a = g_scale;
+  g.scale_b = q_scale;
+  if (int rc = launch_gemm(h, A_DENSE, E_SCORES_T, g, s, kTimeCosineSeed, dt)) return rc;
   // 2. seed candidates with their exact top-k; tau = k-th best score
   if (int rc = launch_select_dense_seed(h, scores_t, L.ld, (int)L.s, nq, k, 0, cand, L.cap, cnt, tau, s)) return rc;
   // 3. remaining rows: fused GEMM + threshold filter (scores never hit HBM)
-  if (n > L.s) {
-    long long done = L.s;
-    while (done < n) {
-      const long long rows = std::min<long long>(n - done, 0x7fffff00LL);
-      GemmArgs f;
-      f.A = gallery + done * d;
-      f.lda = d;
-      f.M = (int)rows;
-      f.K = d;
-      f.B = queries;
-      f.ldb = d;
-      f.N = nq;
-      f.tau = tau;
-      f.cand = cand;
-      f.cnt = cnt;
-      f.cap = L.cap;
-      f.row_offset = done;
-      if (int rc = launch_gemm(h, A_DENSE, E_FILTER, f, s, kTimeCosine)) return rc;
-      done += rows;
-    }
+  long long done = L.s;
+  while (done < n) {
+    const long long rows = std::min<long long>(n - done, 0x7fffff00LL);
+    GemmArgs f;
+    f.A = (const float*)((const char*)gallery + done * d * es);
+    f.lda = d;
+    f.M = (int)rows;
+    f.K = d;
+    f.B = (const float*)queries;
+    f.ldb = d;
+    f.N = nq;
+    f.tau = tau;
+    f.cand = cand;
+    f.cnt = cnt;
+    f.cap = L.cap;
+    f.row_offset = done;
+    f.scale_a = g_scale ? g_scale + done : nullptr;
+    f.scale_b = q_scale;
+    if (int rc = launch_gemm(h, A_DENSE, E_FILTER, f, s, kTimeCosine, dt)) return rc;
+    done += rows;
   }
   // 4. exact top-k of the survivors, stable order
   return launch_select_final(h, cand, L.cap, cnt, nq, k, idx_offset, out_scores, out_idx, ovf, s);
+}
+}  // namespace rr
+
+extern "C" {
+
+int rr_cosine_topk(rr_handle_t h, const float* queries, int nq, const float* gallery, long long n, int d, int k,
+                   long long idx_offset, float* out_scores, long long* out_idx, void* workspace,
+                   size_t workspace_bytes, void* stream) {
+  if (!h) return RR_EINVAL;
+  return cosine_topk_impl(h, queries, nullptr, nq, gallery, nullptr, n, d, k, idx_offset, out_scores, out_idx,
+                          workspace, workspace_bytes, (hipStream_t)stream, DT_F32);
+}
+
+int rr_cosine_topk_lp(rr_handle_t h, const void* queries, const float* q_scale, int nq, const void* gallery,
+                      const float* g_scale, long long n, int d, int dtype, int k, long long idx_offset,
+                      float* out_scores, long long* out_idx, void* workspace, size_t workspace_bytes,
+                      void* stream) {
+  if (!h) return RR_EINVAL;
+  if (dtype != DT_BF16 && dtype != DT_FP8) return set_error(h, RR_EINVAL, "rr_cosine_topk_lp: dtype must be 1 or 2");
+  if (dtype == DT_FP8 && (!q_scale || !g_scale))
+    return set_error(h, RR_EINVAL, "rr_cosine_topk_lp: fp8 needs per-row scales");
+  if ((d % (dtype == DT_BF16 ? 8 : 16)) != 0)
+    return set_error(h, RR_EINVAL, "rr_cosine_topk_lp: rows must be multiples of 16 bytes");
+  return cosine_topk_impl(h, queries, q_scale, nq, gallery, g_scale, n, d, k, idx_offset, out_scores, out_idx,
+                          workspace, workspace_bytes, (hipStream_t)stream, dtype);
+}
+
+int rr_linear_bf16(rr_handle_t h, const void* x, int m, int k, const void* w, const float* bias, int n,
+                   const float* residual, int act, int out_bf16, void* y, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !w || !y || m < 0 || k <= 0 || n <= 0 || (k & 7) || act < 0 || act > 2)
+    return set_error(h, RR_EINVAL, "rr_linear_bf16: bad argument (k % 8 == 0)");
+  if (((uintptr_t)x & 15) || ((uintptr_t)w & 15)) return set_error(h, RR_EINVAL, "rr_linear_bf16: 16-B alignment");
+  GemmArgs g;
+  g.A = (const float*)x;
+  g.lda = k;
+  g.M = m;
+  g.K = k;
+  g.B = (const float*)w;
+  g.ldb = k;
+  g.N = n;
+  g.C = (float*)y;
+  g.ldc = n;
+  g.bias = bias;
+  g.residual = residual;
+  g.relu = act;
+  g.out_bf16 = out_bf16 ? 1 : 0;
+  return launch_gemm(h, A_DENSE, E_STORE, g, (hipStream_t)stream, kTimeGemm, DT_BF16);
 }
 
 int rr_cosine_scores(rr_handle_t h, const float* queries, int nq, const float* gallery, long long n, int d,

@@ -69,6 +69,7 @@ __host__ __device__ inline float key_score(unsigned long long k) {
 // ---- GEMM core launchers (gemm_f32.hip) ---------------------------------
 enum AMode { A_DENSE = 0, A_CONV = 1, A_CONV_GENERIC = 2, A_CONV_C4 = 3 };
 enum EMode { E_STORE = 0, E_SCORES_T = 1, E_FILTER = 2 };
+enum DType { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2 };
 
 struct GemmArgs {
   // A operand (M rows x K): dense [M][lda] or implicit im2col of NHWC input
@@ -92,9 +93,14 @@ struct GemmArgs {
   int* cnt = nullptr;
   long long cap = 0;
   long long row_offset = 0;  // added to the A row index in candidate keys
+  // per-row dequantisation scales (fp8 inputs), applied to the accumulator
+  const float* scale_a = nullptr;  // [M]
+  const float* scale_b = nullptr;  // [N]
+  int out_bf16 = 0;                // E_STORE: write bf16 instead of fp32
 };
 
-int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls);
+int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,
+                int dt = DT_F32);
 
 // ---- top-k kernels (topk.hip) -------------------------------------------
 // Dense scores, query-major [nq][ld] (first `rows` valid) -> per query the

@@ -13,11 +13,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // One wave per row: y = (x - mean) / sqrt(var + eps) * gamma + beta, biased
 // variance, two-pass over the row held in registers (D <= 64 * 64).
-template <int PER_LANE>
+template <int PER_LANE, typename OutT>
 __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, long long ldx, int M, int D,
                                                         const float* __restrict__ gamma,
                                                         const float* __restrict__ beta, float eps,
-                                                        float* __restrict__ y) {
+                                                        OutT* __restrict__ y) {
   const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
   if (row >= M) return;
@@ -43,11 +43,11 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
   const float rstd = 1.0f / sqrtf(q / (float)D + eps);
-  float* yr = y + (long long)row * D;
+  OutT* yr = y + (long long)row * D;
 #pragma unroll
   for (int i = 0; i < PER_LANE; ++i) {
     const int c = lane + 64 * i;
-    if (c < D) yr[c] = (v[i] - mean) * rstd * gamma[c] + beta[c];
+    if (c < D) yr[c] = (OutT)((v[i] - mean) * rstd * gamma[c] + beta[c]);
   }
 }
 
@@ -101,9 +101,9 @@ __global__ void vit_tokens_kernel(const float* __restrict__ patches, int B, int 
 //     lane (query, h) supplies P[query][key(r, h)] for MFMA step r, and the V
 //     fragment is read from LDS at that same key.  O /= rowsum; store.
 // Q is pre-scaled by 1/sqrt(64) = 0.125 (exact).
-template <int NC>
+template <int NC, typename OutT>
 __global__ __launch_bounds__(64 * NC) void attention_kernel(const float* __restrict__ qkv, int B, int L, int NH,
-                                                            float* __restrict__ out) {
+                                                            OutT* __restrict__ out) {
   constexpr int HD = 64;
   constexpr int LP = NC * 32;
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -212,9 +212,9 @@ __global__ __launch_bounds__(64 * NC) void attention_kernel(const float* __restr
     const float iq = __shfl(inv, qi, 64);
     const int q = q0 + qi;
     if (q < L) {
-      float* op = out + ((long long)b * L + q) * width + h * HD;
-      op[lr] = o[0][r] * iq;
-      op[32 + lr] = o[1][r] * iq;
+      OutT* op = out + ((long long)b * L + q) * width + h * HD;
+      op[lr] = (OutT)(o[0][r] * iq);
+      op[32 + lr] = (OutT)(o[1][r] * iq);
     }
   }
 }
@@ -226,16 +226,44 @@ static dim3 grid_for(long long n, int block) {
   return dim3((unsigned)g);
 }
 
-template <int NC>
-static hipError_t launch_attn(const float* qkv, int B, int L, int NH, float* out, hipStream_t s) {
+template <int NC, typename OutT>
+static hipError_t launch_attn(const float* qkv, int B, int L, int NH, OutT* out, hipStream_t s) {
   const size_t lds = (size_t)2 * NC * 32 * 64 * 4;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)attention_kernel<NC>,
+    hipError_t e = hipFuncSetAttribute((const void*)attention_kernel<NC, OutT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL(attention_kernel<NC>, dim3((unsigned)(B * NH)), dim3(64 * NC), lds, s, qkv, B, L, NH, out);
+  hipLaunchKernelGGL((attention_kernel<NC, OutT>), dim3((unsigned)(B * NH)), dim3(64 * NC), lds, s, qkv, B, L, NH,
+                     out);
   return hipGetLastError();
+}
+
+template <typename OutT>
+static hipError_t launch_attn_nc(int nc, const float* qkv, int b, int seq, int heads, OutT* out, hipStream_t s) {
+  switch (nc) {
+    case 1: return launch_attn<1>(qkv, b, seq, heads, out, s);
+    case 2: return launch_attn<2>(qkv, b, seq, heads, out, s);
+    case 3: return launch_attn<3>(qkv, b, seq, heads, out, s);
+    case 4: return launch_attn<4>(qkv, b, seq, heads, out, s);
+    case 5: return launch_attn<5>(qkv, b, seq, heads, out, s);
+    case 6: return launch_attn<6>(qkv, b, seq, heads, out, s);
+    case 7: return launch_attn<7>(qkv, b, seq, heads, out, s);
+    default: return launch_attn<8>(qkv, b, seq, heads, out, s);
+  }
+}
+
+template <typename OutT>
+static void launch_ln(int per, dim3 grid, hipStream_t s, const float* x, long long ldx, int m, int d,
+                      const float* gamma, const float* beta, float eps, OutT* y) {
+  if (per <= 4)
+    hipLaunchKernelGGL((layernorm_kernel<4, OutT>), grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
+  else if (per <= 12)
+    hipLaunchKernelGGL((layernorm_kernel<12, OutT>), grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
+  else if (per <= 16)
+    hipLaunchKernelGGL((layernorm_kernel<16, OutT>), grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
+  else
+    hipLaunchKernelGGL((layernorm_kernel<64, OutT>), grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
 }
 
 }  // namespace rr
@@ -244,22 +272,23 @@ using namespace rr;
 
 extern "C" int rr_layernorm(rr_handle_t h, const float* x, long long ldx, int m, int d, const float* gamma,
                             const float* beta, float eps, float* y, void* stream) {
+  return rr_layernorm_ex(h, x, ldx, m, d, gamma, beta, eps, 0, y, stream);
+}
+
+extern "C" int rr_layernorm_ex(rr_handle_t h, const float* x, long long ldx, int m, int d, const float* gamma,
+                               const float* beta, float eps, int out_dtype, void* y, void* stream) {
   if (!h) return RR_EINVAL;
-  if (!x || !y || !gamma || !beta || m < 0 || d <= 0 || d > 4096 || ldx < d)
-    return set_error(h, RR_EINVAL, "rr_layernorm: bad argument (d <= 4096, ldx >= d)");
+  if (!x || !y || !gamma || !beta || m < 0 || d <= 0 || d > 4096 || ldx < d || (out_dtype != 0 && out_dtype != 1))
+    return set_error(h, RR_EINVAL, "rr_layernorm: bad argument (d <= 4096, ldx >= d, out_dtype 0|1)");
   if (m == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeElem, s);
   const dim3 grid((unsigned)(((long long)m * 64 + 255) / 256));
   const int per = (d + 63) / 64;
-  if (per <= 4)
-    hipLaunchKernelGGL(layernorm_kernel<4>, grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
-  else if (per <= 12)
-    hipLaunchKernelGGL(layernorm_kernel<12>, grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
-  else if (per <= 16)
-    hipLaunchKernelGGL(layernorm_kernel<16>, grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
+  if (out_dtype == 1)
+    launch_ln<__bf16>(per, grid, s, x, ldx, m, d, gamma, beta, eps, (__bf16*)y);
   else
-    hipLaunchKernelGGL(layernorm_kernel<64>, grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
+    launch_ln<float>(per, grid, s, x, ldx, m, d, gamma, beta, eps, (float*)y);
   return check_hip(h, hipGetLastError(), "layernorm launch");
 }
 
@@ -292,23 +321,20 @@ extern "C" int rr_vit_tokens(rr_handle_t h, const float* patches, int b, int npa
 
 extern "C" int rr_attention(rr_handle_t h, const float* qkv, int b, int seq, int heads, int head_dim, float* out,
                             void* stream) {
+  return rr_attention_ex(h, qkv, b, seq, heads, head_dim, 0, out, stream);
+}
+
+extern "C" int rr_attention_ex(rr_handle_t h, const float* qkv, int b, int seq, int heads, int head_dim,
+                               int out_dtype, void* out, void* stream) {
   if (!h) return RR_EINVAL;
-  if (!qkv || !out || b < 0 || heads <= 0 || head_dim != 64 || seq <= 0 || seq > 256)
-    return set_error(h, RR_EINVAL, "rr_attention: supports head_dim == 64, 1 <= seq <= 256");
+  if (!qkv || !out || b < 0 || heads <= 0 || head_dim != 64 || seq <= 0 || seq > 256 ||
+      (out_dtype != 0 && out_dtype != 1))
+    return set_error(h, RR_EINVAL, "rr_attention: supports head_dim == 64, 1 <= seq <= 256, out_dtype 0|1");
   if (b == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeAttn, s);
   const int nc = (seq + 31) / 32;
-  hipError_t e;
-  switch (nc) {
-    case 1: e = launch_attn<1>(qkv, b, seq, heads, out, s); break;
-    case 2: e = launch_attn<2>(qkv, b, seq, heads, out, s); break;
-    case 3: e = launch_attn<3>(qkv, b, seq, heads, out, s); break;
-    case 4: e = launch_attn<4>(qkv, b, seq, heads, out, s); break;
-    case 5: e = launch_attn<5>(qkv, b, seq, heads, out, s); break;
-    case 6: e = launch_attn<6>(qkv, b, seq, heads, out, s); break;
-    case 7: e = launch_attn<7>(qkv, b, seq, heads, out, s); break;
-    default: e = launch_attn<8>(qkv, b, seq, heads, out, s); break;
-  }
+  const hipError_t e = out_dtype == 1 ? launch_attn_nc<__bf16>(nc, qkv, b, seq, heads, (__bf16*)out, s)
+                                      : launch_attn_nc<float>(nc, qkv, b, seq, heads, (float*)out, s);
   return check_hip(h, e, "attention launch");
 }

@@ -216,7 +216,7 @@ class VisionTransformer(_Extractor):
     proj).  LayerNorm eps 1e-5 (nn.LayerNorm default)."""
 
     def __init__(self, input_resolution=224, patch_size=16, width=768, layers=12, heads=12, output_dim=512,
-                 state_dict=None, device="cuda"):
+                 state_dict=None, device="cuda", dtype="fp32"):
         if width % heads or width // heads != 64:
             raise ValueError("VisionTransformer: librr's fused attention needs head_dim == 64")
         if state_dict is None:
@@ -243,9 +243,36 @@ class VisionTransformer(_Extractor):
                 "mlp.c_proj.bias", "ln_2.weight", "ln_2.bias")})
         self.ln_post = (t("ln_post.weight"), t("ln_post.bias"))
         self.proj_t = state_dict["proj"].float().t().contiguous().to(self.device)  # [out, width]
+        if dtype not in ("fp32", "bf16"):
+            raise ValueError("VisionTransformer dtype must be fp32 or bf16")
+        self.dtype = dtype
+        if dtype == "bf16":
+            # config C4: bf16 GEMM operands (weights rounded once, RNE), fp32
+            # accumulate, fp32 residual stream / LayerNorm / softmax
+            self.conv_w_bf = self.conv_w.to(torch.bfloat16)
+            for blk in self.blocks:
+                for k in ("attn.in_proj_weight", "attn.out_proj.weight", "mlp.c_fc.weight", "mlp.c_proj.weight"):
+                    blk[k + ".bf16"] = blk[k].to(torch.bfloat16)
+
+    def _forward_bf16(self, x_nhwc, b):
+        p, _ = ops.quantize_rows(ops.patchify(x_nhwc, self.patch), "bf16")
+        x = ops.vit_tokens(ops.linear_bf16(p, self.conv_w_bf), b, self.cls, self.pos)
+        x = ops.layernorm(x, *self.ln_pre)
+        for blk in self.blocks:
+            y = ops.layernorm_bf16(x, blk["ln_1.weight"], blk["ln_1.bias"])
+            qkv = ops.linear_bf16(y, blk["attn.in_proj_weight.bf16"], blk["attn.in_proj_bias"])
+            a = ops.attention_bf16(qkv, b, self.seq, self.heads)
+            x = ops.linear_bf16(a, blk["attn.out_proj.weight.bf16"], blk["attn.out_proj.bias"], residual=x)
+            y = ops.layernorm_bf16(x, blk["ln_2.weight"], blk["ln_2.bias"])
+            y = ops.linear_bf16(y, blk["mlp.c_fc.weight.bf16"], blk["mlp.c_fc.bias"], act=2, out_bf16=True)
+            x = ops.linear_bf16(y, blk["mlp.c_proj.weight.bf16"], blk["mlp.c_proj.bias"], residual=x)
+        cls = ops.layernorm(x, *self.ln_post, rows=b, row_stride=self.seq * self.width)
+        return ops.linear(cls, self.proj_t)
 
     def forward_nhwc(self, x_nhwc):
         b, h, w, _ = x_nhwc.shape
+        if self.dtype == "bf16" and h == self.res and w == self.res:
+            return self._forward_bf16(x_nhwc, b)
         if h != self.res or w != self.res:
             raise ValueError(f"VisionTransformer: fixed {self.res}x{self.res} input (positional embedding has "
                              f"{self.seq} tokens; networks/model.py:228)")

@@ -288,3 +288,80 @@ def attention(qkv, b, seq, heads, head_dim=64):
     _lib.check(_lib.lib().rr_attention(hd, _ptr(qkv), b, seq, heads, head_dim, _ptr(out), _stream(dev)), hd,
                "rr_attention")
     return out
+
+
+# ---- low precision (C4 bf16 / C5 fp8) --------------------------------------
+DT_BF16, DT_FP8 = 1, 2
+_LP = {"bf16": DT_BF16, "fp8": DT_FP8}
+
+
+def quantize_rows(x, dtype):
+    """fp32 [rows, d] -> (bf16 tensor, None) or (fp8-e4m3 bytes as uint8, per-row fp32 scales)."""
+    _f32(x, "quantize_rows")
+    dev = _dev(x)
+    dt = _LP[dtype]
+    rows, d = x.shape
+    if dt == DT_BF16:
+        y = torch.empty((rows, d), dtype=torch.bfloat16, device=x.device)
+        sc = None
+    else:
+        y = torch.empty((rows, d), dtype=torch.uint8, device=x.device)
+        sc = torch.empty(rows, dtype=torch.float32, device=x.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_quantize_rows(hd, _ptr(x), rows, d, dt, _ptr(y), _ptr(sc), _stream(dev)), hd,
+               "rr_quantize_rows")
+    return y, sc
+
+
+def cosine_topk_lp(q, q_scale, g, g_scale, k, dtype, idx_offset=0, workspace=None):
+    """Fused top-k on bf16 / fp8 rows (fp32 accumulate); scores dequantised."""
+    dev = _dev(q)
+    dt = _LP[dtype]
+    nq, d = q.shape
+    n = g.shape[0]
+    need = cosine_topk_workspace_size(nq, n, d, k)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    os_ = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+    oi = torch.empty((nq, k), dtype=torch.int64, device=q.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_cosine_topk_lp(hd, _ptr(q), _ptr(q_scale), nq, _ptr(g), _ptr(g_scale), n, d, dt, k,
+                                            int(idx_offset), _ptr(os_), _ptr(oi), _ptr(workspace), workspace.numel(),
+                                            _stream(dev)), hd, "rr_cosine_topk_lp")
+    return os_, oi
+
+
+def linear_bf16(x, w, bias=None, residual=None, act=0, out_bf16=False):
+    """bf16 x [M,K] . bf16 w [N,K]^T -> fp32 (or bf16) with fused epilogue."""
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        raise TypeError("linear_bf16: x and w must be bfloat16")
+    dev = _dev(x)
+    m, k = x.shape
+    n = w.shape[0]
+    y = torch.empty((m, n), dtype=torch.bfloat16 if out_bf16 else torch.float32, device=x.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_linear_bf16(hd, _ptr(x), m, k, _ptr(w), _ptr(bias), n, _ptr(residual), int(act),
+                                         int(out_bf16), _ptr(y), _stream(dev)), hd, "rr_linear_bf16")
+    return y
+
+
+def layernorm_bf16(x, gamma, beta, eps=1e-5):
+    _f32(x, "layernorm_bf16")
+    dev = _dev(x)
+    d = x.shape[-1]
+    m = x.numel() // d
+    y = torch.empty((m, d), dtype=torch.bfloat16, device=x.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_layernorm_ex(hd, _ptr(x), d, m, d, _ptr(gamma), _ptr(beta), float(eps), 1, _ptr(y),
+                                          _stream(dev)), hd, "rr_layernorm_ex")
+    return y
+
+
+def attention_bf16(qkv, b, seq, heads, head_dim=64):
+    _f32(qkv, "attention_bf16")
+    dev = _dev(qkv)
+    out = torch.empty((b * seq, heads * head_dim), dtype=torch.bfloat16, device=qkv.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_attention_ex(hd, _ptr(qkv), b, seq, heads, head_dim, 1, _ptr(out), _stream(dev)), hd,
+               "rr_attention_ex")
+    return out

@@ -34,11 +34,19 @@ class GallerySearcher:
     iris_evaluate.py:380); pass False for descriptors that are already unit
     norm (extractor outputs are)."""
 
-    def __init__(self, gallery, device="cuda", normalize=True, idx_offset=0):
+    def __init__(self, gallery, device="cuda", normalize=True, idx_offset=0, dtype="fp32"):
+        """dtype "fp32" (exact, default), or "bf16" / "fp8" (configs C4 / C5:
+        the gallery is quantised once; parity vs fp32 is recall@k)."""
+        if dtype not in ("fp32", "bf16", "fp8"):
+            raise ValueError("dtype must be fp32, bf16 or fp8")
         self.device = torch.device(device)
         g = _dev_f32(gallery, self.device)
         self.gallery = ops.l2_normalize(g, 1e-12) if normalize else g
         self.idx_offset = int(idx_offset)
+        self.dtype = dtype
+        self.gallery_lp, self.gallery_scale = (None, None)
+        if dtype != "fp32":
+            self.gallery_lp, self.gallery_scale = ops.quantize_rows(self.gallery, dtype)
         self._ws = None
 
     @property
@@ -53,6 +61,10 @@ class GallerySearcher:
         need = ops.cosine_topk_workspace_size(q.shape[0], self.n, q.shape[1], k)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        if self.dtype != "fp32":
+            q_lp, q_sc = ops.quantize_rows(q.contiguous(), self.dtype)
+            return ops.cosine_topk_lp(q_lp, q_sc, self.gallery_lp, self.gallery_scale, k, self.dtype,
+                                      idx_offset=self.idx_offset, workspace=self._ws)
         return ops.cosine_topk(q, self.gallery, k, idx_offset=self.idx_offset, workspace=self._ws)
 
 

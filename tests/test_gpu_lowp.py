@@ -1,0 +1,81 @@
+"""Low-precision paths (configs C4 bf16 / C5 fp8): GEMM numerics vs a torch
+fp32 reference on the same rounded inputs, recall@100 of the bf16 / fp8
+cosine top-k against the exact fp32 ranking, ViT-B/16 bf16 vs the reference
+fixture."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+import oracle
+from research_image_retrieval_amd import ops
+from research_image_retrieval_amd.networks import VisionTransformer
+from research_image_retrieval_amd.search import GallerySearcher
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+sys.path.insert(0, GOLD)
+import inputs as I  # noqa: E402
+
+
+def test_bf16_linear_vs_torch(cuda):
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(300, 768, generator=g)
+    w = torch.randn(1000, 768, generator=g) * 0.03
+    b = torch.randn(1000, generator=g)
+    r = torch.randn(300, 1000, generator=g)
+    xb, wb = x.to(torch.bfloat16), w.to(torch.bfloat16)
+    ref = torch.nn.functional.linear(xb.double(), wb.double(), b.double()) + r.double()
+    out = ops.linear_bf16(xb.to(cuda), wb.to(cuda), b.to(cuda), residual=r.to(cuda)).cpu()
+    torch.testing.assert_close(out, ref.float(), rtol=1e-5, atol=1e-4)
+    z = torch.nn.functional.linear(xb.double(), wb.double(), b.double())
+    refg = (z * torch.sigmoid(1.702 * z)).to(torch.bfloat16)
+    outg = ops.linear_bf16(xb.to(cuda), wb.to(cuda), b.to(cuda), act=2, out_bf16=True).cpu()
+    assert (outg.float() - refg.float()).abs().max() <= 0.02 * refg.float().abs().max()
+
+
+def test_fp8_quantize_and_scores(cuda):
+    rng = np.random.RandomState(1)
+    x = I.normed(rng, 50, 512)
+    xt = torch.from_numpy(x).to(cuda)
+    q, sc = ops.quantize_rows(xt, "fp8")
+    deq = q.cpu().view(torch.float8_e4m3fn).float() * sc.cpu()[:, None]
+    xs = torch.from_numpy(x)
+    # e4m3: 3 mantissa bits -> half-ulp 2^-4 relative; subnormals 2^-10 absolute (in scaled units)
+    bound = xs.abs() * 2.0 ** -4 + 2.0 ** -10 * sc.cpu()[:, None]
+    assert ((deq - xs).abs() <= bound).all()
+    # fp8 GEMM scores == fp32 dot products of the dequantised rows (fp32 accumulate)
+    s, i = ops.cosine_topk_lp(q[:7].contiguous(), sc[:7].contiguous(), q, sc, 50, "fp8")
+    ref = (deq[:7].double() @ deq.double().T).float()
+    got = torch.full_like(ref, float("nan"))
+    got.scatter_(1, i.cpu(), s.cpu())
+    torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize("dtype,min_recall", [("bf16", 0.95), ("fp8", 0.80)])
+def test_lowp_cosine_recall_at_100(cuda, dtype, min_recall):
+    q, g = I.rank_inputs(23, 32, 60000, 512)
+    _, i_ref = oracle.cosine_topk(q, g, 100)
+    srch = GallerySearcher(g, device=cuda, normalize=False, dtype=dtype)
+    _, i = srch.topk(q, 100, normalize=False)
+    i = i.cpu().numpy()
+    recall = np.mean([len(set(i[r]) & set(i_ref[r])) / 100.0 for r in range(len(q))])
+    print(dtype, "recall@100", recall)
+    assert recall >= min_recall
+    assert (i[:6, 0] == i_ref[:6, 0]).all()  # planted near-duplicates stay first
+
+
+def test_vit_b16_bf16_vs_reference(cuda):
+    fx = np.load(os.path.join(GOLD, "vit.npz"))
+    res, patch, width, layers, heads, out_dim, seed = (int(v) for v in fx["b16_cfg"])
+    sd = I.vit_state_dict(seed, width, layers, heads, patch, res, out_dim)
+    net = VisionTransformer(res, patch, width, layers, heads, out_dim, state_dict=sd, device=cuda, dtype="bf16")
+    rsx = np.random.RandomState(seed + 100)
+    x = torch.from_numpy(rsx.standard_normal((2, 3, res, res)).astype(np.float32))
+    got = net(x.to(cuda)).cpu().numpy()
+    ref = fx["b16"]
+    cos = (got * ref).sum(1) / np.linalg.norm(got, axis=1) / np.linalg.norm(ref, axis=1)
+    print("bf16 ViT cosine to fp32 reference", cos)
+    assert cos.min() > 0.995
