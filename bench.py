@@ -35,7 +35,8 @@ from research_image_retrieval_amd.distributed import ShardedGallery, shard_bound
 from research_image_retrieval_amd.networks import GeM, ConvDimReduction, GeMPCAw, VisionTransformer  # noqa: E402
 
 METRIC = "images embedded+ranked/sec on 1.6M×2048 gallery; mAP on ROxf/RPar"
-PEAK_FP32_TFLOPS = 157.3  # MI355X_MICROARCH.md: f32 MFMA (= f32 vector) peak
+# MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) per input dtype, HBM3E peak
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "fp8": 5000.0}
 PEAK_HBM_GBS = 8000.0
 
 
@@ -146,14 +147,20 @@ def main():
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--arch", default="resnet101")
     ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
-                    help="c3: ResNet101-GeM 2048-d + PCA-w (BASELINE metric config); "
-                         "c4: ViT-B/16 CLS 512-d (fp32 here; bf16 is the next row)")
+                    help="c3: ResNet101-GeM 2048-d + PCA-w, fp32 (BASELINE metric config); "
+                         "c4: ViT-B/16 CLS 512-d, bf16 GEMMs + bf16 cosine")
+    ap.add_argument("--dtype", choices=("fp32", "bf16", "fp8"), default=None,
+                    help="GEMM input dtype (default: fp32 for c3, bf16 for c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
     if a.workload == "c4":
         if a.dim == 2048:
             a.dim = 512
         a.arch = "vit_b16"
+    if a.dtype is None:
+        a.dtype = "bf16" if a.workload == "c4" else "fp32"
+    if a.workload == "c3" and a.dtype != "fp32":
+        raise SystemExit("c3 is defined in fp32 (the reference's arithmetic)")
 
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # started bare with --gpus N: run ourselves under torch.distributed.run
@@ -186,7 +193,7 @@ def main():
     lo, hi = shard_bounds(a.gallery, world, rank)
     gallery = make_gallery(a.gallery, a.dim, lo, hi, dev)
     if a.workload == "c4":
-        net = VisionTransformer(224, 16, 768, 12, 12, a.dim,
+        net = VisionTransformer(224, 16, 768, 12, 12, a.dim, dtype="bf16" if a.dtype != "fp32" else "fp32",
                                 state_dict=W.synthetic_vit_state_dict(out_dim=a.dim, seed=0), device=dev)
     else:
         net = build_extractor(a.arch, dev)
@@ -194,7 +201,8 @@ def main():
     imgs = torch.from_numpy(rs.randint(0, 256, size=(a.batch, 224, 224, 3), dtype=np.uint8)).to(dev)
     q_total = a.batch * world
     ws = torch.empty(ops.cosine_topk_workspace_size(q_total, hi - lo, a.dim, a.k), dtype=torch.uint8, device=dev)
-    sharded = ShardedGallery(gallery, lo, workspace=ws) if world > 1 else None
+    sharded = ShardedGallery(gallery, lo, workspace=ws, dtype=a.dtype) if world > 1 else None
+    gal_lp, gal_sc = ops.quantize_rows(gallery, a.dtype) if (a.dtype != "fp32" and world == 1) else (None, None)
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: shard [{lo},{hi}) x {a.dim}, batch {a.batch}")
 
@@ -202,6 +210,9 @@ def main():
         desc = net.forward_test_u8(imgs)
         if sharded is not None:
             return sharded.search(desc, a.k)
+        if gal_lp is not None:
+            q_lp, q_sc = ops.quantize_rows(desc, a.dtype)
+            return ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws)
         return ops.cosine_topk(desc, gallery, a.k, idx_offset=lo, workspace=ws)
 
     for _ in range(a.warmup):
@@ -249,16 +260,35 @@ def main():
         conv_flops_img = sum(W.resnet_conv_flops(a.arch, 224, 224).values()) + 2 * 2 * 2048 * 2048  # + whiten, PCA-w
     traffic = load_traffic()
     rk = {}
-    for name, fl in (("cosine_filter", flop_filter * a.steps), ("conv_gemm", conv_flops_img * a.batch * a.steps),
-                     ("cosine_seed", flop_seed * a.steps), ("attention", attn_flops_img * a.batch * a.steps)):
+    esz = {"fp32": 4, "bf16": 2, "fp8": 1}[a.dtype]
+    rows_filter = max(0, (hi - lo) - s_rows)
+    # (class, algorithmic FLOPs, algorithmic HBM bytes or None, dtype of its MFMA)
+    entries = (("cosine_filter", flop_filter, float(rows_filter) * a.dim * esz, a.dtype),
+               ("conv_gemm", conv_flops_img * a.batch, None, a.dtype),
+               ("cosine_seed", flop_seed, float(s_rows) * a.dim * esz, a.dtype),
+               ("attention", attn_flops_img * a.batch, None, "fp32"))
+    for name, fl_step, by_step, dt in entries:
         ms, n = cls[name]
         if n == 0 or ms <= 0:
             continue
-        ach = fl / (ms / 1e3) / 1e12
-        rk[name] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                    "frac": round(ach / PEAK_FP32_TFLOPS, 4), "ms_per_step": round(ms / a.steps, 3),
-                    "launches_per_step": n / a.steps,
-                    "traffic": (traffic or {}).get(name)}
+        sec = ms / 1e3 / a.steps
+        peak = PEAK_TFLOPS[dt]
+        t_mfma = fl_step / (peak * 1e12)
+        t_hbm = by_step / (PEAK_HBM_GBS * 1e9) if by_step else 0.0
+        if t_hbm > t_mfma:
+            ach = by_step / sec / 1e9
+            e = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                 "frac": round(ach / PEAK_HBM_GBS, 4)}
+        else:
+            ach = fl_step / sec / 1e12
+            e = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                 "frac": round(ach / peak, 4)}
+        e.update({"dtype": dt, "ms_per_step": round(ms / a.steps, 3), "launches_per_step": n / a.steps,
+                  "algorithmic_flop_per_launch": fl_step / max(1.0, n / a.steps),
+                  "algorithmic_bytes_per_launch": (by_step / max(1.0, n / a.steps)) if by_step else None,
+                  "traffic": ((traffic or {}).get(name) or {}).get("hbm_bytes_per_launch")
+                  if a.workload == "c3" else None})
+        rk[name] = e
     for name in ("select", "elementwise"):
         ms, n = cls[name]
         rk[name] = {"ms_per_step": round(ms / a.steps, 3), "launches_per_step": n / a.steps}
@@ -268,11 +298,11 @@ def main():
 
     res = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
-           "scaling": "weak", "vs_baseline": None, "dtype": "fp32",
+           "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
            "data": "synthetic: uint8 224x224x3 images RandomState(1234+rank); seeded Gaussian L2-normalised "
                    "gallery; seeded ResNet/whiten/PCA-w weights (no pretrained weights offline)",
            "config": {"workload": (f"C3: {a.arch}-GeM 2048-d + PCA-whiten" if a.workload == "c3" else
-                                   f"C4 (fp32): ViT-B/16 CLS {a.dim}-d") +
+                                   f"C4: ViT-B/16 CLS {a.dim}-d ({a.dtype} GEMMs + {a.dtype} cosine)") +
                                   f", embed + exact top-{a.k} against a {a.gallery}x{a.dim} gallery",
                       "global_batch": q_total,
                       "images_per_gpu_per_step": a.batch, "gallery_rows": a.gallery, "dim": a.dim, "k": a.k,

@@ -59,13 +59,17 @@ def _all_gather_var(t, group):
 class ShardedGallery:
     """This rank's shard of a gallery that is row-partitioned over the group."""
 
-    def __init__(self, shard, global_offset, group=None, local_topk=None, merge=None, workspace=None):
+    def __init__(self, shard, global_offset, group=None, local_topk=None, merge=None, workspace=None, dtype="fp32"):
         self.shard = shard
         self.offset = int(global_offset)
         self.group = group
         self._local_topk = local_topk
         self._merge = merge
         self._ws = workspace
+        self.dtype = dtype
+        self.shard_lp, self.shard_scale = (None, None)
+        if dtype != "fp32" and local_topk is None:
+            self.shard_lp, self.shard_scale = ops.quantize_rows(shard, dtype)
 
     def _local(self, q, k):
         if self._local_topk is not None:
@@ -73,6 +77,10 @@ class ShardedGallery:
         need = ops.cosine_topk_workspace_size(q.shape[0], self.shard.shape[0], q.shape[1], k)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=q.device)
+        if self.dtype != "fp32":
+            q_lp, q_sc = ops.quantize_rows(q, self.dtype)
+            return ops.cosine_topk_lp(q_lp, q_sc, self.shard_lp, self.shard_scale, k, self.dtype,
+                                      idx_offset=self.offset, workspace=self._ws)
         return ops.cosine_topk(q, self.shard, k, idx_offset=self.offset, workspace=self._ws)
 
     def _merge_parts(self, ps, pi, k):

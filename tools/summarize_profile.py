@@ -13,9 +13,9 @@ import re
 import sys
 from collections import defaultdict
 
-CLASS = [(r"gemm_kernel<\d, \d, 0, 2>", "cosine_filter"), (r"gemm_kernel<\d, \d, 0, 1>", "cosine_seed"),
-         (r"gemm_kernel<\d, \d, [012], 0>", "conv_gemm"), (r"select_|merge_kernel", "select"),
-         (r"rr::", "elementwise")]
+CLASS = [(r"gemm_kernel<\d, \d, 0, 2[,>]", "cosine_filter"), (r"gemm_kernel<\d, \d, 0, 1[,>]", "cosine_seed"),
+         (r"gemm_kernel<\d, \d, [0-3], 0[,>]", "conv_gemm"), (r"select_|merge_kernel", "select"),
+         (r"attention_kernel", "attention"), (r"rr::", "elementwise")]
 
 
 def short(name):
