@@ -33,6 +33,7 @@ from research_image_retrieval_amd import _lib, ops  # noqa: E402
 from research_image_retrieval_amd import weights as W  # noqa: E402
 from research_image_retrieval_amd.distributed import ShardedGallery, shard_bounds  # noqa: E402
 from research_image_retrieval_amd.networks import GeM, ConvDimReduction, GeMPCAw, VisionTransformer  # noqa: E402
+from research_image_retrieval_amd.extract import _rescale  # noqa: E402
 
 METRIC = "images embedded+ranked/sec on 1.6M×2048 gallery; mAP on ROxf/RPar"
 # MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) per input dtype, HBM3E peak
@@ -146,9 +147,10 @@ def main():
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--arch", default="resnet101")
-    ap.add_argument("--workload", choices=("c3", "c4"), default="c3",
+    ap.add_argument("--workload", choices=("c3", "c4", "c5"), default="c3",
                     help="c3: ResNet101-GeM 2048-d + PCA-w, fp32 (BASELINE metric config); "
-                         "c4: ViT-B/16 CLS 512-d, bf16 GEMMs + bf16 cosine")
+                         "c4: ViT-B/16 CLS 512-d, bf16 GEMMs + bf16 cosine; "
+                         "c5: c3 extractor at 3 scales + fp8 cosine + alpha-QE re-rank (1 GPU)")
     ap.add_argument("--dtype", choices=("fp32", "bf16", "fp8"), default=None,
                     help="GEMM input dtype (default: fp32 for c3, bf16 for c4)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -158,7 +160,7 @@ def main():
             a.dim = 512
         a.arch = "vit_b16"
     if a.dtype is None:
-        a.dtype = "bf16" if a.workload == "c4" else "fp32"
+        a.dtype = {"c3": "fp32", "c4": "bf16", "c5": "fp8"}[a.workload]
     if a.workload == "c3" and a.dtype != "fp32":
         raise SystemExit("c3 is defined in fp32 (the reference's arithmetic)")
 
@@ -182,6 +184,8 @@ def main():
     # one process per GPU; ranks beyond the visible devices share them (rehearsal)
     dev = torch.device("cuda", local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
+    if a.workload == "c5" and world > 1:
+        raise SystemExit("c5 is single-GPU in this round (sharded alpha-QE needs an all-reduce of partial expansions)")
     if world > 1:
         backend = os.environ.get("RR_DIST_BACKEND", "nccl")  # "gloo" only for 1-GPU rehearsals
         if backend == "nccl":
@@ -206,8 +210,29 @@ def main():
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: shard [{lo},{hi}) x {a.dim}, batch {a.batch}")
 
+    scales = (1.0, 1.0 / np.sqrt(2.0), 0.5)  # C5 multi-scale set
+
+    def embed():
+        if a.workload != "c5":
+            return net.forward_test_u8(imgs)
+        # multi-scale extraction (utils/helpfunc.py:30-46): rescale, embed, average, renormalise
+        x = ops.preprocess_u8(imgs, out_c=4)
+        acc = None
+        for sc in scales:
+            xs = x if sc == 1.0 else _rescale(x, sc)
+            f = net.forward_test_nhwc(xs)
+            acc = f.clone() if acc is None else acc.add_(f)
+        acc.div_(len(scales))
+        return ops.l2_normalize(acc, 1e-12, out=acc)
+
     def step():
-        desc = net.forward_test_u8(imgs)
+        desc = embed()
+        if a.workload == "c5":
+            q_lp, q_sc = ops.quantize_rows(desc, a.dtype)
+            s1, i1 = ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws)
+            q2 = ops.alpha_qe(desc, gallery, i1, s1, n=2, alpha=3.0, idx_offset=lo)
+            q_lp, q_sc = ops.quantize_rows(q2, a.dtype)
+            return ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws)
         if sharded is not None:
             return sharded.search(desc, a.k)
         if gal_lp is not None:
@@ -256,6 +281,11 @@ def main():
     attn_flops_img = 0
     if a.workload == "c4":
         conv_flops_img, attn_flops_img = W.vit_flops(out_dim=a.dim)
+    elif a.workload == "c5":
+        conv_flops_img = sum(sum(W.resnet_conv_flops(a.arch, int(224.0 * sc), int(224.0 * sc)).values())
+                             + 2 * 2 * 2048 * 2048 for sc in scales)
+        flop_filter *= 2  # two searches (before and after alpha-QE)
+        flop_seed *= 2
     else:
         conv_flops_img = sum(W.resnet_conv_flops(a.arch, 224, 224).values()) + 2 * 2 * 2048 * 2048  # + whiten, PCA-w
     traffic = load_traffic()
@@ -263,9 +293,10 @@ def main():
     esz = {"fp32": 4, "bf16": 2, "fp8": 1}[a.dtype]
     rows_filter = max(0, (hi - lo) - s_rows)
     # (class, algorithmic FLOPs, algorithmic HBM bytes or None, dtype of its MFMA)
-    entries = (("cosine_filter", flop_filter, float(rows_filter) * a.dim * esz, a.dtype),
-               ("conv_gemm", conv_flops_img * a.batch, None, a.dtype),
-               ("cosine_seed", flop_seed, float(s_rows) * a.dim * esz, a.dtype),
+    searches = 2 if a.workload == "c5" else 1
+    entries = (("cosine_filter", flop_filter, searches * float(rows_filter) * a.dim * esz, a.dtype),
+               ("conv_gemm", conv_flops_img * a.batch, None, a.dtype if a.workload == "c4" else "fp32"),
+               ("cosine_seed", flop_seed, searches * float(s_rows) * a.dim * esz, a.dtype),
                ("attention", attn_flops_img * a.batch, None, "fp32"))
     for name, fl_step, by_step, dt in entries:
         ms, n = cls[name]
@@ -301,9 +332,11 @@ def main():
            "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
            "data": "synthetic: uint8 224x224x3 images RandomState(1234+rank); seeded Gaussian L2-normalised "
                    "gallery; seeded ResNet/whiten/PCA-w weights (no pretrained weights offline)",
-           "config": {"workload": (f"C3: {a.arch}-GeM 2048-d + PCA-whiten" if a.workload == "c3" else
-                                   f"C4: ViT-B/16 CLS {a.dim}-d ({a.dtype} GEMMs + {a.dtype} cosine)") +
-                                  f", embed + exact top-{a.k} against a {a.gallery}x{a.dim} gallery",
+           "config": {"workload": {"c3": f"C3: {a.arch}-GeM 2048-d + PCA-whiten",
+                                   "c4": f"C4: ViT-B/16 CLS {a.dim}-d ({a.dtype} GEMMs + {a.dtype} cosine)",
+                                   "c5": f"C5: {a.arch}-GeM+PCA-w at 3 scales, {a.dtype} cosine + alpha-QE "
+                                         f"(n=2, alpha=3) re-rank"}[a.workload] +
+                                  f", embed + {'exact' if a.dtype == 'fp32' else a.dtype} top-{a.k} against a {a.gallery}x{a.dim} gallery",
                       "global_batch": q_total,
                       "images_per_gpu_per_step": a.batch, "gallery_rows": a.gallery, "dim": a.dim, "k": a.k,
                       "parallelism": f"query-dp{world} + gallery-shard{world}"},

@@ -109,6 +109,18 @@ int rr_cosine_topk_lp(rr_handle_t h, const void* queries, const float* q_scale,
                       float* out_scores, long long* out_idx, void* workspace,
                       size_t workspace_bytes, void* stream);
 
+/* alpha-weighted query expansion (config C5; absent from the reference,
+ * SURVEY.md §8f row 3 — defined as in Radenovic et al., TPAMI 2018, the GeM
+ * paper models/gem_pooling.py:3 cites):
+ *   out[i] = normalize(q[i] + sum_{r<n} max(s[i][r],0)^alpha * g[idx[i][r]-idx_offset])
+ * top_idx / top_scores [nq][k] as returned by rr_cosine_topk (idx < 0 =
+ * padding, skipped); gallery rows are the local shard.  Re-rank by calling
+ * rr_cosine_topk with `out` as the queries.                                */
+int rr_alpha_qe(rr_handle_t h, const float* queries, int nq,
+                const float* gallery, int d, const long long* top_idx,
+                const float* top_scores, int k, int n, float alpha,
+                long long idx_offset, float* out, void* stream);
+
 /* ---- embed (extractor) ---------------------------------------------------
  * uint8 HWC pixels -> fp32 NHWC, (x/255 - mean[c]) / std[c].
  * Replaces transforms.ToTensor + Normalize(mean=[.485,.456,.406],

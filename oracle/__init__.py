@@ -97,3 +97,18 @@ def argsort_stable_desc(scores):
     """Full stable ranking of each row (the reference's np.argsort(-S, axis=1),
     iris_evaluate.py:386, with a stable tie-break)."""
     return np.argsort(-np.asarray(scores), axis=1, kind="stable")
+
+
+def alpha_qe(q, g, top_idx, top_scores, n=2, alpha=3.0, idx_offset=0):
+    """alpha-QE restatement (float64 accumulate, then fp32): q + sum max(s,0)^a g_r, L2-normalised."""
+    q = np.asarray(q, np.float64)
+    out = q.copy()
+    for i in range(q.shape[0]):
+        for r in range(n):
+            j = int(top_idx[i, r]) - idx_offset
+            if j < 0:
+                continue
+            w = max(float(top_scores[i, r]), 0.0) ** alpha
+            out[i] += w * np.asarray(g[j], np.float64)
+    out /= np.maximum(np.linalg.norm(out, axis=1, keepdims=True), 1e-12)
+    return out.astype(np.float32)

@@ -271,3 +271,65 @@ extern "C" int rr_resize_bilinear(rr_handle_t h, const float* x, int b, int hgt,
                      sw, y);
   return check_hip(h, hipGetLastError(), "resize launch");
 }
+
+// ---- alpha-weighted query expansion (config C5) --------------------------
+// q'[i] = normalize(q[i] + sum_{r < n} max(s[i][r], 0)^alpha * g[idx[i][r]])
+// One workgroup per query; the n neighbour rows are gathered with coalesced
+// float4 loads and accumulated in registers, then the row is L2-normalised
+// with a block reduction.  Padding entries (idx < 0) are skipped.
+namespace rr {
+__global__ __launch_bounds__(256) void alpha_qe_kernel(const float* __restrict__ q, const float* __restrict__ g,
+                                                       const long long* __restrict__ idx,
+                                                       const float* __restrict__ sc, int k, int n, int d,
+                                                       float alpha, long long idx_offset, float* __restrict__ out) {
+  __shared__ float red[256 / 64];
+  const int qi = blockIdx.x;
+  const int d4 = d >> 2;
+  float ss = 0.f;
+  for (int c = threadIdx.x; c < d4; c += 256) {
+    float4 acc = reinterpret_cast<const float4*>(q + (long long)qi * d)[c];
+    for (int r = 0; r < n; ++r) {
+      const long long j = idx[(long long)qi * k + r] - idx_offset;
+      if (j < 0) continue;
+      const float s = sc[(long long)qi * k + r];
+      const float w = s > 0.f ? powf(s, alpha) : 0.f;
+      const float4 v = reinterpret_cast<const float4*>(g + j * d)[c];
+      acc.x = fmaf(w, v.x, acc.x);
+      acc.y = fmaf(w, v.y, acc.y);
+      acc.z = fmaf(w, v.z, acc.z);
+      acc.w = fmaf(w, v.w, acc.w);
+    }
+    reinterpret_cast<float4*>(out + (long long)qi * d)[c] = acc;
+    ss = fmaf(acc.x, acc.x, fmaf(acc.y, acc.y, fmaf(acc.z, acc.z, fmaf(acc.w, acc.w, ss))));
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = ss;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float inv = 1.0f / fmaxf(sqrtf(tot), 1e-12f);
+  for (int c = threadIdx.x; c < d4; c += 256) {
+    float4 v = reinterpret_cast<float4*>(out + (long long)qi * d)[c];
+    v.x *= inv;
+    v.y *= inv;
+    v.z *= inv;
+    v.w *= inv;
+    reinterpret_cast<float4*>(out + (long long)qi * d)[c] = v;
+  }
+}
+}  // namespace rr
+
+extern "C" int rr_alpha_qe(rr_handle_t h, const float* queries, int nq, const float* gallery, int d,
+                           const long long* top_idx, const float* top_scores, int k, int n, float alpha,
+                           long long idx_offset, float* out, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!queries || !gallery || !top_idx || !top_scores || !out || nq < 0 || d <= 0 || (d & 3) || k <= 0 || n < 0 ||
+      n > k || ((uintptr_t)queries & 15) || ((uintptr_t)gallery & 15) || ((uintptr_t)out & 15))
+    return set_error(h, RR_EINVAL, "rr_alpha_qe: bad argument (d % 4 == 0, 0 <= n <= k, 16-B aligned rows)");
+  if (nq == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  hipLaunchKernelGGL(alpha_qe_kernel, dim3((unsigned)nq), dim3(256), 0, s, queries, gallery, top_idx, top_scores, k,
+                     n, d, alpha, idx_offset, out);
+  return check_hip(h, hipGetLastError(), "alpha_qe launch");
+}

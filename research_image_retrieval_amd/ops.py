@@ -365,3 +365,18 @@ def attention_bf16(qkv, b, seq, heads, head_dim=64):
     _lib.check(_lib.lib().rr_attention_ex(hd, _ptr(qkv), b, seq, heads, head_dim, 1, _ptr(out), _stream(dev)), hd,
                "rr_attention_ex")
     return out
+
+
+def alpha_qe(queries, gallery, top_idx, top_scores, n=2, alpha=3.0, idx_offset=0):
+    """alpha-QE new queries (see include/rr.h rr_alpha_qe)."""
+    _f32(queries, "alpha_qe queries")
+    _f32(gallery, "alpha_qe gallery")
+    dev = _dev(queries)
+    nq, d = queries.shape
+    k = top_idx.shape[1]
+    out = torch.empty_like(queries)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_alpha_qe(hd, _ptr(queries), nq, _ptr(gallery), d, _ptr(top_idx.contiguous()),
+                                      _ptr(top_scores.contiguous()), k, int(n), float(alpha), int(idx_offset),
+                                      _ptr(out), _stream(dev)), hd, "rr_alpha_qe")
+    return out

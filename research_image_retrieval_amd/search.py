@@ -85,3 +85,15 @@ def search(qvecs, vecs, k=None, return_scores=False, device="cuda", normalize=Tr
     s, i = s.cpu().numpy(), i.cpu().numpy()
     ranks = i.T.copy() if k is None else [row for row in i]
     return (ranks, s) if return_scores else ranks
+
+
+def alpha_qe_search(searcher, queries, k=100, n=2, alpha=3.0, normalize=True):
+    """Search, alpha-QE the queries with their top-n, search again (config C5).
+    Returns (scores, idx) of the second search and the expanded queries."""
+    q = _dev_f32(queries, searcher.device)
+    if normalize:
+        q = ops.l2_normalize(q, 1e-12)
+    s, i = searcher.topk(q, max(k, n), normalize=False)
+    q2 = ops.alpha_qe(q, searcher.gallery, i, s, n=n, alpha=alpha, idx_offset=searcher.idx_offset)
+    s2, i2 = searcher.topk(q2, k, normalize=False)
+    return s2, i2, q2

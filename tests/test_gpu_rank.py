@@ -68,3 +68,18 @@ def test_topk_merge_matches_oracle(cuda):
     sr, ir = oracle.topk_merge(ps, pi, kout)
     np.testing.assert_array_equal(io.cpu().numpy(), ir)
     np.testing.assert_array_equal(so.cpu().numpy(), sr)
+
+
+def test_alpha_qe_vs_oracle(cuda):
+    from research_image_retrieval_amd.search import GallerySearcher, alpha_qe_search
+    rng = np.random.RandomState(9)
+    q = _normed(rng, 12, 256)
+    g = _normed(rng, 20000, 256)
+    srch = GallerySearcher(g, device=cuda, normalize=False)
+    s, i = srch.topk(q, 10, normalize=False)
+    q2 = ops.alpha_qe(torch.from_numpy(q).to(cuda), srch.gallery, i, s, n=3, alpha=3.0).cpu().numpy()
+    q2_ref = oracle.alpha_qe(q, g, i.cpu().numpy(), s.cpu().numpy(), n=3, alpha=3.0)
+    np.testing.assert_allclose(q2, q2_ref, rtol=0, atol=2e-6)
+    s2, i2, _ = alpha_qe_search(srch, q, k=10, n=3, alpha=3.0, normalize=False)
+    s2r, i2r = oracle.cosine_topk(q2, g, 10)
+    assert (i2.cpu().numpy() == i2r).mean() > 0.99  # q2 differs from the oracle's by <= 2e-6
