@@ -121,6 +121,19 @@ int rr_alpha_qe(rr_handle_t h, const float* queries, int nq,
                 const float* top_scores, int k, int n, float alpha,
                 long long idx_offset, float* out, void* stream);
 
+/* PCA-whitening learning, GPU half (replaces the
+ * m = X.mean(0), Xc = X - m, np.dot(Xc.T, Xc) lines of
+ * networks/backbone.py:46-49, called from networks/spca.py:215-217):
+ *   mean_out [d]   fp64 column means of X [n][d] (fp32, row-major, device)
+ *   gram_out [d*d] fp64 sum_i (x_i - m)(x_i - m)^T, symmetric (device)
+ * fp32 MFMA partials over <= 8192-row slices, summed in fp64.  The caller
+ * symmetrises / scales by 1/(2n) and runs the eigendecomposition on the host
+ * (backbone.py:50-57).  Workspace is bounded (<= 131072-row chunks).          */
+size_t rr_pcaw_gram_workspace_size(long long n, int d);
+int rr_pcaw_gram(rr_handle_t h, const float* x, long long n, int d,
+                 void* workspace, size_t workspace_bytes, double* mean_out,
+                 double* gram_out, void* stream);
+
 /* ---- embed (extractor) ---------------------------------------------------
  * uint8 HWC pixels -> fp32 NHWC, (x/255 - mean[c]) / std[c].
  * Replaces transforms.ToTensor + Normalize(mean=[.485,.456,.406],

@@ -79,6 +79,24 @@ def gem_model_descriptor(x, sd, layers, proj_w, proj_b, p=3.0):
     return F.normalize(f, p=2, dim=1)
 
 
+def pcawhitenlearn_ref(X, s=1.0):
+    """CPU restatement of pcawhitenlearn_shrinkage (networks/backbone.py:42-58),
+    in X's dtype with numpy: m = X.mean(0); Xc = X - m; Xcov = Xc^T Xc,
+    symmetrised / 2N; np.linalg.eig; descending order; P = diag(lam^(s/2))^-1 V^T.
+    Returns (m [1,D], P^T)."""
+    import numpy as np
+    n = X.shape[0]
+    m = X.mean(axis=0, keepdims=True)
+    xc = X - m
+    cov = xc.T @ xc
+    cov = (cov + cov.T) / (2 * n)
+    lam, vec = np.linalg.eig(cov)
+    order = np.argsort(lam)[::-1]
+    lam, vec = lam[order], vec[:, order]
+    proj = np.linalg.inv(np.diag(np.power(lam, 0.5 * s))) @ vec.T
+    return m, proj.T
+
+
 def pcaw_apply(x, w, b):
     """ConvDimReduction forward on [B,D] descriptors, then F.normalize."""
     return F.normalize(F.linear(x, w, b), dim=-1)

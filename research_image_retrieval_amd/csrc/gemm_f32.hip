@@ -88,7 +88,14 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
 
   const int slot = tid % SLOTS;
   const int crow = tid / SLOTS;
-  const int K = g.K;
+  int K = g.K;
+  long long koff = 0;
+  float* const Cb = g.C + (g.k_split > 0 ? (long long)blockIdx.y * g.c_split_stride : 0LL);
+  if (g.k_split > 0) {
+    koff = (long long)blockIdx.y * g.k_split;
+    K = (int)(g.K - koff < g.k_split ? g.K - koff : g.k_split);
+  }
+  if (g.sym && m0 > n0 + BN - 1) return;  // block-uniform, before any barrier
   const int nk = (K + EPR - 1) / EPR;
 
   // ---- per-chunk A row state ----
@@ -100,7 +107,7 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
     const int m = m0 + crow + i * ROWS_PER_PASS;
     a_ok[i] = m < g.M;
     if constexpr (AMODE == A_DENSE) {
-      a_ptr[i] = reinterpret_cast<const ET*>(g.A) + (long long)(a_ok[i] ? m : 0) * g.lda;
+      a_ptr[i] = reinterpret_cast<const ET*>(g.A) + (long long)(a_ok[i] ? m : 0) * g.lda + koff;
       a_ih0[i] = 0;
       a_iw0[i] = 0;
     } else {
@@ -121,7 +128,7 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
   for (int i = 0; i < B_CH; ++i) {
     const int n = n0 + crow + i * ROWS_PER_PASS;
     b_ok[i] = n < g.N;
-    b_ptr[i] = reinterpret_cast<const ET*>(g.B) + (long long)(b_ok[i] ? n : 0) * g.ldb;
+    b_ptr[i] = reinterpret_cast<const ET*>(g.B) + (long long)(b_ok[i] ? n : 0) * g.ldb + koff;
   }
 
   f32x4 ra[A_CH], rb[B_CH];
@@ -429,9 +436,9 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
           if (g.out_bf16) {
             typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
             const bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-            *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(g.C) + (long long)m * g.ldc + n) = o;
+            *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(Cb) + (long long)m * g.ldc + n) = o;
           } else {
-            *reinterpret_cast<f32x4*>(g.C + (long long)m * g.ldc + n) = v;
+            *reinterpret_cast<f32x4*>(Cb + (long long)m * g.ldc + n) = v;
           }
         }
       } else {
@@ -451,9 +458,9 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
             else if (g.relu == 2) x = quick_gelu(x);
             if (g.out_bf16) {
               const __bf16 xb = (__bf16)x;
-              reinterpret_cast<__bf16*>(g.C)[o + e] = xb;
+              reinterpret_cast<__bf16*>(Cb)[o + e] = xb;
             } else {
-              g.C[o + e] = x;
+              Cb[o + e] = x;
             }
           }
         }
@@ -470,8 +477,9 @@ static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, AM, EM, BK, DT>), dim3((unsigned)nblk), dim3(64 * WM * WN), 0, s, g,
-                     (int)tiles_n);
+  const unsigned splits = g.k_split > 0 ? (unsigned)((g.K + g.k_split - 1) / g.k_split) : 1u;
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, AM, EM, BK, DT>), dim3((unsigned)nblk, splits), dim3(64 * WM * WN), 0, s,
+                     g, (int)tiles_n);
   return hipGetLastError();
 }
 
@@ -556,6 +564,9 @@ int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStre
   if (amode != A_CONV_GENERIC && (g.ldb & 3) != 0) return set_error(h, RR_EINVAL, "gemm: ldb must be a multiple of 4");
   if (emode == E_SCORES_T && (g.ldc & 3)) return set_error(h, RR_EINVAL, "gemm: ldc must be a multiple of 4");
   if (amode == A_CONV && (g.Cin % 32) != 0) return set_error(h, RR_EINVAL, "gemm: A_CONV needs Cin % 32 == 0");
+  if ((g.k_split > 0 || g.sym) && (amode != A_DENSE || emode != E_STORE))
+    return set_error(h, RR_EINVAL, "gemm: split-K / symmetric mode needs dense A and a stored C");
+  if (g.k_split > 0 && (g.k_split % 32) != 0) return set_error(h, RR_EINVAL, "gemm: k_split must be a multiple of 32");
   if (g.M == 0 || g.N == 0) return RR_OK;
   hipError_t e = hipSuccess;
   {

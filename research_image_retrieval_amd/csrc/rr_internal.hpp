@@ -97,6 +97,11 @@ struct GemmArgs {
   const float* scale_a = nullptr;  // [M]
   const float* scale_b = nullptr;  // [N]
   int out_bf16 = 0;                // E_STORE: write bf16 instead of fp32
+  // split-K (dense A, E_STORE): blockIdx.y = split s covers k in
+  // [s*k_split, (s+1)*k_split) and stores its partial C at C + s*c_split_stride
+  int k_split = 0;
+  long long c_split_stride = 0;
+  int sym = 0;  // E_STORE of a symmetric product: skip tiles strictly below the diagonal
 };
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,

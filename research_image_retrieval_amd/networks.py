@@ -151,7 +151,7 @@ class ConvDimReduction:
     def initialize_pca_whitening(self, des):
         """Fit (m, P) on descriptors des [N, input_dim] (numpy), exactly as
         pcawhitenlearn_shrinkage (networks/backbone.py:42-58) + spca.py:215-227."""
-        m, P = pcawhitenlearn_shrinkage(np.asarray(des))
+        m, P = pcawhitenlearn_shrinkage(des, device=self.device)
         m, P = m.T, P.T
         self.weight = torch.tensor(P[: self.dim, :], dtype=torch.float32).contiguous().to(self.device)
         shift = -torch.mm(torch.tensor(P, dtype=torch.float32), torch.tensor(m, dtype=torch.float32)).squeeze()
@@ -168,23 +168,31 @@ class ConvDimReduction:
         return ops.linear(x, self.weight, self.bias)
 
 
-def pcawhitenlearn_shrinkage(X, s=1.0):
-    """PCA whitening with shrinkage, restating networks/backbone.py:42-58 on the
-    host: symmetrised covariance of the centred descriptors, LAPACK geev
-    (np.linalg.eig, as the reference, so eigenvector signs agree), components in
-    descending eigenvalue order, projection scaled by lambda^(-s/2).
-    Returns (mean [1,D], P^T [D,D])."""
-    n = X.shape[0]
-    mean = X.mean(axis=0, keepdims=True)
-    centred = X - mean
-    gram = centred.T @ centred
-    cov = (gram + gram.T) / (2 * n)
+def pcawhitenlearn_shrinkage(X, s=1.0, device="cuda"):
+    """PCA whitening with shrinkage (networks/backbone.py:42-58).
+
+    The O(n d^2) part — column mean and centred Gram Xc^T Xc — runs on the GPU
+    (rr_pcaw_gram: fp32 MFMA over 8192-row slices, fp64 sums).  The d x d tail
+    stays on the host exactly as the reference writes it: symmetrise / 2n,
+    LAPACK geev (np.linalg.eig, so eigenvector signs follow the reference's
+    solver), descending eigenvalue order, projection scaled by lambda^(-s/2),
+    in X's floating dtype.  Returns (mean [1,D], P^T [D,D])."""
+    if isinstance(X, torch.Tensor):
+        dt = np.float64 if X.dtype == torch.float64 else np.float32
+    else:
+        X = np.asarray(X)
+        dt = X.dtype if X.dtype in (np.float32, np.float64) else np.float32
+    x = torch.as_tensor(X).to(device=device, dtype=torch.float32).contiguous()
+    n = x.shape[0]
+    mean64, gram = ops.pcaw_gram(x)
+    gram = gram.cpu().numpy()
+    cov = ((gram + gram.T) / (2 * n)).astype(dt)
     lam, vec = np.linalg.eig(cov)
     desc = np.argsort(lam)[::-1]
     lam, vec = lam[desc], vec[:, desc]
     # np.power, not `**`: numpy turns `x ** 0.5` into sqrt, 1 ulp off pow
     proj = np.linalg.inv(np.diag(np.power(lam, 0.5 * s))) @ vec.T
-    return mean, proj.T
+    return mean64.cpu().numpy()[None, :].astype(dt), proj.T
 
 
 class GeMPCAw(_Extractor):

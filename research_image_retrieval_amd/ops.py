@@ -380,3 +380,22 @@ def alpha_qe(queries, gallery, top_idx, top_scores, n=2, alpha=3.0, idx_offset=0
                                       _ptr(top_scores.contiguous()), k, int(n), float(alpha), int(idx_offset),
                                       _ptr(out), _stream(dev)), hd, "rr_alpha_qe")
     return out
+
+
+def pcaw_gram(x):
+    """Column mean and centred Gram sum_i (x_i - m)(x_i - m)^T of fp32 rows
+    x [n, d] on the device (include/rr.h rr_pcaw_gram) -> (mean fp64 [d],
+    gram fp64 [d, d])."""
+    _f32(x, "pcaw_gram")
+    dev = _dev(x)
+    n, d = x.shape
+    if n == 0:
+        raise ValueError("pcaw_gram: empty descriptor set")
+    L = _lib.lib()
+    ws = torch.empty(L.rr_pcaw_gram_workspace_size(n, d), dtype=torch.uint8, device=dev)
+    mean = torch.empty(d, dtype=torch.float64, device=dev)
+    gram = torch.empty((d, d), dtype=torch.float64, device=dev)
+    hd = _lib.handle(dev)
+    _lib.check(L.rr_pcaw_gram(hd, _ptr(x), n, d, _ptr(ws), ws.numel(), _ptr(mean), _ptr(gram), _stream(dev)),
+               hd, "rr_pcaw_gram")
+    return mean, gram

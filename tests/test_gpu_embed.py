@@ -149,3 +149,45 @@ def test_resize_bilinear_matches_torch(cuda):
         got = ops.resize_bilinear(x.permute(0, 2, 3, 1).contiguous().to(cuda), ref.shape[2], ref.shape[3],
                                   scale_factor=s).permute(0, 3, 1, 2).cpu()
         torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-5)
+
+
+# ---- PCA-whitening learning -------------------------
+
+@pytest.mark.parametrize("n,d", [(1000, 98), (2000, 64), (300_000, 512)])
+def test_pcaw_gram_vs_float64(cuda, n, d):
+    """rr_pcaw_gram (GPU mean + centred Gram, fp32 MFMA partials over 8192-row
+    slices summed in fp64) against float64 numpy on the same fp32 inputs; the
+    300k case spans three 131072-row chunks with a ragged last one."""
+    rs = np.random.RandomState(n + d)
+    A = rs.standard_normal((d, d)).astype(np.float32) / np.sqrt(d)
+    X = (rs.standard_normal((n, d)).astype(np.float32) @ A + rs.standard_normal(d).astype(np.float32)).astype(np.float32)
+    mean, gram = ops.pcaw_gram(torch.from_numpy(X).to(cuda))
+    X64 = X.astype(np.float64)
+    m_ref = X64.mean(0)
+    xc = X64 - m_ref
+    g_ref = xc.T @ xc
+    np.testing.assert_allclose(mean.cpu().numpy(), m_ref, rtol=0, atol=1e-12 * n + 1e-9)
+    g = gram.cpu().numpy()
+    assert np.array_equal(g, g.T)
+    # fp32 centring (x - fp32(m)) + fp32 fmaf chains of <= 8192 terms
+    err = np.abs(g - g_ref).max() / np.abs(np.diag(g_ref)).max()
+    assert err < 5e-6, err
+
+
+def test_pcaw_learn_vs_reference_fixture(cuda):
+    """GPU-learned PCA-w vs the reference's pcawhitenlearn_shrinkage output on
+    its fixture.  Eigenvector signs are LAPACK-arbitrary (a 1-ulp change of
+    the covariance flips them), so rows are compared sign-aligned; the
+    whitened-descriptor Gram matrix, which retrieval sees, is sign-invariant."""
+    from research_image_retrieval_amd.networks import ConvDimReduction, pcawhitenlearn_shrinkage
+    fx = np.load(os.path.join(GOLD, "pcaw.npz"))
+    m, PT = pcawhitenlearn_shrinkage(fx["X"], device=cuda)
+    np.testing.assert_allclose(m, fx["mean"], rtol=0, atol=1e-6)
+    P, Pr = PT.T, fx["PT"].T
+    sg = np.sign((P * Pr).sum(1))
+    top = np.abs(P * sg[:, None] - Pr)[:32].max() / np.abs(Pr[:32]).max()
+    assert top < 1e-5, top  # the 32 components the fixture's ConvDimReduction keeps
+    cdr = ConvDimReduction(64, 32, device=cuda)
+    cdr.initialize_pca_whitening(fx["X"])
+    y = ops.l2_normalize(cdr(torch.from_numpy(fx["Y"]).to(cuda)), 1e-12).cpu().numpy()
+    np.testing.assert_allclose(y @ y.T, fx["y"] @ fx["y"].T, rtol=0, atol=1e-5)

@@ -72,16 +72,19 @@ def test_oracle_extractor_tails():
 
 
 def test_pca_whitening_learn_matches_reference():
-    from research_image_retrieval_amd.networks import ConvDimReduction, pcawhitenlearn_shrinkage
+    """The oracle's restatement of pcawhitenlearn_shrinkage + ConvDimReduction
+    (networks/backbone.py:42-58, networks/spca.py:215-227) against the
+    reference's own outputs, bit-exact."""
     fx = load("pcaw")
-    m, PT = pcawhitenlearn_shrinkage(fx["X"])
+    m, PT = embed_ref.pcawhitenlearn_ref(fx["X"])
     np.testing.assert_array_equal(m, fx["mean"])
     np.testing.assert_array_equal(PT, fx["PT"])
-    cdr = ConvDimReduction(64, 32, device="cpu")
-    cdr.initialize_pca_whitening(fx["X"])
-    np.testing.assert_array_equal(cdr.weight.numpy(), fx["w"].reshape(32, 64))
-    np.testing.assert_array_equal(cdr.bias.numpy(), fx["b"])
-    y = embed_ref.pcaw_apply(torch.from_numpy(fx["Y"]), cdr.weight, cdr.bias)
+    P = PT.T
+    w = torch.tensor(P[:32, :], dtype=torch.float32)
+    b = -torch.mm(torch.tensor(P, dtype=torch.float32), torch.tensor(m.T, dtype=torch.float32)).squeeze()[:32]
+    np.testing.assert_array_equal(w.numpy(), fx["w"].reshape(32, 64))
+    np.testing.assert_array_equal(b.numpy(), fx["b"])
+    y = embed_ref.pcaw_apply(torch.from_numpy(fx["Y"]), w, b)
     np.testing.assert_allclose(y.numpy(), fx["y"], rtol=0, atol=1e-6)
 
 
