@@ -1,6 +1,8 @@
 """Deterministic inputs for the golden fixtures (numpy RandomState streams are
 stable across numpy versions), shared by make_golden.py and the tests so large
 inputs are regenerated from seeds instead of being committed."""
+import os
+
 import numpy as np
 import torch
 import torch.nn.functional as F
@@ -112,3 +114,48 @@ def vit_state_dict(seed, width, layers, heads, patch, res, out_dim):
     sd["ln_post.bias"] = t(0.1 * rs.standard_normal(width))
     sd["proj"] = t(rs.standard_normal((width, out_dim)) * sc)
     return sd
+
+
+def loader_images(seed=61):
+    """Deterministic RGB images of assorted sizes and aspect ratios (uint8
+    HWC): smooth gradients plus noise, so resampling filters matter."""
+    rs = np.random.RandomState(seed)
+    out = []
+    for h, w in [(97, 130), (240, 180), (64, 64), (333, 211), (150, 401)]:
+        yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+        base = np.stack([(np.sin(xx / (7 + 3 * c)) + np.cos(yy / (5 + 2 * c))) * 60 + 128 for c in range(3)], -1)
+        out.append(np.clip(base + rs.randint(-30, 31, size=(h, w, 3)), 0, 255).astype(np.uint8))
+    return out
+
+
+# query boxes (x0, y0, x1, y1) in the revisitop gnd['bbx'] convention (floats)
+LOADER_BBOXES = [(10.5, 7.25, 120.0, 90.0), (0.0, 0.0, 180.0, 240.0), (3.0, 5.0, 40.0, 61.0),
+                 (50.2, 20.7, 200.9, 300.1), (100.0, 10.0, 390.5, 149.0)]
+
+
+def write_pngs(imgs, directory):
+    from PIL import Image
+    paths = []
+    for i, a in enumerate(imgs):
+        p = os.path.join(directory, f"img{i}.png")
+        Image.fromarray(a).save(p)
+        paths.append(p)
+    return paths
+
+
+def write_fake_revisited(root, name="roxford5k"):
+    """A 5-image revisitop-layout dataset (jpg/ + gnd_<name>.pkl) with two
+    bbox queries, for the loader / full-resolution extraction tests."""
+    import pickle
+    from PIL import Image
+    d = os.path.join(root, name, "jpg")
+    os.makedirs(d)
+    for i, a in enumerate(loader_images(61)):
+        Image.fromarray(a).save(os.path.join(d, f"im{i}.jpg"), quality=95)
+    e = np.array([], dtype=np.int64)
+    gnd = [{"bbx": np.array(LOADER_BBOXES[0]), "easy": np.array([1, 3]), "hard": np.array([4]), "junk": e},
+           {"bbx": np.array(LOADER_BBOXES[3]), "easy": np.array([0]), "hard": e, "junk": np.array([2])}]
+    cfg = {"imlist": [f"im{i}" for i in range(5)], "qimlist": ["im0", "im3"], "gnd": gnd}
+    with open(os.path.join(root, name, f"gnd_{name}.pkl"), "wb") as f:
+        pickle.dump(cfg, f)
+    return cfg

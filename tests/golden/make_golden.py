@@ -29,11 +29,40 @@ def _stub_torchvision():
     tv.transforms.functional = tvf
     sys.modules.update({"torchvision": tv, "torchvision.models": tv.models, "torchvision.transforms": tv.transforms,
                         "torchvision.transforms.functional": tvf})
+    # lmdb (GLDv2 training reader, dataset/configdataset.py:13) is absent too;
+    # the dataset package imports it at top level, nothing below uses it
+    sys.modules.setdefault("lmdb", types.ModuleType("lmdb"))
+
+
+def loader_fixture():
+    """(viii) ImageFromList (dataset/ImageFromList.py:30-57): full-size, thumbnail
+    and query-bbox crops.  Pillow >= 10 has no Image.ANTIALIAS, on which the
+    reference's imthumbnail crashes; it was an alias of
+    LANCZOS in the Pillow versions the code was written for, restored here."""
+    import tempfile
+    from PIL import Image
+    if not hasattr(Image, "ANTIALIAS"):
+        Image.ANTIALIAS = Image.LANCZOS
+    from dataset.ImageFromList import ImageFromList
+    imgs = I.loader_images(61)
+    out = {}
+    with tempfile.TemporaryDirectory() as d:
+        paths = I.write_pngs(imgs, d)
+        for imsize in (None, 100, 57):
+            for use_bb in (0, 1):
+                ds = ImageFromList(paths, imsize=imsize, bbox=I.LOADER_BBOXES if use_bb else None)
+                for i in range(len(ds)):
+                    out[f"im{imsize}_b{use_bb}_{i}"] = np.asarray(ds[i])
+    np.savez_compressed(os.path.join(HERE, "loader.npz"), seed=61, **out)
 
 
 def main():
     _stub_torchvision()
     sys.path.insert(0, REF)
+    if "--only-loader" in sys.argv:
+        loader_fixture()
+        return
+    loader_fixture()
     from networks.RetrievalNet import gem, GeM
     from networks.backbone import pcawhitenlearn_shrinkage
     from networks.spca import ConvDimReduction

@@ -191,3 +191,31 @@ def test_pcaw_learn_vs_reference_fixture(cuda):
     cdr.initialize_pca_whitening(fx["X"])
     y = ops.l2_normalize(cdr(torch.from_numpy(fx["Y"]).to(cuda)), 1e-12).cpu().numpy()
     np.testing.assert_allclose(y @ y.T, fx["y"] @ fx["y"].T, rtol=0, atol=1e-5)
+
+
+# ---- revisited protocol at full resolution ----------
+
+def test_revisited_fullres_extraction_and_map(cuda, tmp_path):
+    """gnd config -> bbox-cropped / thumbnailed variable-size queries and
+    gallery (dataset.py) -> batch-1 GPU extraction -> full ranks -> revisited
+    mAP, against the oracle's CPU extractor on the same decoded pixels."""
+    from research_image_retrieval_amd import dataset as D
+    I.write_fake_revisited(str(tmp_path))
+    cfg = D.RoxfordAndRparis("roxford5k", str(tmp_path))
+    ql, gl = D.revisited_loaders(cfg, imsize=160, num_workers=0)
+    net = GeM(2048, backbone="resnet50", seed=5, device=cuda)
+    qv = extract_vectors(net, ql, device=cuda, print_freq=0).numpy()
+    gv = extract_vectors(net, gl, device=cuda, print_freq=0).numpy()
+    sd = W.synthetic_resnet_state_dict("resnet50", 5)
+    ww, wb = W.synthetic_linear(2048, 2048, 6)
+    fwd = lambda x: embed_ref.gem_net_forward_test(x, sd, W.RESNET_LAYERS["resnet50"], ww, wb)  # noqa: E731
+    qr = embed_ref.extract_vectors_ref(fwd, [embed_ref.normalize_u8(b) for b in ql]).numpy()
+    gr = embed_ref.extract_vectors_ref(fwd, [embed_ref.normalize_u8(b) for b in gl]).numpy()
+    assert qv.shape == (2, 2048) and gv.shape == (5, 2048)
+    assert np.abs(qv - qr).max() < DESC_TOL and np.abs(gv - gr).max() < DESC_TOL
+    ranks = search(qv, gv, k=None, device=cuda)
+    ranks_ref = oracle.argsort_stable_desc(oracle.cosine_scores(qr, gr)).T
+    assert np.array_equal(ranks, ranks_ref)
+    got = compute_map_and_print("roxford5k", "gpu", "global", ranks, cfg["gnd"])
+    ref = compute_map_and_print("roxford5k", "ref", "global", ranks_ref, cfg["gnd"])
+    assert got == ref
