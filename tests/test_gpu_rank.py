@@ -83,3 +83,20 @@ def test_alpha_qe_vs_oracle(cuda):
     s2, i2, _ = alpha_qe_search(srch, q, k=10, n=3, alpha=3.0, normalize=False)
     s2r, i2r = oracle.cosine_topk(q2, g, 10)
     assert (i2.cpu().numpy() == i2r).mean() > 0.99  # q2 differs from the oracle's by <= 2e-6
+
+
+def test_descriptor_store_to_hbm_and_search(cuda, tmp_path):
+    """Gallery streamed from the on-disk store (pinned double buffer, side
+    stream) equals the source rows bit for bit and ranks like the oracle."""
+    from research_image_retrieval_amd import store as S
+    rs = np.random.RandomState(77)
+    g = rs.standard_normal((70_001, 128)).astype(np.float32)
+    q = rs.standard_normal((9, 128)).astype(np.float32)
+    st = S.write_store(str(tmp_path / "g"), g, shard_rows=20_000)
+    dev_g = st.to_device(0, st.n, cuda, chunk_rows=8192)
+    assert torch.equal(dev_g.cpu(), torch.from_numpy(g))
+    part, lo = S.load_gallery_shard(st, 1, 3, cuda)
+    assert torch.equal(part.cpu(), torch.from_numpy(g[lo:lo + part.shape[0]]))
+    s, i = ops.cosine_topk(torch.from_numpy(q).to(cuda), dev_g, 50)
+    s_o, i_o = oracle.cosine_topk(q, g, 50)
+    assert np.array_equal(i.cpu().numpy(), i_o) and np.array_equal(s.cpu().numpy(), s_o)
