@@ -153,6 +153,9 @@ def main():
                          "c5: c3 extractor at 3 scales + fp8 cosine + alpha-QE re-rank (1 GPU)")
     ap.add_argument("--dtype", choices=("fp32", "bf16", "fp8"), default=None,
                     help="GEMM input dtype (default: fp32 for c3, bf16 for c4)")
+    ap.add_argument("--ranker", choices=("exhaustive", "prefilter"), default="exhaustive",
+                    help="fp32 exact ranking: exhaustive fp32 MFMA sweep, or the bf16-bound prefilter + exact "
+                         "fp32 rescoring (bit-identical results)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
     if a.workload == "c4":
@@ -204,8 +207,14 @@ def main():
     rs = np.random.RandomState(1234 + rank)
     imgs = torch.from_numpy(rs.randint(0, 256, size=(a.batch, 224, 224, 3), dtype=np.uint8)).to(dev)
     q_total = a.batch * world
-    ws = torch.empty(ops.cosine_topk_workspace_size(q_total, hi - lo, a.dim, a.k), dtype=torch.uint8, device=dev)
-    sharded = ShardedGallery(gallery, lo, workspace=ws, dtype=a.dtype) if world > 1 else None
+    pre = a.ranker == "prefilter" and a.dtype == "fp32"
+    wsize = ops.cosine_topk_prefilter_workspace_size if pre else ops.cosine_topk_workspace_size
+    ws = torch.empty(wsize(q_total, hi - lo, a.dim, a.k), dtype=torch.uint8, device=dev)
+    sharded = ShardedGallery(gallery, lo, workspace=ws, dtype=a.dtype, prefilter=pre) if world > 1 else None
+    gal_bf, gal_bound = (None, None)
+    if pre and world == 1:
+        gal_bf, _ = ops.quantize_rows(gallery, "bf16")
+        gal_bound = ops.prefilter_gallery_bound(gallery, gal_bf)
     gal_lp, gal_sc = ops.quantize_rows(gallery, a.dtype) if (a.dtype != "fp32" and world == 1) else (None, None)
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: shard [{lo},{hi}) x {a.dim}, batch {a.batch}")
@@ -238,11 +247,21 @@ def main():
         if gal_lp is not None:
             q_lp, q_sc = ops.quantize_rows(desc, a.dtype)
             return ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws)
+        if gal_bf is not None:
+            return ops.cosine_topk_prefilter(desc, gallery, gal_bf, gal_bound, a.k, idx_offset=lo, workspace=ws)
         return ops.cosine_topk(desc, gallery, a.k, idx_offset=lo, workspace=ws)
 
     for _ in range(a.warmup):
         out = step()
     torch.cuda.synchronize()
+    if gal_bf is not None:  # the prefilter must reproduce the exhaustive fp32 ranking bit for bit
+        d0 = embed()
+        s_p, i_p = ops.cosine_topk_prefilter(d0, gallery, gal_bf, gal_bound, a.k, idx_offset=lo, workspace=ws)
+        s_p, i_p = s_p.clone(), i_p.clone()
+        s_x, i_x = ops.cosine_topk(d0, gallery, a.k, idx_offset=lo, workspace=ws)
+        assert torch.equal(i_p, i_x) and torch.equal(s_p.view(torch.int32), s_x.view(torch.int32)), \
+            "prefilter ranking differs from the exhaustive fp32 ranking"
+        log("[rank 0] prefilter == exhaustive fp32 ranking on this batch (bit-exact)")
     # sanity: a gallery row used as a query must come back first
     chk_s, chk_i = ops.cosine_topk(gallery[:2].contiguous(), gallery, 1, idx_offset=lo, workspace=ws)
     assert chk_i[:, 0].tolist() == [lo, lo + 1], chk_i
@@ -290,13 +309,17 @@ def main():
         conv_flops_img = sum(W.resnet_conv_flops(a.arch, 224, 224).values()) + 2 * 2 * 2048 * 2048  # + whiten, PCA-w
     traffic = load_traffic()
     rk = {}
-    esz = {"fp32": 4, "bf16": 2, "fp8": 1}[a.dtype]
+    rank_dt = "bf16" if pre else a.dtype  # the dtype the gallery sweep runs in
+    esz = {"fp32": 4, "bf16": 2, "fp8": 1}[rank_dt]
     rows_filter = max(0, (hi - lo) - s_rows)
+    if pre:  # the prefilter sweeps every row (the seed rows again) in bf16
+        rows_filter = hi - lo
+        flop_filter = 2.0 * q_total * rows_filter * a.dim
     # (class, algorithmic FLOPs, algorithmic HBM bytes or None, dtype of its MFMA)
     searches = 2 if a.workload == "c5" else 1
-    entries = (("cosine_filter", flop_filter, searches * float(rows_filter) * a.dim * esz, a.dtype),
+    entries = (("cosine_filter", flop_filter, searches * float(rows_filter) * a.dim * esz, rank_dt),
                ("conv_gemm", conv_flops_img * a.batch, None, a.dtype if a.workload == "c4" else "fp32"),
-               ("cosine_seed", flop_seed, searches * float(s_rows) * a.dim * esz, a.dtype),
+               ("cosine_seed", flop_seed, searches * float(s_rows) * a.dim * esz, rank_dt),
                ("attention", attn_flops_img * a.batch, None, "fp32"))
     for name, fl_step, by_step, dt in entries:
         ms, n = cls[name]
@@ -318,7 +341,7 @@ def main():
                   "algorithmic_flop_per_launch": fl_step / max(1.0, n / a.steps),
                   "algorithmic_bytes_per_launch": (by_step / max(1.0, n / a.steps)) if by_step else None,
                   "traffic": ((traffic or {}).get(name) or {}).get("hbm_bytes_per_launch")
-                  if a.workload == "c3" else None})
+                  if (a.workload == "c3" and not pre) else None})
         rk[name] = e
     for name in ("select", "elementwise"):
         ms, n = cls[name]
@@ -336,7 +359,9 @@ def main():
                                    "c4": f"C4: ViT-B/16 CLS {a.dim}-d ({a.dtype} GEMMs + {a.dtype} cosine)",
                                    "c5": f"C5: {a.arch}-GeM+PCA-w at 3 scales, {a.dtype} cosine + alpha-QE "
                                          f"(n=2, alpha=3) re-rank"}[a.workload] +
-                                  f", embed + {'exact' if a.dtype == 'fp32' else a.dtype} top-{a.k} against a {a.gallery}x{a.dim} gallery",
+                                  f", embed + {'exact' if a.dtype == 'fp32' else a.dtype} top-{a.k} against a {a.gallery}x{a.dim} gallery"
+                                  + (" (ranker: bf16-bound prefilter + exact fp32 rescoring, bit-identical to the "
+                                     "exhaustive fp32 ranker)" if pre else ""),
                       "global_batch": q_total,
                       "images_per_gpu_per_step": a.batch, "gallery_rows": a.gallery, "dim": a.dim, "k": a.k,
                       "parallelism": f"query-dp{world} + gallery-shard{world}"},

@@ -121,6 +121,24 @@ int rr_alpha_qe(rr_handle_t h, const float* queries, int nq,
                 const float* top_scores, int k, int n, float alpha,
                 long long idx_offset, float* out, void* stream);
 
+/* Exact cosine top-k through a bf16 prefilter: the SAME scores and indices,
+ * bit for bit, as rr_cosine_topk (iris_evaluate.py:383-386 ranker), with the
+ * full gallery sweep on the bf16 MFMA and only rows that can still reach the
+ * exact top-k rescored with the fp32 core's fmaf chain (proof and bound in
+ * csrc/prefilter.hip).  gallery_bf16 = rr_quantize_rows(gallery, bf16);
+ * bound3 (device, 3 doubles) = rr_prefilter_gallery_bound of the same pair,
+ * computed once per gallery.  d % 8 == 0.                                   */
+int rr_prefilter_gallery_bound(rr_handle_t h, const float* gallery,
+                               const void* gallery_bf16, long long n, int d,
+                               double* bound3, void* stream);
+size_t rr_cosine_topk_prefilter_workspace_size(int nq, long long n, int d, int k);
+int rr_cosine_topk_prefilter(rr_handle_t h, const float* queries, int nq,
+                             const float* gallery, const void* gallery_bf16,
+                             const double* bound3, long long n, int d, int k,
+                             long long idx_offset, float* out_scores,
+                             long long* out_idx, void* workspace,
+                             size_t workspace_bytes, void* stream);
+
 /* PCA-whitening learning, GPU half (replaces the
  * m = X.mean(0), Xc = X - m, np.dot(Xc.T, Xc) lines of
  * networks/backbone.py:46-49, called from networks/spca.py:215-217):

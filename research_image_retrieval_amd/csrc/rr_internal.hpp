@@ -56,6 +56,18 @@ __host__ __device__ inline float unord_f32(uint32_t o) {
   __builtin_memcpy(&f, &u, 4);
   return f;
 }
+// next float toward -inf / +inf (finite inputs; -inf / +inf map to themselves)
+__host__ __device__ inline float next_down(float f) {
+  uint32_t u;
+  __builtin_memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) == 0) u = 0x80000001u;                  // +-0 -> -min denormal
+  else if (u == 0xff800000u || (u & 0x7fffffffu) > 0x7f800000u) {  // -inf, NaN
+  } else if (u & 0x80000000u) ++u;
+  else --u;
+  __builtin_memcpy(&f, &u, 4);
+  return f;
+}
+__host__ __device__ inline float next_up(float f) { return -next_down(-f); }
 __host__ __device__ inline unsigned long long make_key(float s, uint32_t idx) {
   return ((unsigned long long)ord_f32(s) << 32) | (unsigned long long)(~idx);
 }
@@ -117,6 +129,10 @@ int launch_select_dense_seed(rr_handle_s* h, const float* scores_t, long long ld
 int launch_select_final(rr_handle_s* h, const unsigned long long* cand, long long cap,
                         const int* cnt, int nq, int k, long long idx_offset, float* out_scores,
                         long long* out_idx, int* overflow_flag, hipStream_t s);
+// exact bf16-bound prefilter, pass 2: clear keys that cannot reach the exact
+// top-k, rescore the others with the fp32 MFMA core's exact fmaf chain
+int launch_prefilter_rescore(rr_handle_s* h, unsigned long long* cand, long long cap, const int* cnt, int nq, int k,
+                             const float* eps2, const float* q, const float* g, int d, hipStream_t s);
 int launch_merge(rr_handle_s* h, const float* ps, const long long* pi, int nparts, int nq, int kin,
                  int kout, float* os, long long* oi, hipStream_t s);
 

@@ -22,10 +22,13 @@ struct SelShared {
   int digit, above, dcnt, gcount, all;
 };
 
+// MSB-first radix select of the k largest keys: on return, the winners are
+// exactly the keys with (key >> fshift) >= (prefix >> fshift), or every
+// non-zero key when `all` (<= k of them).
 // Src: callable int64 index -> key (0 = empty / padding, never selected)
 template <class Src>
-__device__ int block_select_sort(Src src, long long count, int k, int P, unsigned long long* skeys,
-                                 SelShared& sh) {
+__device__ void block_radix_select(Src src, long long count, int k, SelShared& sh, unsigned long long& prefix_out,
+                                   int& fshift_out, bool& all_out) {
   const int tid = threadIdx.x;
   unsigned long long prefix = 0, mask = 0;
   int remaining = k;
@@ -71,6 +74,19 @@ __device__ int block_select_sort(Src src, long long count, int k, int P, unsigne
     __syncthreads();
     if (done) break;
   }
+  prefix_out = prefix;
+  fshift_out = fshift;
+  all_out = all;
+}
+
+template <class Src>
+__device__ int block_select_sort(Src src, long long count, int k, int P, unsigned long long* skeys,
+                                 SelShared& sh) {
+  const int tid = threadIdx.x;
+  unsigned long long prefix;
+  int fshift;
+  bool all;
+  block_radix_select(src, count, k, sh, prefix, fshift, all);
 
   // gather winners
   if (tid == 0) sh.gcount = 0;
@@ -173,6 +189,86 @@ __global__ __launch_bounds__(SEL_NT) void merge_kernel(const float* __restrict__
   write_out(skeys, nsel, kout, 0, os + (long long)q * kout, oi + (long long)q * kout);
 }
 
+// Exact fp32 score of one gallery row in the order the fp32 MFMA core
+// accumulates it (gemm_f32.hip: within each 16-deep chunk k = 16c + e from
+// lane half 0, then 16c + 8 + e from lane half 1, e = 0..7; k >= d is a zero
+// product, as the zero-padded k-tile is), one fmaf per term: bit-identical to
+// rr_cosine_topk's scores.
+__device__ inline float exact_chain_score(const float* __restrict__ qs, const float* __restrict__ gr, int d) {
+  float acc = 0.f;
+  for (int c = 0; c < d; c += 16) {
+    float gv[16], qv[16];
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      const int kk = c + 4 * v;
+      const float4 x = kk < d ? *reinterpret_cast<const float4*>(gr + kk) : float4{0.f, 0.f, 0.f, 0.f};
+      const float4 y = kk < d ? *reinterpret_cast<const float4*>(qs + kk) : float4{0.f, 0.f, 0.f, 0.f};
+      gv[4 * v] = x.x, gv[4 * v + 1] = x.y, gv[4 * v + 2] = x.z, gv[4 * v + 3] = x.w;
+      qv[4 * v] = y.x, qv[4 * v + 1] = y.y, qv[4 * v + 2] = y.z, qv[4 * v + 3] = y.w;
+    }
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      acc = __builtin_fmaf(gv[e], qv[e], acc);
+      acc = __builtin_fmaf(gv[8 + e], qv[8 + e], acc);
+    }
+  }
+  return acc;
+}
+
+// Pass 2 of the exact bf16-bound prefilter (rr_cosine_topk_prefilter), one
+// block per query.  cand[q][0..cnt) holds (bf16 score, row) keys of every row
+// whose bf16 score passed pass 1.  With s'_k the k-th largest of them and
+// eps2 = 2 * (bound on |exact - bf16| for this query), a row can be in the
+// exact top-k only if s' >= s'_k - eps2: those keys are rescored exactly in
+// place, all others are cleared to 0 (empty); select_final then ranks them.
+__global__ __launch_bounds__(SEL_NT) void prefilter_rescore_kernel(unsigned long long* __restrict__ cand, long long cap,
+                                                                   const int* __restrict__ cnt, int k,
+                                                                   const float* __restrict__ eps2,
+                                                                   const float* __restrict__ q,
+                                                                   const float* __restrict__ g, int d, int dpad) {
+  extern __shared__ __attribute__((aligned(16))) float qs[];
+  __shared__ SelShared sh;
+  __shared__ unsigned long long kmin;
+  const int qi = blockIdx.x;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < dpad; i += SEL_NT) qs[i] = i < d ? q[(long long)qi * d + i] : 0.f;
+  const long long c0 = cnt[qi];
+  const long long c = c0 < cap ? c0 : cap;
+  unsigned long long* cq = cand + (long long)qi * cap;
+  float t2 = -__builtin_inff();
+  if (c > k) {
+    auto src = [&](long long i) -> unsigned long long { return cq[i]; };
+    unsigned long long prefix;
+    int fshift;
+    bool all;
+    block_radix_select(src, c, k, sh, prefix, fshift, all);
+    if (tid == 0) kmin = ~0ull;
+    __syncthreads();
+    const unsigned long long ptop = prefix >> fshift;
+    unsigned long long m = ~0ull;
+    for (long long i = tid; i < c; i += SEL_NT) {
+      const unsigned long long key = cq[i];
+      if (key != 0ull && (all || (key >> fshift) >= ptop) && key < m) m = key;
+    }
+    atomicMin(&kmin, m);
+    __syncthreads();
+    const double t = (double)key_score(kmin) - (double)eps2[qi];
+    t2 = (float)t;
+    if ((double)t2 > t) t2 = next_down(t2);
+  }
+  __syncthreads();
+  for (long long i = tid; i < c; i += SEL_NT) {
+    const unsigned long long key = cq[i];
+    if (key == 0ull) continue;
+    if (key_score(key) >= t2) {
+      const uint32_t row = key_idx(key);
+      cq[i] = make_key(exact_chain_score(qs, g + (long long)row * d, d), row);
+    } else {
+      cq[i] = 0ull;
+    }
+  }
+}
+
 static int pow2_at_least(int k) {
   int p = 1;
   while (p < k) p <<= 1;
@@ -230,6 +326,19 @@ int launch_merge(rr_handle_s* h, const float* ps, const long long* pi, int npart
   TimedLaunch tl(h, kTimeSelect, s);
   hipLaunchKernelGGL(merge_kernel, dim3(nq), dim3(SEL_NT), lds, s, ps, pi, nparts, nq, kin, kout, P, os, oi);
   return check_hip(h, hipGetLastError(), "merge launch");
+}
+
+int launch_prefilter_rescore(rr_handle_s* h, unsigned long long* cand, long long cap, const int* cnt, int nq, int k,
+                             const float* eps2, const float* q, const float* g, int d, hipStream_t s) {
+  if (int rc = check_k(h, k)) return rc;
+  if (nq <= 0) return RR_OK;
+  const int dpad = (d + 15) & ~15;
+  const size_t lds = (size_t)dpad * 4;
+  hipError_t e = set_lds((const void*)prefilter_rescore_kernel, lds);
+  if (e != hipSuccess) return check_hip(h, e, "prefilter_rescore attr");
+  TimedLaunch tl(h, kTimeSelect, s);
+  hipLaunchKernelGGL(prefilter_rescore_kernel, dim3(nq), dim3(SEL_NT), lds, s, cand, cap, cnt, k, eps2, q, g, d, dpad);
+  return check_hip(h, hipGetLastError(), "prefilter_rescore launch");
 }
 
 }  // namespace rr

@@ -59,7 +59,10 @@ def _all_gather_var(t, group):
 class ShardedGallery:
     """This rank's shard of a gallery that is row-partitioned over the group."""
 
-    def __init__(self, shard, global_offset, group=None, local_topk=None, merge=None, workspace=None, dtype="fp32"):
+    def __init__(self, shard, global_offset, group=None, local_topk=None, merge=None, workspace=None, dtype="fp32",
+                 prefilter=False):
+        """dtype "fp32" ranks exactly; prefilter=True gives the same exact
+        result through the bf16-bound prefilter (rr_cosine_topk_prefilter)."""
         self.shard = shard
         self.offset = int(global_offset)
         self.group = group
@@ -67,16 +70,24 @@ class ShardedGallery:
         self._merge = merge
         self._ws = workspace
         self.dtype = dtype
-        self.shard_lp, self.shard_scale = (None, None)
-        if dtype != "fp32" and local_topk is None:
-            self.shard_lp, self.shard_scale = ops.quantize_rows(shard, dtype)
+        self.prefilter = bool(prefilter) and dtype == "fp32"
+        self.shard_lp, self.shard_scale, self.bound = (None, None, None)
+        if local_topk is None and (dtype != "fp32" or self.prefilter):
+            self.shard_lp, self.shard_scale = ops.quantize_rows(shard, "bf16" if self.prefilter else dtype)
+        if self.prefilter and local_topk is None:
+            self.bound = ops.prefilter_gallery_bound(shard, self.shard_lp)
 
     def _local(self, q, k):
         if self._local_topk is not None:
             return self._local_topk(q, self.shard, k, self.offset)
-        need = ops.cosine_topk_workspace_size(q.shape[0], self.shard.shape[0], q.shape[1], k)
+        n, d = self.shard.shape[0], q.shape[1]
+        need = (ops.cosine_topk_prefilter_workspace_size if self.prefilter else ops.cosine_topk_workspace_size)(
+            q.shape[0], n, d, k)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=q.device)
+        if self.prefilter:
+            return ops.cosine_topk_prefilter(q, self.shard, self.shard_lp, self.bound, k, idx_offset=self.offset,
+                                             workspace=self._ws)
         if self.dtype != "fp32":
             q_lp, q_sc = ops.quantize_rows(q, self.dtype)
             return ops.cosine_topk_lp(q_lp, q_sc, self.shard_lp, self.shard_scale, k, self.dtype,

@@ -399,3 +399,38 @@ def pcaw_gram(x):
     _lib.check(L.rr_pcaw_gram(hd, _ptr(x), n, d, _ptr(ws), ws.numel(), _ptr(mean), _ptr(gram), _stream(dev)),
                hd, "rr_pcaw_gram")
     return mean, gram
+
+
+def prefilter_gallery_bound(gallery, gallery_bf16):
+    """Row-norm maxima (|g|, |g - bf16(g)|, |bf16(g)|) as fp64 [3] on the device."""
+    _f32(gallery, "prefilter_gallery_bound")
+    dev = _dev(gallery)
+    n, d = gallery.shape
+    out = torch.empty(3, dtype=torch.float64, device=gallery.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_prefilter_gallery_bound(hd, _ptr(gallery), _ptr(gallery_bf16), n, d, _ptr(out),
+                                                     _stream(dev)), hd, "rr_prefilter_gallery_bound")
+    return out
+
+
+def cosine_topk_prefilter_workspace_size(nq, n, d, k):
+    return int(_lib.lib().rr_cosine_topk_prefilter_workspace_size(nq, n, d, k))
+
+
+def cosine_topk_prefilter(q, g, g_bf16, bound3, k, idx_offset=0, workspace=None):
+    """Exact top-k (bit-identical to cosine_topk) via the bf16 prefilter."""
+    _f32(q, "cosine_topk_prefilter q")
+    _f32(g, "cosine_topk_prefilter g")
+    dev = _dev(q)
+    nq, d = q.shape
+    n = g.shape[0]
+    need = cosine_topk_prefilter_workspace_size(nq, n, d, k)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    s = torch.empty((nq, k), dtype=torch.float32, device=q.device)
+    i = torch.empty((nq, k), dtype=torch.int64, device=q.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_cosine_topk_prefilter(hd, _ptr(q), nq, _ptr(g), _ptr(g_bf16), _ptr(bound3), n, d, k,
+                                                   int(idx_offset), _ptr(s), _ptr(i), _ptr(workspace),
+                                                   workspace.numel(), _stream(dev)), hd, "rr_cosine_topk_prefilter")
+    return s, i

@@ -34,9 +34,12 @@ class GallerySearcher:
     iris_evaluate.py:380); pass False for descriptors that are already unit
     norm (extractor outputs are)."""
 
-    def __init__(self, gallery, device="cuda", normalize=True, idx_offset=0, dtype="fp32"):
+    def __init__(self, gallery, device="cuda", normalize=True, idx_offset=0, dtype="fp32", prefilter=False):
         """dtype "fp32" (exact, default), or "bf16" / "fp8" (configs C4 / C5:
-        the gallery is quantised once; parity vs fp32 is recall@k)."""
+        the gallery is quantised once; parity vs fp32 is recall@k).
+        prefilter=True (fp32, D % 8 == 0): same exact result, bit for bit,
+        through the bf16-bound prefilter (rr_cosine_topk_prefilter); keeps a
+        bf16 copy of the gallery beside the fp32 one."""
         if dtype not in ("fp32", "bf16", "fp8"):
             raise ValueError("dtype must be fp32, bf16 or fp8")
         self.device = torch.device(device)
@@ -44,9 +47,12 @@ class GallerySearcher:
         self.gallery = ops.l2_normalize(g, 1e-12) if normalize else g
         self.idx_offset = int(idx_offset)
         self.dtype = dtype
-        self.gallery_lp, self.gallery_scale = (None, None)
-        if dtype != "fp32":
-            self.gallery_lp, self.gallery_scale = ops.quantize_rows(self.gallery, dtype)
+        self.prefilter = bool(prefilter) and dtype == "fp32" and self.gallery.shape[1] % 8 == 0
+        self.gallery_lp, self.gallery_scale, self.bound = (None, None, None)
+        if dtype != "fp32" or self.prefilter:
+            self.gallery_lp, self.gallery_scale = ops.quantize_rows(self.gallery, "bf16" if self.prefilter else dtype)
+        if self.prefilter:
+            self.bound = ops.prefilter_gallery_bound(self.gallery, self.gallery_lp)
         self._ws = None
 
     @property
@@ -58,9 +64,13 @@ class GallerySearcher:
         q = _dev_f32(queries, self.device)
         if normalize:
             q = ops.l2_normalize(q, 1e-12)
-        need = ops.cosine_topk_workspace_size(q.shape[0], self.n, q.shape[1], k)
+        size = ops.cosine_topk_prefilter_workspace_size if self.prefilter else ops.cosine_topk_workspace_size
+        need = size(q.shape[0], self.n, q.shape[1], k)
         if self._ws is None or self._ws.numel() < need:
             self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        if self.prefilter:
+            return ops.cosine_topk_prefilter(q.contiguous(), self.gallery, self.gallery_lp, self.bound, k,
+                                             idx_offset=self.idx_offset, workspace=self._ws)
         if self.dtype != "fp32":
             q_lp, q_sc = ops.quantize_rows(q.contiguous(), self.dtype)
             return ops.cosine_topk_lp(q_lp, q_sc, self.gallery_lp, self.gallery_scale, k, self.dtype,

@@ -100,3 +100,59 @@ def test_descriptor_store_to_hbm_and_search(cuda, tmp_path):
     s, i = ops.cosine_topk(torch.from_numpy(q).to(cuda), dev_g, 50)
     s_o, i_o = oracle.cosine_topk(q, g, 50)
     assert np.array_equal(i.cpu().numpy(), i_o) and np.array_equal(s.cpu().numpy(), s_o)
+
+
+def _prefilter_vs_exhaustive(cuda, q, g, k, idx_offset=0):
+    qd = torch.from_numpy(q).to(cuda)
+    gd = torch.from_numpy(g).to(cuda)
+    gb, _ = ops.quantize_rows(gd, "bf16")
+    bound = ops.prefilter_gallery_bound(gd, gb)
+    s1, i1 = ops.cosine_topk_prefilter(qd, gd, gb, bound, k, idx_offset=idx_offset)
+    s0, i0 = ops.cosine_topk(qd, gd, k, idx_offset=idx_offset)
+    assert torch.equal(i1, i0)
+    assert torch.equal(s1.view(torch.int32), s0.view(torch.int32))  # bit-identical scores
+    return s1.cpu().numpy(), i1.cpu().numpy()
+
+
+@pytest.mark.parametrize("nq,n,d,k", [(64, 100_000, 512, 100), (7, 50_000, 2048, 100), (33, 40_000, 128, 1000),
+                                      (5, 60, 64, 100), (3, 70_001, 24, 1)])
+def test_prefilter_bitexact_random(cuda, nq, n, d, k):
+    """bf16-bound prefilter + exact rescoring == exhaustive fp32 ranker, bit
+    for bit (scores and indices), incl. n < k and d not a multiple of 16."""
+    rs = np.random.RandomState(n + d)
+    q = rs.standard_normal((nq, d)).astype(np.float32)
+    g = rs.standard_normal((n, d)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    s, i = _prefilter_vs_exhaustive(cuda, q, g, k, idx_offset=123)
+    s_o, i_o = oracle.cosine_topk(q, g, k, idx_offset=123)
+    assert np.array_equal(i, i_o) and np.array_equal(s, s_o)
+
+
+def test_prefilter_bitexact_ties_and_clusters(cuda):
+    """Exact ties (duplicate rows on both sides of the seed boundary), planted
+    near-duplicates, and a dense cluster where thousands of rows score within
+    the bf16 bound of the k-th best (every one must be rescored)."""
+    rs = np.random.RandomState(5)
+    d = 256
+    g = rs.standard_normal((80_000, d)).astype(np.float32)
+    base = rs.standard_normal(d).astype(np.float32)
+    g[40_000:45_000] = base + 0.01 * rs.standard_normal((5000, d)).astype(np.float32)  # cluster
+    g[1000] = g[50_000] = g[79_999] = g[7]  # exact ties across the seed boundary
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    q = np.stack([g[7], base / np.linalg.norm(base), g[60_000] + 1e-4 * rs.standard_normal(d).astype(np.float32),
+                  rs.standard_normal(d).astype(np.float32)])
+    q = (q / np.linalg.norm(q, axis=1, keepdims=True)).astype(np.float32)
+    s, i = _prefilter_vs_exhaustive(cuda, q, g, 300)
+    assert list(i[0, :4]) == [7, 1000, 50_000, 79_999]
+    s_o, i_o = oracle.cosine_topk(q, g, 300)
+    assert np.array_equal(i, i_o) and np.array_equal(s, s_o)
+
+
+def test_prefilter_unnormalised_rows(cuda):
+    """The bound uses the gallery's row-norm maxima: rows of very different
+    norms (not unit) still rank exactly."""
+    rs = np.random.RandomState(9)
+    g = (rs.standard_normal((30_000, 64)) * rs.uniform(0.01, 3.0, size=(30_000, 1))).astype(np.float32)
+    q = (rs.standard_normal((11, 64)) * 2.5).astype(np.float32)
+    _prefilter_vs_exhaustive(cuda, q, g, 50)
