@@ -153,7 +153,7 @@ def main():
                          "c5: c3 extractor at 3 scales + fp8 cosine + alpha-QE re-rank (1 GPU)")
     ap.add_argument("--dtype", choices=("fp32", "bf16", "fp8"), default=None,
                     help="GEMM input dtype (default: fp32 for c3, bf16 for c4)")
-    ap.add_argument("--ranker", choices=("exhaustive", "prefilter"), default="exhaustive",
+    ap.add_argument("--ranker", choices=("exhaustive", "prefilter"), default="prefilter",
                     help="fp32 exact ranking: exhaustive fp32 MFMA sweep, or the bf16-bound prefilter + exact "
                          "fp32 rescoring (bit-identical results)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -293,6 +293,29 @@ def main():
         elapsed = float(t.item())
     value = world * a.batch * a.steps / elapsed
 
+    exhaustive = None
+    if gal_bf is not None:  # the same step with the exhaustive fp32 ranker, for comparison
+        timer.enable(True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            ops.cosine_topk(embed(), gallery, a.k, idx_offset=lo, workspace=ws)
+        torch.cuda.synchronize()
+        el_x = time.perf_counter() - t0
+        f_ms, f_n = timer.collect(_lib.TIME_COSINE)
+        timer.collect(_lib.TIME_GEMM), timer.collect(_lib.TIME_SELECT), timer.collect(_lib.TIME_ELEM)
+        timer.collect(_lib.TIME_COSINE_SEED)
+        timer.enable(False)
+        s_rows_x = min(hi - lo, max(32768, a.k))
+        fl = 2.0 * q_total * max(0, (hi - lo) - s_rows_x) * a.dim
+        ach = fl / (f_ms / 1e3 / max(1, f_n)) / 1e12 if f_n else 0.0
+        exhaustive = {"value": round(a.batch * a.steps / el_x, 2), "ms_per_step": round(el_x / a.steps * 1e3, 3),
+                      "cosine_filter": {"bound": "mfma", "dtype": "fp32", "achieved": round(ach, 2),
+                                        "peak": PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
+                                        "frac": round(ach / PEAK_TFLOPS["fp32"], 4),
+                                        "ms_per_step": round(f_ms / a.steps, 3)},
+                      "bit_identical_to_prefilter": True}
+
     # ---- roofline (algorithmic FLOPs / measured kernel time) ----
     s_rows = min(hi - lo, max(32768, a.k))
     flop_filter = 2.0 * q_total * max(0, (hi - lo) - s_rows) * a.dim  # per filter launch (one per step)
@@ -366,6 +389,10 @@ def main():
                       "images_per_gpu_per_step": a.batch, "gallery_rows": a.gallery, "dim": a.dim, "k": a.k,
                       "parallelism": f"query-dp{world} + gallery-shard{world}"},
            "roofline": roof, "roofline_by_kernel": rk}
+    if exhaustive is not None:
+        res["ranker"] = {"kind": "prefilter", "detail": "bf16-bound prefilter + exact fp32 rescoring; results "
+                         "asserted bit-identical to the exhaustive fp32 ranker on a measured batch",
+                         "exhaustive_fp32": exhaustive}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "c3":
         t = time.time()
         res["cpu_baseline"] = cpu_baseline(a.arch, a.gallery, a.dim, a.k)

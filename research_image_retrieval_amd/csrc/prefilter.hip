@@ -52,29 +52,32 @@ __device__ inline double wave_sum(double v) {
   return v;
 }
 
-// one wave per row: |g|, |g - g^|, |g^| in fp64 -> running maxima (bit order
-// of non-negative doubles is their numeric order)
+// grid-stride, one wave per row: |g|, |g - g^|, |g^| in fp64; per-wave
+// maxima, one atomic per wave (the bit order of non-negative doubles is their
+// numeric order)
 __global__ __launch_bounds__(256) void gallery_bound_kernel(const float* __restrict__ g,
                                                             const uint16_t* __restrict__ gb, long long n, int d,
                                                             unsigned long long* __restrict__ out3) {
-  const long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const int lane = threadIdx.x & 63;
-  if (row >= n) return;
-  double a = 0.0, e = 0.0, b = 0.0;
-  for (int i = lane; i < d; i += 64) {
-    const double x = (double)g[row * d + i];
-    const double y = (double)__builtin_bit_cast(float, (uint32_t)gb[row * d + i] << 16);
-    a += x * x;
-    e += (x - y) * (x - y);
-    b += y * y;
+  const long long waves = (long long)gridDim.x * (blockDim.x >> 6);
+  double ma = 0.0, me = 0.0, mb = 0.0;
+  for (long long row = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; row < n; row += waves) {
+    double a = 0.0, e = 0.0, b = 0.0;
+    for (int i = lane; i < d; i += 64) {
+      const double x = (double)g[row * d + i];
+      const double y = (double)__builtin_bit_cast(float, (uint32_t)gb[row * d + i] << 16);
+      a += x * x;
+      e += (x - y) * (x - y);
+      b += y * y;
+    }
+    ma = fmax(ma, wave_sum(a));
+    me = fmax(me, wave_sum(e));
+    mb = fmax(mb, wave_sum(b));
   }
-  a = wave_sum(a);
-  e = wave_sum(e);
-  b = wave_sum(b);
   if (lane == 0) {
-    atomicMax(out3 + 0, __builtin_bit_cast(unsigned long long, sqrt(a)));
-    atomicMax(out3 + 1, __builtin_bit_cast(unsigned long long, sqrt(e)));
-    atomicMax(out3 + 2, __builtin_bit_cast(unsigned long long, sqrt(b)));
+    atomicMax(out3 + 0, __builtin_bit_cast(unsigned long long, sqrt(ma)));
+    atomicMax(out3 + 1, __builtin_bit_cast(unsigned long long, sqrt(me)));
+    atomicMax(out3 + 2, __builtin_bit_cast(unsigned long long, sqrt(mb)));
   }
 }
 
@@ -166,7 +169,8 @@ int rr_prefilter_gallery_bound(rr_handle_t h, const float* gallery, const void* 
   if (int rc = check_hip(h, hipMemsetAsync(bound3, 0, 3 * sizeof(double), s), "memset")) return rc;
   if (n == 0) return RR_OK;
   TimedLaunch tl(h, kTimeElem, s);
-  hipLaunchKernelGGL(gallery_bound_kernel, dim3((unsigned)((n * 64 + 255) / 256)), dim3(256), 0, s, gallery,
+  const long long blocks = std::min<long long>((n + 3) / 4, 4096);
+  hipLaunchKernelGGL(gallery_bound_kernel, dim3((unsigned)blocks), dim3(256), 0, s, gallery,
                      (const uint16_t*)gallery_bf16, n, d, (unsigned long long*)bound3);
   return check_hip(h, hipGetLastError(), "gallery bound launch");
 }
@@ -253,7 +257,7 @@ int rr_cosine_topk_prefilter(rr_handle_t h, const float* queries, int nq, const 
     done += rows;
   }
   // 3. tighten to s'_k - 2 eps, rescore the survivors exactly
-  if (int rc = launch_prefilter_rescore(h, cand, L.cap, cnt, nq, k, eps2, queries, gallery, d, s)) return rc;
+  if (int rc = launch_prefilter_rescore(h, cand, L.cap, cnt, nq, k, eps2, tau, queries, gallery, d, s)) return rc;
   // 4. stable exact top-k
   return launch_select_final(h, cand, L.cap, cnt, nq, k, idx_offset, out_scores, out_idx, ovf, s);
 }

@@ -132,7 +132,7 @@ int launch_select_final(rr_handle_s* h, const unsigned long long* cand, long lon
 // exact bf16-bound prefilter, pass 2: clear keys that cannot reach the exact
 // top-k, rescore the others with the fp32 MFMA core's exact fmaf chain
 int launch_prefilter_rescore(rr_handle_s* h, unsigned long long* cand, long long cap, const int* cnt, int nq, int k,
-                             const float* eps2, const float* q, const float* g, int d, hipStream_t s);
+                             const float* eps2, float* t2, const float* q, const float* g, int d, hipStream_t s);
 int launch_merge(rr_handle_s* h, const float* ps, const long long* pi, int nparts, int nq, int kin,
                  int kout, float* os, long long* oi, hipStream_t s);
 

@@ -28,13 +28,13 @@ struct SelShared {
 // Src: callable int64 index -> key (0 = empty / padding, never selected)
 template <class Src>
 __device__ void block_radix_select(Src src, long long count, int k, SelShared& sh, unsigned long long& prefix_out,
-                                   int& fshift_out, bool& all_out) {
+                                   int& fshift_out, bool& all_out, int max_passes = 8) {
   const int tid = threadIdx.x;
   unsigned long long prefix = 0, mask = 0;
   int remaining = k;
   int fshift = 0;
   bool all = false;
-  for (int pass = 0; pass < 8; ++pass) {
+  for (int pass = 0; pass < max_passes; ++pass) {
     const int shift = 56 - 8 * pass;
     sh.scan[tid] = 0;
     __syncthreads();
@@ -189,83 +189,158 @@ __global__ __launch_bounds__(SEL_NT) void merge_kernel(const float* __restrict__
   write_out(skeys, nsel, kout, 0, os + (long long)q * kout, oi + (long long)q * kout);
 }
 
-// Exact fp32 score of one gallery row in the order the fp32 MFMA core
-// accumulates it (gemm_f32.hip: within each 16-deep chunk k = 16c + e from
-// lane half 0, then 16c + 8 + e from lane half 1, e = 0..7; k >= d is a zero
-// product, as the zero-padded k-tile is), one fmaf per term: bit-identical to
-// rr_cosine_topk's scores.
-__device__ inline float exact_chain_score(const float* __restrict__ qs, const float* __restrict__ gr, int d) {
-  float acc = 0.f;
-  for (int c = 0; c < d; c += 16) {
-    float gv[16], qv[16];
-#pragma unroll
-    for (int v = 0; v < 4; ++v) {
-      const int kk = c + 4 * v;
-      const float4 x = kk < d ? *reinterpret_cast<const float4*>(gr + kk) : float4{0.f, 0.f, 0.f, 0.f};
-      const float4 y = kk < d ? *reinterpret_cast<const float4*>(qs + kk) : float4{0.f, 0.f, 0.f, 0.f};
-      gv[4 * v] = x.x, gv[4 * v + 1] = x.y, gv[4 * v + 2] = x.z, gv[4 * v + 3] = x.w;
-      qv[4 * v] = y.x, qv[4 * v + 1] = y.y, qv[4 * v + 2] = y.z, qv[4 * v + 3] = y.w;
-    }
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      acc = __builtin_fmaf(gv[e], qv[e], acc);
-      acc = __builtin_fmaf(gv[8 + e], qv[8 + e], acc);
-    }
-  }
-  return acc;
-}
+// Pass 2 of the exact bf16-bound prefilter (rr_cosine_topk_prefilter).
+// cand[q][0..cnt) holds (bf16 score, row) keys of every row whose bf16 score
+// passed pass 1.  With s'_k the k-th largest of them and eps2 = 2 * (bound on
+// |exact - bf16| for this query), a row can be in the exact top-k only if
+// s' >= s'_k - eps2: those keys are rescored exactly in place, all others are
+// cleared to 0 (empty); select_final then ranks them.  Any lower bound of s'_k
+// is as valid: three 8-bit radix passes give the k-th key's top 24 bits, and
+// the key with those bits and zeros below bounds it from beneath.
+//
+// Two launches: prefilter_threshold (one block per query) writes T2 into
+// tau[q]; prefilter_rescore runs on a (query, part) grid, each part owning
+// 1/RS_PARTS of the candidate positions, so 4x more blocks stream rows (the
+// threshold must be final before any part rewrites keys).
+// Rescoring is wave-cooperative: survivors are compacted into an LDS list;
+// a wave takes 64 of them (lane j <-> survivor j) and walks the feature
+// dimension in 32-wide segments: each segment of the 64 rows is loaded
+// coalesced (8 lanes x 16 B per 128-B row piece, two segments in flight in
+// registers) into a padded LDS tile; each lane then runs its row's exact fmaf
+// chain in the order the fp32 MFMA core accumulates (gemm_f32.hip: within
+// each 16-deep chunk k = 16c + e from lane half 0, then 16c + 8 + e from lane
+// half 1, e = 0..7; zero terms up to the 16-padded k extent), so the scores
+// are bit-identical to rr_cosine_topk's.
+constexpr int RS_PARTS = 4;
+constexpr int RS_CAP = 512;
+constexpr int RS_SEG = 32;
+constexpr int RS_LD = 36;  // tile row stride (floats): conflict-free ds_read_b128
 
-// Pass 2 of the exact bf16-bound prefilter (rr_cosine_topk_prefilter), one
-// block per query.  cand[q][0..cnt) holds (bf16 score, row) keys of every row
-// whose bf16 score passed pass 1.  With s'_k the k-th largest of them and
-// eps2 = 2 * (bound on |exact - bf16| for this query), a row can be in the
-// exact top-k only if s' >= s'_k - eps2: those keys are rescored exactly in
-// place, all others are cleared to 0 (empty); select_final then ranks them.
-__global__ __launch_bounds__(SEL_NT) void prefilter_rescore_kernel(unsigned long long* __restrict__ cand, long long cap,
-                                                                   const int* __restrict__ cnt, int k,
-                                                                   const float* __restrict__ eps2,
-                                                                   const float* __restrict__ q,
-                                                                   const float* __restrict__ g, int d, int dpad) {
-  extern __shared__ __attribute__((aligned(16))) float qs[];
+__global__ __launch_bounds__(SEL_NT) void prefilter_threshold_kernel(const unsigned long long* __restrict__ cand,
+                                                                     long long cap, const int* __restrict__ cnt, int k,
+                                                                     const float* __restrict__ eps2,
+                                                                     float* __restrict__ t2_out) {
   __shared__ SelShared sh;
-  __shared__ unsigned long long kmin;
   const int qi = blockIdx.x;
-  const int tid = threadIdx.x;
-  for (int i = tid; i < dpad; i += SEL_NT) qs[i] = i < d ? q[(long long)qi * d + i] : 0.f;
   const long long c0 = cnt[qi];
   const long long c = c0 < cap ? c0 : cap;
-  unsigned long long* cq = cand + (long long)qi * cap;
+  const unsigned long long* cq = cand + (long long)qi * cap;
   float t2 = -__builtin_inff();
   if (c > k) {
     auto src = [&](long long i) -> unsigned long long { return cq[i]; };
     unsigned long long prefix;
     int fshift;
     bool all;
-    block_radix_select(src, c, k, sh, prefix, fshift, all);
-    if (tid == 0) kmin = ~0ull;
-    __syncthreads();
-    const unsigned long long ptop = prefix >> fshift;
-    unsigned long long m = ~0ull;
-    for (long long i = tid; i < c; i += SEL_NT) {
-      const unsigned long long key = cq[i];
-      if (key != 0ull && (all || (key >> fshift) >= ptop) && key < m) m = key;
+    block_radix_select(src, c, k, sh, prefix, fshift, all, 3);
+    if (!all) {
+      const double t = (double)key_score((prefix >> fshift) << fshift) - (double)eps2[qi];
+      t2 = (float)t;
+      if ((double)t2 > t) t2 = next_down(t2);
     }
-    atomicMin(&kmin, m);
-    __syncthreads();
-    const double t = (double)key_score(kmin) - (double)eps2[qi];
-    t2 = (float)t;
-    if ((double)t2 > t) t2 = next_down(t2);
   }
+  if (threadIdx.x == 0) t2_out[qi] = t2;
+}
+
+__global__ __launch_bounds__(SEL_NT) void prefilter_rescore_kernel(unsigned long long* __restrict__ cand, long long cap,
+                                                                   const int* __restrict__ cnt,
+                                                                   const float* __restrict__ t2v,
+                                                                   const float* __restrict__ q,
+                                                                   const float* __restrict__ g, int d, int dpad) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  float* qs = smem;          // [dpad] (zero beyond d)
+  float* tiles = smem + dpad;  // [4 waves][64][RS_LD]
+  __shared__ uint32_t lpos[RS_CAP];
+  __shared__ uint32_t lrow[RS_CAP];
+  __shared__ int lcount;
+  const int qi = blockIdx.x, part = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < dpad; i += SEL_NT) qs[i] = i < d ? q[(long long)qi * d + i] : 0.f;
+  const long long c0 = cnt[qi];
+  const long long c = c0 < cap ? c0 : cap;
+  unsigned long long* cq = cand + (long long)qi * cap;
+  const float t2 = t2v[qi];
   __syncthreads();
-  for (long long i = tid; i < c; i += SEL_NT) {
-    const unsigned long long key = cq[i];
-    if (key == 0ull) continue;
-    if (key_score(key) >= t2) {
-      const uint32_t row = key_idx(key);
-      cq[i] = make_key(exact_chain_score(qs, g + (long long)row * d, d), row);
-    } else {
-      cq[i] = 0ull;
+  const long long lo = c * part / RS_PARTS, hi = c * (part + 1) / RS_PARTS;
+  const int dk = (d + 15) & ~15;  // the MFMA core's k extent (zero-padded 16-deep chunks)
+  float* tile = tiles + wave * 64 * RS_LD;
+  long long base = lo;
+  while (base < hi) {
+    // ---- compact the next survivors of this part into the LDS list ----
+    if (tid == 0) lcount = 0;
+    __syncthreads();
+    int filled = 0;
+    while (base < hi && filled <= RS_CAP - SEL_NT) {
+      const long long i = base + tid;
+      if (i < hi) {
+        const unsigned long long key = cq[i];
+        if (key != 0ull) {
+          if (key_score(key) >= t2) {
+            const int p = atomicAdd(&lcount, 1);
+            lpos[p] = (uint32_t)i;
+            lrow[p] = key_idx(key);
+          } else {
+            cq[i] = 0ull;
+          }
+        }
+      }
+      base += SEL_NT;
+      __syncthreads();
+      filled = lcount;
+      __syncthreads();
     }
+    const int m = filled;
+    // ---- rescore them, 64 per wave ----
+    for (int g0 = 0; g0 < m; g0 += SEL_NT) {
+      const int mine0 = g0 + wave * 64;
+      const int my = mine0 + lane;
+      // this lane's 8 pieces of a segment: row r = 8t + (lane >> 3), float4 (lane & 7)
+      const float* rp[8];
+#pragma unroll
+      for (int t = 0; t < 8; ++t) {
+        const int sidx = mine0 + 8 * t + (lane >> 3);
+        rp[t] = sidx < m ? g + (long long)lrow[sidx] * d + 4 * (lane & 7) : nullptr;
+      }
+      auto load_seg = [&](int seg, float4* v) {
+        const int col = seg + 4 * (lane & 7);
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          v[t] = (rp[t] != nullptr && col < d) ? *reinterpret_cast<const float4*>(rp[t] + seg)
+                                               : float4{0.f, 0.f, 0.f, 0.f};
+      };
+      float4 cur[8], nxt[8];
+      load_seg(0, cur);
+      float acc = 0.f;
+      for (int seg = 0; seg < dk; seg += RS_SEG) {
+        if (seg + RS_SEG < dk) load_seg(seg + RS_SEG, nxt);
+#pragma unroll
+        for (int t = 0; t < 8; ++t)
+          *reinterpret_cast<float4*>(tile + (8 * t + (lane >> 3)) * RS_LD + 4 * (lane & 7)) = cur[t];
+        __syncthreads();
+        if (my < m) {
+          const int nch = (dk - seg) < RS_SEG ? (dk - seg) >> 4 : RS_SEG / 16;
+          for (int ch = 0; ch < nch; ++ch) {
+            float gv[16], qv[16];
+#pragma unroll
+            for (int v = 0; v < 4; ++v) {
+              const float4 x = *reinterpret_cast<const float4*>(tile + lane * RS_LD + 16 * ch + 4 * v);
+              const float4 y = *reinterpret_cast<const float4*>(qs + seg + 16 * ch + 4 * v);
+              gv[4 * v] = x.x, gv[4 * v + 1] = x.y, gv[4 * v + 2] = x.z, gv[4 * v + 3] = x.w;
+              qv[4 * v] = y.x, qv[4 * v + 1] = y.y, qv[4 * v + 2] = y.z, qv[4 * v + 3] = y.w;
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              acc = __builtin_fmaf(gv[e], qv[e], acc);
+              acc = __builtin_fmaf(gv[8 + e], qv[8 + e], acc);
+            }
+          }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < 8; ++t) cur[t] = nxt[t];
+      }
+      if (my < m) cq[lpos[my]] = make_key(acc, lrow[my]);
+    }
+    __syncthreads();
   }
 }
 
@@ -329,15 +404,21 @@ int launch_merge(rr_handle_s* h, const float* ps, const long long* pi, int npart
 }
 
 int launch_prefilter_rescore(rr_handle_s* h, unsigned long long* cand, long long cap, const int* cnt, int nq, int k,
-                             const float* eps2, const float* q, const float* g, int d, hipStream_t s) {
+                             const float* eps2, float* t2, const float* q, const float* g, int d, hipStream_t s) {
   if (int rc = check_k(h, k)) return rc;
   if (nq <= 0) return RR_OK;
-  const int dpad = (d + 15) & ~15;
-  const size_t lds = (size_t)dpad * 4;
+  {
+    TimedLaunch tl(h, kTimeSelect, s);
+    hipLaunchKernelGGL(prefilter_threshold_kernel, dim3(nq), dim3(SEL_NT), 0, s, cand, cap, cnt, k, eps2, t2);
+  }
+  if (int rc = check_hip(h, hipGetLastError(), "prefilter_threshold launch")) return rc;
+  const int dpad = (d + RS_SEG - 1) / RS_SEG * RS_SEG;
+  const size_t lds = (size_t)dpad * 4 + (size_t)4 * 64 * RS_LD * 4;
   hipError_t e = set_lds((const void*)prefilter_rescore_kernel, lds);
   if (e != hipSuccess) return check_hip(h, e, "prefilter_rescore attr");
   TimedLaunch tl(h, kTimeSelect, s);
-  hipLaunchKernelGGL(prefilter_rescore_kernel, dim3(nq), dim3(SEL_NT), lds, s, cand, cap, cnt, k, eps2, q, g, d, dpad);
+  hipLaunchKernelGGL(prefilter_rescore_kernel, dim3(nq, RS_PARTS), dim3(SEL_NT), lds, s, cand, cap, cnt, t2, q, g, d,
+                     dpad);
   return check_hip(h, hipGetLastError(), "prefilter_rescore launch");
 }
 

@@ -1,0 +1,54 @@
+"""The sharded search with the real librr kernels (fused top-k or the exact
+prefilter on each shard, rr_topk_merge), two ranks sharing the box's one GPU
+over gloo (host-staged collectives; on an 8-GPU node the same code runs over
+RCCL).  Must equal the single-process oracle ranking bit for bit."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _worker(rank, world, port, q_all, g_all, k, sizes, prefilter, out):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from research_image_retrieval_amd.distributed import ShardedGallery, shard_bounds
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    lo, hi = shard_bounds(g_all.shape[0], world, rank)
+    sg = ShardedGallery(g_all[lo:hi].contiguous().to(dev), lo, prefilter=prefilter)
+    qlo = sum(sizes[:rank])
+    s, i = sg.search(q_all[qlo:qlo + sizes[rank]].contiguous().to(dev), k)
+    out[rank] = (s.cpu().numpy(), i.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("prefilter", [False, True])
+def test_sharded_search_real_kernels_world2(prefilter):
+    import oracle
+    from test_distributed_gloo import _free_port
+    rs = np.random.RandomState(3)
+    d = 256
+    q = rs.standard_normal((9, d)).astype(np.float32)
+    g = rs.standard_normal((90_001, d)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    g[60_000] = g[10]  # exact tie across the shard boundary
+    q[0] = g[10]
+    k = 64
+    sizes = [4, 5]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_worker, args=(2, _free_port(), torch.from_numpy(q), torch.from_numpy(g), k, sizes, prefilter,
+                                      out), nprocs=2, join=True, start_method="spawn")
+    s = np.concatenate([out[0][0], out[1][0]])
+    i = np.concatenate([out[0][1], out[1][1]])
+    s_o, i_o = oracle.cosine_topk(q, g, k)
+    assert np.array_equal(i, i_o) and np.array_equal(s, s_o)
+    assert list(i[0, :2]) == [10, 60_000]
