@@ -25,6 +25,7 @@
 // Block ids are remapped so consecutive tiles of one XCD share the A panel
 // (the streamed gallery / activation rows) in that XCD's L2.
 #include <cstdlib>
+#include <cstring>
 
 #include "rr_internal.hpp"
 
@@ -52,27 +53,47 @@ __device__ __forceinline__ int swz(int row, int slot) {
   else return slot ^ ((row >> 2) & 3);
 }
 
+// Pin the scheduler to alternate MFMAs with the next k-step's LDS fragment
+// reads (NR reads, NM >= NR MFMAs in the region): MFMA, read, MFMA, read,
+// ..., then the remaining MFMAs, so the reads' latency runs under MFMAs.
+template <int NR, int NM>
+__device__ __forceinline__ void interleave() {
+#pragma unroll
+  for (int x = 0; x < NR; ++x) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
+  }
+  if constexpr (NM > NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+}
+
 // QuickGELU, x * sigmoid(1.702 x) (networks/model.py:166-168)
 __device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f + expf(-(1.702f * x)))); }
 
 // BK = 32: 64 KB LDS per 128x128 block, 2 blocks (2 waves/SIMD) per CU.
 // BK = 16: 32 KB, 3 blocks (3 waves/SIMD) per CU, twice the barriers.
-template <int WM, int WN, int AMODE, int EMODE, int BK, int DT>
-__global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(GemmArgs g, int tiles_n) {
+template <int WM, int WN, int FM, int FN, int AMODE, int EMODE, int BK, int DT, int MINB, int GL>
+__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, int tiles_n) {
   using ET = typename ElemT<DT>::T;
-  static_assert(DT == DT_F32 || (AMODE == A_DENSE && BK == 32), "low-precision GEMM: dense A, 128-B rows");
+  static_assert(DT == DT_F32 || (AMODE == A_DENSE && (BK == 32 || (BK == 16 && GL == 2))),
+                "low-precision GEMM: dense A, 128-B rows (64-B rows in the 4-stage pipeline)");
+  static_assert(!GL || AMODE == A_DENSE, "LDS-DMA staging: dense A/B");
   constexpr int ES = (int)sizeof(ET);
   constexpr int EPR = BK * 4 / ES;  // elements per LDS row (= k per k-tile)
   constexpr int CH = 16 / ES;       // elements per 16-byte staging chunk
   constexpr int NT = 64 * WM * WN;
-  constexpr int BM = 64 * WM, BN = 64 * WN;
+  constexpr int WTM = 32 * FM, WTN = 32 * FN;  // one wave's output block
+  constexpr int BM = WTM * WM, BN = WTN * WN;
   constexpr int SLOTS = BK / 4;
   constexpr int ROWS_PER_PASS = NT / SLOTS;
   constexpr int A_CH = BM / ROWS_PER_PASS;
   constexpr int B_CH = BN / ROWS_PER_PASS;
   static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for block");
+  static_assert(BM % ROWS_PER_PASS == 0 && BN % ROWS_PER_PASS == 0, "staging passes must tile the block");
   constexpr int BUF = (BM + BN) * BK;  // floats per LDS buffer
-  __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
+  // GL == 2: 4-stage LDS-DMA ring, three k-tiles in flight across raw
+  // barriers with counted vmcnt (never drained to 0 in the steady state)
+  constexpr int NSTAGE = GL == 2 ? 4 : 2;
+  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * BUF];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -206,6 +227,30 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
     }
   };
 
+  // LDS-DMA staging (GL): global_load_lds writes a wave's 64 x 16 B lane-
+  // linearly = 8 whole 128-B rows; the XOR swizzle moves to the SOURCE slot
+  // (it is an involution, so the fragment reads below stay as they are).
+  // Needs K % EPR == 0 (no partial k-tile to zero-fill).
+  auto glds_tile = [&](int kt, int buf) {
+    float* la = lds + buf * BUF;
+    float* lb = la + BM * BK;
+    const int wv = tid >> 6;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int row = crow + i * ROWS_PER_PASS;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(a_ptr[i] + (long long)kt * EPR + swz<BK>(row, slot) * CH),
+          (__attribute__((address_space(3))) void*)(la + (i * ROWS_PER_PASS + wv * (64 / SLOTS)) * BK), 16, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      const int row = crow + i * ROWS_PER_PASS;
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(b_ptr[i] + (long long)kt * EPR + swz<BK>(row, slot) * CH),
+          (__attribute__((address_space(3))) void*)(lb + (i * ROWS_PER_PASS + wv * (64 / SLOTS)) * BK), 16, 0, 0);
+    }
+  };
+
   auto store_tile = [&](int buf) {
     float* la = lds + buf * BUF;
     float* lb = la + BM * BK;
@@ -221,128 +266,173 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
     }
   };
 
-  f32x16 acc[2][2];
+  f32x16 acc[FM][FN];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int lr = lane & 31, lh = lane >> 5;
 
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
+  constexpr int LPT = A_CH + B_CH;  // LDS-DMA instructions per k-tile per wave
+  if constexpr (GL == 2) {
+#pragma unroll
+    for (int t = 0; t < NSTAGE - 1; ++t)
+      if (t < nk) glds_tile(t, t);
+  } else if constexpr (GL == 1) {
+    glds_tile(0, 0);
+    __syncthreads();
+  } else {
+    load_tile(0);
+    store_tile(0);
+    __syncthreads();
+  }
 
   for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile(kt + 1);
+    int cur;
+    if constexpr (GL == 2) {
+      cur = kt & (NSTAGE - 1);
+      // tile kt is retired once at most the younger tiles' DMAs are pending
+      const int younger = nk - 1 - kt;
+      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPT) : "memory");
+      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // all waves' DMAs for kt landed; all reads of kt-1 done
+      asm volatile("" ::: "memory");
+      if (kt + NSTAGE - 1 < nk) glds_tile(kt + NSTAGE - 1, (kt + NSTAGE - 1) & (NSTAGE - 1));
+    } else {
+      cur = kt & 1;
+      if (kt + 1 < nk) {
+        if constexpr (GL) glds_tile(kt + 1, cur ^ 1);
+        else load_tile(kt + 1);
+      }
+    }
     const float* la = lds + cur * BUF;
     const float* lb = la + BM * BK;
     if constexpr (DT == DT_F32) {
 #pragma unroll
     for (int c2 = 0; c2 < BK / 16; ++c2) {
-      f32x4 af[2][2], bf[2][2];
+      f32x4 af[FM][2], bf[FN][2];
       const int s0 = c2 * 4 + 2 * lh;
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int row = wm * 64 + i * 32 + lr;
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * WTM + i * 32 + lr;
         af[i][0] = *reinterpret_cast<const f32x4*>(la + row * BK + swz<BK>(row, s0) * 4);
         af[i][1] = *reinterpret_cast<const f32x4*>(la + row * BK + swz<BK>(row, s0 + 1) * 4);
       }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int row = wn * 64 + j * 32 + lr;
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * WTN + j * 32 + lr;
         bf[j][0] = *reinterpret_cast<const f32x4*>(lb + row * BK + swz<BK>(row, s0) * 4);
         bf[j][1] = *reinterpret_cast<const f32x4*>(lb + row * BK + swz<BK>(row, s0 + 1) * 4);
       }
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[i][e >> 2][e & 3], bf[j][e >> 2][e & 3],
                                                              acc[i][j], 0, 0, 0);
       }
     }
     } else if constexpr (DT == DT_BF16) {
-      // 4 k-steps of 16; lane half h holds k = 16s + 8h .. +7 = 16-B slot 2s + h
+      // BK/8 k-steps of 16; lane half h holds k = 16s + 8h .. +7 = 16-B slot 2s + h.
+      // Fragments are double-buffered in registers: step s+1's ds_reads are
+      // issued before step s's MFMAs, so LDS latency hides under the MFMAs.
+      constexpr int S = BK / 8;
+      bf16x8 af[2][FM], bf[2][FN];
+      auto rd = [&](int st, bf16x8* a, bf16x8* b) {
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        bf16x8 af[2], bf[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int row = wm * 64 + i * 32 + lr;
-          af[i] = *reinterpret_cast<const bf16x8*>(la + row * BK + swz<BK>(row, 2 * st + lh) * 4);
+        for (int i = 0; i < FM; ++i) {
+          const int row = wm * WTM + i * 32 + lr;
+          a[i] = *reinterpret_cast<const bf16x8*>(la + row * BK + swz<BK>(row, 2 * st + lh) * 4);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int row = wn * 64 + j * 32 + lr;
-          bf[j] = *reinterpret_cast<const bf16x8*>(lb + row * BK + swz<BK>(row, 2 * st + lh) * 4);
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn * WTN + j * 32 + lr;
+          b[j] = *reinterpret_cast<const bf16x8*>(lb + row * BK + swz<BK>(row, 2 * st + lh) * 4);
         }
+      };
+      rd(0, af[0], bf[0]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+      for (int st = 0; st < S; ++st) {
+        if (st + 1 < S) rd(st + 1, af[(st + 1) & 1], bf[(st + 1) & 1]);
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bf[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[st & 1][i], bf[st & 1][j], acc[i][j], 0, 0, 0);
+        if (st + 1 < S) interleave<FM + FN, FM * FN>();
       }
     } else {
-      // fp8: 8 k-steps of 16; lane half h holds bytes 8h..8h+7 of 16-B slot s
+      // fp8: BK/4 k-steps of 16; lane half h holds bytes 8h..8h+7 of 16-B slot s
+      constexpr int S = BK / 4;
+      long af[2][FM], bf[2][FN];
+      auto rd = [&](int st, long* a, long* b) {
 #pragma unroll
-      for (int st = 0; st < 8; ++st) {
-        long af[2], bf[2];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const int row = wm * 64 + i * 32 + lr;
-          af[i] = *reinterpret_cast<const long*>(la + row * BK + swz<BK>(row, st) * 4 + 2 * lh);
+        for (int i = 0; i < FM; ++i) {
+          const int row = wm * WTM + i * 32 + lr;
+          a[i] = *reinterpret_cast<const long*>(la + row * BK + swz<BK>(row, st) * 4 + 2 * lh);
         }
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          const int row = wn * 64 + j * 32 + lr;
-          bf[j] = *reinterpret_cast<const long*>(lb + row * BK + swz<BK>(row, st) * 4 + 2 * lh);
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn * WTN + j * 32 + lr;
+          b[j] = *reinterpret_cast<const long*>(lb + row * BK + swz<BK>(row, st) * 4 + 2 * lh);
         }
+      };
+      rd(0, af[0], bf[0]);
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+      for (int st = 0; st < S; ++st) {
+        if (st + 1 < S) rd(st + 1, af[(st + 1) & 1], bf[(st + 1) & 1]);
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(af[i], bf[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(af[st & 1][i], bf[st & 1][j], acc[i][j], 0, 0, 0);
+        if (st + 1 < S) interleave<FM + FN, FM * FN>();
       }
     }
-    if (kt + 1 < nk) store_tile(cur ^ 1);
-    __syncthreads();
+    if constexpr (GL != 2) {
+      if constexpr (!GL) {
+        if (kt + 1 < nk) store_tile(cur ^ 1);
+      }
+      __syncthreads();  // with GL: also the vmcnt(0) that retires the DMA
+    }
   }
+  if constexpr (GL == 2) __syncthreads();  // epilogues reuse the LDS
 
   // ---- epilogue ----
   // 32x32 C/D map: col (N index) = lane & 31, row (M index) = (r&3) + 8(r>>2) + 4(lane>>5)
   if (g.scale_a != nullptr || g.scale_b != nullptr) {  // per-row dequantisation (fp8)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int n = n0 + wn * 64 + j * 32 + lr;
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wn * WTN + j * 32 + lr;
       const float sb = (g.scale_b != nullptr && n < g.N) ? g.scale_b[n] : 1.f;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int m = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           const float sa = (g.scale_a != nullptr && m < g.M) ? g.scale_a[m] : 1.f;
           acc[i][j][r] = acc[i][j][r] * sa * sb;
         }
     }
   }
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n = n0 + wn * 64 + j * 32 + lr;
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wn * WTN + j * 32 + lr;
     const bool nok = n < g.N;
     if constexpr (EMODE == E_STORE) {
       // handled below through LDS
     } else if constexpr (EMODE == E_SCORES_T) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < FM; ++i) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-          const int mb = m0 + wm * 64 + i * 32 + 8 * q + 4 * lh;
+          const int mb = m0 + wm * WTM + i * 32 + 8 * q + 4 * lh;
           if (!nok) continue;
           float* dst = g.C + (long long)n * g.ldc + mb;
           if (mb + 3 < g.M) {
@@ -358,10 +448,10 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
     } else {  // E_FILTER: keep only scores strictly above the query's threshold
       const float t = nok ? g.tau[n] : __builtin_inff();
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < FM; ++i) {
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+          const int m = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           const float v = acc[i][j][r];
           if (v > t && m < g.M) {
             const int pos = atomicAdd(g.cnt + n, 1);
@@ -377,7 +467,7 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
     // barrier of the k-loop), then write whole rows: each lane moves 16 B,
     // 32 lanes cover a 512-B row run, residual read the same way.  When the
     // tile exceeds the LDS image (BK = 16) it goes in P row slabs.
-    constexpr int CAP = 2 * BUF;
+    constexpr int CAP = NSTAGE * BUF;
     constexpr int P = (BM * BN + CAP - 1) / CAP;
     static_assert(WM % P == 0, "row slabs must align with wave rows");
     constexpr int SLAB = BM / P;
@@ -391,13 +481,13 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
       if (p > 0) __syncthreads();
       if (wm / (WM / P) == p) {
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j)
+          for (int j = 0; j < FN; ++j)
 #pragma unroll
             for (int r = 0; r < 16; ++r) {
-              const int row = wm * 64 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh - p * SLAB;
-              const int col = wn * 64 + j * 32 + lr;
+              const int row = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh - p * SLAB;
+              const int col = wn * WTN + j * 32 + lr;
               ct[row * BN + col] = acc[i][j][r];
             }
       }
@@ -469,17 +559,17 @@ __global__ __launch_bounds__(64 * WM * WN, BK == 16 ? 3 : 2) void gemm_kernel(Ge
   }
 }
 
-template <int WM, int WN, int AM, int EM, int BK, int DT>
+template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0>
 static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
-  constexpr int BM = 64 * WM, BN = 64 * WN;
+  constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM;
   const long long tiles_n = (g.N + BN - 1) / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
   const unsigned splits = g.k_split > 0 ? (unsigned)((g.K + g.k_split - 1) / g.k_split) : 1u;
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, AM, EM, BK, DT>), dim3((unsigned)nblk, splits), dim3(64 * WM * WN), 0, s,
-                     g, (int)tiles_n);
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL>), dim3((unsigned)nblk, splits),
+                     dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
 
@@ -518,21 +608,65 @@ template <int AM, int EM>
 static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
   const int cfg = pick_cfg(g, EM);
   if (pick_bk(EM) == 16) {
-    if (cfg == 41) return launch_t<4, 1, AM, EM, 16, DT_F32>(g, s);
-    return launch_t<2, 2, AM, EM, 16, DT_F32>(g, s);
+    if (cfg == 41) return launch_t<4, 1, 2, 2, AM, EM, 16, DT_F32, 3>(g, s);
+    return launch_t<2, 2, 2, 2, AM, EM, 16, DT_F32, 3>(g, s);
   }
-  if (cfg == 41) return launch_t<4, 1, AM, EM, 32, DT_F32>(g, s);
-  return launch_t<2, 2, AM, EM, 32, DT_F32>(g, s);
+  if (cfg == 41) return launch_t<4, 1, 2, 2, AM, EM, 32, DT_F32, 2>(g, s);
+  return launch_t<2, 2, 2, 2, AM, EM, 32, DT_F32, 2>(g, s);
 }
 
-// low-precision (dense A only, 128-B LDS rows, 2 blocks per CU)
+// Low precision (dense A only, 128-B LDS rows).  Configs (waves WMxWN, MFMA
+// tiles per wave FMxFN, blocks per CU):
+//   22: 128x128, 4 waves of 64x64, 2/CU      41: 256x64, 4 waves of 64x64, 2/CU
+//   big: 256x256, 8 waves of 128x64, 1/CU (128 KB LDS) — the large GEMMs
+//   q320: 256x320, 8 waves of 64x160, 1/CU (144 KB) — a 320-query batch in
+//         one tile column: the streamed gallery is read exactly once
+// picked by estimated rounds x tile area (RR_GEMM_LPCFG=22|41|big|q320 forces).
+static int pick_lp(const GemmArgs& g, int emode) {
+  static const int forced = [] {
+    const char* e = getenv("RR_GEMM_LPCFG");
+    if (!e) return 0;
+    if (!strcmp(e, "22")) return 1;
+    if (!strcmp(e, "41")) return 2;
+    if (!strcmp(e, "big")) return 3;
+    if (!strcmp(e, "q320")) return 4;
+    if (!strcmp(e, "big4")) return 5;
+    return 0;
+  }();
+  if (forced == 4 && emode == E_STORE) return 3;
+  if (forced) return forced;
+  // rounds x tile area / relative per-FLOP speed (measured, tools/lp_bench.py:
+  // the 8-wave tiles run ViT linears 1.2-1.3x faster than 128x128; the
+  // 320-query tile runs the bf16 d=2048 sweep 1.35x faster, but not d=512 or
+  // fp8, where 4-wave tiles win)
+  auto cost = [&](long long bm, long long bn, long long slots, double speed) {
+    const long long t = ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn);
+    return (double)((t + slots - 1) / slots) * bm * bn / speed;
+  };
+  double best = cost(128, 128, 512, 1.0);
+  int cfg = 1;
+  if (cost(256, 64, 512, 1.0) < best) best = cost(256, 64, 512, 1.0), cfg = 2;
+  if (emode == E_STORE && cost(256, 256, 256, 1.25) < best) best = cost(256, 256, 256, 1.25), cfg = 3;
+  if (emode != E_STORE && g.K >= 1024 && g.scale_a == nullptr && cost(256, 320, 256, 1.35) < best)
+    best = cost(256, 320, 256, 1.35), cfg = 4;
+  return cfg;
+}
+
 template <int EM, int DT>
 static hipError_t launch_lp(const GemmArgs& g, hipStream_t s) {
-  const long long t22 = ((g.M + 127) / 128) * ((g.N + 127) / 128);
-  const long long t41 = ((g.M + 255) / 256) * ((g.N + 63) / 64);
-  const long long c22 = ((t22 + 511) / 512) * 128 * 128, c41 = ((t41 + 511) / 512) * 256 * 64;
-  if (c41 < c22) return launch_t<4, 1, A_DENSE, EM, 32, DT>(g, s);
-  return launch_t<2, 2, A_DENSE, EM, 32, DT>(g, s);
+  constexpr int EPR = DT == DT_BF16 ? 64 : 128;  // elements per 128-B k-tile row
+  int cfg = pick_lp(g, EM);
+  if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles
+  if (cfg == 5 && (g.K % (EPR / 2)) != 0) cfg = 1;
+  switch (cfg) {
+    case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2>(g, s);
+    case 3: return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1>(g, s);
+    case 4:
+      if constexpr (EM != E_STORE) return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1>(g, s);
+      return hipErrorInvalidValue;
+    case 5: return launch_t<2, 4, 4, 2, A_DENSE, EM, 16, DT, 1, 2>(g, s);
+    default: return launch_t<2, 2, 2, 2, A_DENSE, EM, 32, DT, 2>(g, s);
+  }
 }
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStream_t s, int timer_cls, int dt) {
