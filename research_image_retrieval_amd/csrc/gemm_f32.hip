@@ -639,9 +639,10 @@ static int pick_lp(const GemmArgs& g, int emode) {
   // the 8-wave tiles run ViT linears 1.2-1.3x faster than 128x128; the
   // 320-query tile runs the bf16 d=2048 sweep 1.35x faster, but not d=512 or
   // fp8, where 4-wave tiles win)
+  // (a round of `slots` resident blocks lasts ~ tile area x blocks per CU)
   auto cost = [&](long long bm, long long bn, long long slots, double speed) {
     const long long t = ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn);
-    return (double)((t + slots - 1) / slots) * bm * bn / speed;
+    return (double)((t + slots - 1) / slots) * bm * bn * (slots / 256) / speed;
   };
   double best = cost(128, 128, 512, 1.0);
   int cfg = 1;
