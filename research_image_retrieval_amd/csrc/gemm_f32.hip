@@ -24,6 +24,7 @@
 // k-tile; the next tile's global loads are in flight under the MFMAs.
 // Block ids are remapped so consecutive tiles of one XCD share the A panel
 // (the streamed gallery / activation rows) in that XCD's L2.
+#include <algorithm>
 #include <cstdlib>
 #include <cstring>
 
@@ -290,6 +291,29 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     __syncthreads();
   }
 
+  // E_STORE epilogue geometry (used below); with a single slab the residual
+  // tile is fetched during the last k-tile, so its HBM latency hides under
+  // the final MFMAs instead of stalling the epilogue
+  constexpr int CAP = NSTAGE * BUF;
+  constexpr int P = (BM * BN + CAP - 1) / CAP;
+  constexpr int SLAB = BM / P;
+  constexpr int C4 = BN / 4;
+  constexpr int ITERS = SLAB * C4 / NT;
+  // (measured slower on MI355X: 64 VGPRs held over the last k-tile cost more
+  // than the hidden latency saves; kept off)
+  constexpr bool RES_PRE = false;
+  const bool vec_ok = ((g.N & 3) == 0) && ((g.ldc & 3) == 0);
+  f32x4 res_pre[RES_PRE ? ITERS : 1];
+  auto load_residual = [&](f32x4* res, int rbase) {
+#pragma unroll
+    for (int it = 0; it < ITERS; ++it) {
+      const int idx = tid + it * NT;
+      const int row = idx / C4, c4 = idx - row * C4;
+      const int m = m0 + rbase + row, n = n0 + c4 * 4;
+      if (m < g.M && n < g.N) res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
+    }
+  };
+
   for (int kt = 0; kt < nk; ++kt) {
     int cur;
     if constexpr (GL == 2) {
@@ -308,6 +332,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
         if constexpr (GL) glds_tile(kt + 1, cur ^ 1);
         else load_tile(kt + 1);
       }
+    }
+    if constexpr (RES_PRE) {
+      if (kt == nk - 1 && g.residual != nullptr && vec_ok) load_residual(res_pre, 0);
     }
     const float* la = lds + cur * BUF;
     const float* lb = la + BM * BK;
@@ -467,15 +494,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     // barrier of the k-loop), then write whole rows: each lane moves 16 B,
     // 32 lanes cover a 512-B row run, residual read the same way.  When the
     // tile exceeds the LDS image (BK = 16) it goes in P row slabs.
-    constexpr int CAP = NSTAGE * BUF;
-    constexpr int P = (BM * BN + CAP - 1) / CAP;
     static_assert(WM % P == 0, "row slabs must align with wave rows");
-    constexpr int SLAB = BM / P;
-    constexpr int C4 = BN / 4;
-    constexpr int ITERS = SLAB * C4 / NT;
     static_assert(ITERS * NT == SLAB * C4, "epilogue tiling");
     float* ct = lds;  // [SLAB][BN] row-major
-    const bool vec_ok = ((g.N & 3) == 0) && ((g.ldc & 3) == 0);
 #pragma unroll
     for (int p = 0; p < P; ++p) {
       if (p > 0) __syncthreads();
@@ -496,16 +517,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
       if (vec_ok) {
         // all residual loads in flight before the first use (one HBM round
         // trip per slab instead of one per row group)
-        f32x4 res[ITERS];
-        if (g.residual != nullptr) {
-#pragma unroll
-          for (int it = 0; it < ITERS; ++it) {
-            const int idx = tid + it * NT;
-            const int row = idx / C4, c4 = idx - row * C4;
-            const int m = m0 + rbase + row, n = n0 + c4 * 4;
-            if (m < g.M && n < g.N)
-              res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
-          }
+        f32x4 res_l[RES_PRE ? 1 : ITERS];
+        f32x4* res = RES_PRE ? res_pre : res_l;
+        if constexpr (!RES_PRE) {
+          if (g.residual != nullptr) load_residual(res, rbase);
         }
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
@@ -590,17 +605,35 @@ static int pick_bk(int emode) {
 // 512): this charges both the padding of N (e.g. 320 queries on 128-wide
 // tiles) and the last partially-filled round (wave quantization).
 // RR_GEMM_CFG=22|41 forces a config (tuning experiments).
+static bool allow88() {
+  static const bool on = [] {
+    const char* e = getenv("RR_GEMM_NO88");
+    return !(e && atoi(e));
+  }();
+  return on;
+}
+
 static int pick_cfg(const GemmArgs& g, int emode) {
   static const int forced = [] {
     const char* e = getenv("RR_GEMM_CFG");
     return e ? atoi(e) : 0;
   }();
-  if (forced == 22 || forced == 41) return forced;
+  if (forced == 22 || forced == 41 || forced == 88) return forced;
   const long long slots = pick_bk(emode) == 16 ? 768 : 512;
   const long long t22 = ((g.M + 127) / 128) * ((g.N + 127) / 128);
   const long long t41 = ((g.M + 255) / 256) * ((g.N + 63) / 64);
   const long long c22 = ((t22 + slots - 1) / slots) * 128 * 128;
   const long long c41 = ((t41 + slots - 1) / slots) * 256 * 64;
+  // 88 (256x256, 1 block/CU) measured per R101 layer (tools/conv_cfg_cmp.sh):
+  // +3-7 % on long-K GEMMs without a residual (3x3 256@14, 1024->512/2048),
+  // -5..-30 % on residual epilogues and short K, -40 % when the grid leaves
+  // CUs idle.  So: no residual, K >= 1024, N a multiple of 256, ~a full round.
+  if (emode == E_STORE && g.k_split == 0 && g.residual == nullptr && g.K >= 1024 && (g.N % 256) == 0 &&
+      allow88()) {
+    const long long t88 = ((g.M + 255) / 256) * (g.N / 256);
+    const long long c88 = ((t88 + 255) / 256) * 256 * 256;  // 1 block/CU vs 2 for 22: compare per CU
+    if (t88 >= 240 && (double)c88 / 1.05 < (double)std::min(c22, c41) * 2.0) return 88;
+  }
   return c41 < c22 ? 41 : 22;
 }
 
@@ -612,6 +645,10 @@ static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
     return launch_t<2, 2, 2, 2, AM, EM, 16, DT_F32, 3>(g, s);
   }
   if (cfg == 41) return launch_t<4, 1, 2, 2, AM, EM, 32, DT_F32, 2>(g, s);
+  if constexpr (EM == E_STORE && (AM == A_DENSE || AM == A_CONV)) {
+    // 88: 256x256, 8 waves of 128x64, 1 block per CU (experimental)
+    if (cfg == 88) return launch_t<2, 4, 4, 2, AM, EM, 32, DT_F32, 1>(g, s);
+  }
   return launch_t<2, 2, 2, 2, AM, EM, 32, DT_F32, 2>(g, s);
 }
 
