@@ -197,6 +197,30 @@ int rr_resize_bilinear(rr_handle_t h, const float* x, int b, int hgt, int wid,
                        int c, int out_h, int out_w, float inv_scale_h,
                        float inv_scale_w, float* y, void* stream);
 
+/* fp32-accurate convolution on the bf16 matrix cores (gemm_s3.hip): the
+ * same operation, layouts and epilogue as rr_conv2d, with the weights given
+ * as three bf16 planes w3 [3][cout][kh][kw][cin] from rr_split3_bf16 and the
+ * activations split in-kernel (x = x0 + x1 + x2 exactly; six bf16 MFMA
+ * products per fp32 product, error vs float64 at or below the exact-fp32
+ * MFMA's).  Needs cin % 32 == 0.  Replaces the same reference ops as
+ * rr_conv2d (networks/backbone.py:103-109, models/gem_pooling.py:44,61).   */
+int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid,
+                 int cin, const void* w3, const float* bias, int cout, int kh,
+                 int kw, int stride, int pad, const float* residual, int relu,
+                 float* y, void* stream);
+
+/* y = x . w^T + bias (+ residual, act as rr_linear_ex) on the split-bf16
+ * core; w3 = three bf16 planes [3][n][k] (rr_split3_bf16); k % 32 == 0.    */
+int rr_linear_s3(rr_handle_t h, const float* x, int m, int k, const void* w3,
+                 const float* bias, int n, const float* residual, int act,
+                 float* y, void* stream);
+
+/* Exact 3-way bf16 split of fp32 x[n]: planes [3][n] (bf16 bit patterns),
+ * x = p0 + p1 + p2 exactly (p0 = x truncated to bf16, p1 = the same of the
+ * remainder, p2 = the rest).  Done once per weight tensor.                 */
+int rr_split3_bf16(rr_handle_t h, const float* x, long long n, void* planes,
+                   void* stream);
+
 /* Max pool (torchvision ResNet stem maxpool 3x3/2 pad 1), NHWC. */
 int rr_maxpool2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int c,
                  int k, int stride, int pad, float* y, void* stream);

@@ -46,6 +46,9 @@ SIGNATURES = {
     "rr_preprocess_u8_ex": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp]),
     "rr_nchw_to_nhwc_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "rr_conv2d": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
+    "rr_conv2d_s3": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
+    "rr_linear_s3": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp]),
+    "rr_split3_bf16": (_i, [_vp, _vp, _ll, _vp, _vp]),
     "rr_resize_bilinear": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _f, _f, _vp, _vp]),
     "rr_maxpool2d": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "rr_gem_pool": (_i, [_vp, _vp, _i, _i, _i, _f, _f, _vp, _vp]),

@@ -1,0 +1,116 @@
+// gemm_epilogue.hpp — the stored-C epilogue shared by the GEMM kernels
+// (gemm_f32.hip, gemm_s3.hip): bias, residual, ReLU / QuickGELU, fp32 or
+// bf16 output, written as whole rows through an LDS-staged tile.
+#pragma once
+
+#include "rr_internal.hpp"
+
+namespace rr {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+// QuickGELU, x * sigmoid(1.702 x) (networks/model.py:166-168)
+__device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f + expf(-(1.702f * x)))); }
+
+// Stage the BM x BN accumulator tile (32x32 MFMA C/D layout: col = lane & 31,
+// row = (r&3) + 8(r>>2) + 4(lane>>5)) through LDS, then write whole rows: each
+// lane moves 16 B, 32 lanes cover a 512-B row run, the residual is read the
+// same way with every load in flight before the first use (one HBM round trip
+// per slab).  When the tile exceeds the CAPF floats of LDS it goes in P row
+// slabs.  Called by every thread of the block after the k-loop's last
+// barrier (the LDS is free).
+template <int WM, int WN, int FM, int FN, int CAPF>
+__device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, const f32x16 (&acc)[FM][FN], float* lds,
+                                               int m0, int n0) {
+  constexpr int NT = 64 * WM * WN;
+  constexpr int WTM = 32 * FM, WTN = 32 * FN;
+  constexpr int BM = WTM * WM, BN = WTN * WN;
+  constexpr int P = (BM * BN + CAPF - 1) / CAPF;
+  constexpr int SLAB = BM / P;
+  constexpr int C4 = BN / 4;
+  constexpr int ITERS = SLAB * C4 / NT;
+  static_assert(WM % P == 0, "row slabs must align with wave rows");
+  static_assert(ITERS * NT == SLAB * C4, "epilogue tiling");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+  const bool vec_ok = ((g.N & 3) == 0) && ((g.ldc & 3) == 0);
+  float* ct = lds;  // [SLAB][BN] row-major
+#pragma unroll
+  for (int p = 0; p < P; ++p) {
+    if (p > 0) __syncthreads();
+    if (wm / (WM / P) == p) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int row = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh - p * SLAB;
+            const int col = wn * WTN + j * 32 + lr;
+            ct[row * BN + col] = acc[i][j][r];
+          }
+    }
+    __syncthreads();
+    const int rbase = p * SLAB;
+    if (vec_ok) {
+      f32x4 res[ITERS];
+      if (g.residual != nullptr) {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) {
+          const int idx = tid + it * NT;
+          const int row = idx / C4, c4 = idx - row * C4;
+          const int m = m0 + rbase + row, n = n0 + c4 * 4;
+          if (m < g.M && n < g.N) res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int idx = tid + it * NT;
+        const int row = idx / C4, c4 = idx - row * C4;
+        const int m = m0 + rbase + row, n = n0 + c4 * 4;
+        if (m >= g.M || n >= g.N) continue;
+        f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
+        if (g.bias != nullptr) v += *reinterpret_cast<const f32x4*>(g.bias + n);
+        if (g.residual != nullptr) v += res[it];
+        if (g.relu == 1) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+        } else if (g.relu == 2) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = quick_gelu(v[e]);
+        }
+        if (g.out_bf16) {
+          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+          const bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+          *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(Cb) + (long long)m * g.ldc + n) = o;
+        } else {
+          *reinterpret_cast<f32x4*>(Cb + (long long)m * g.ldc + n) = v;
+        }
+      }
+    } else {
+      for (int idx = tid; idx < SLAB * C4; idx += NT) {
+        const int row = idx / C4, c4 = idx - row * C4;
+        const int m = m0 + rbase + row, n = n0 + c4 * 4;
+        if (m >= g.M || n >= g.N) continue;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
+        const long long o = (long long)m * g.ldc + n;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (n + e >= g.N) break;
+          float x = v[e];
+          if (g.bias != nullptr) x += g.bias[n + e];
+          if (g.residual != nullptr) x += g.residual[o + e];
+          if (g.relu == 1) x = fmaxf(x, 0.f);
+          else if (g.relu == 2) x = quick_gelu(x);
+          if (g.out_bf16) reinterpret_cast<__bf16*>(Cb)[o + e] = (__bf16)x;
+          else Cb[o + e] = x;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace rr

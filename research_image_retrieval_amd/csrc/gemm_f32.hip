@@ -28,13 +28,10 @@
 #include <cstdlib>
 #include <cstring>
 
+#include "gemm_epilogue.hpp"
 #include "rr_internal.hpp"
 
 namespace rr {
-
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // input element type of A/B: DT_F32 (v_mfma_f32_32x32x2_f32), DT_BF16
 // (v_mfma_f32_32x32x16_bf16), DT_FP8 (OCP e4m3, v_mfma_f32_32x32x16_fp8_fp8).
@@ -66,9 +63,6 @@ __device__ __forceinline__ void interleave() {
   }
   if constexpr (NM > NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
 }
-
-// QuickGELU, x * sigmoid(1.702 x) (networks/model.py:166-168)
-__device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f + expf(-(1.702f * x)))); }
 
 // BK = 32: 64 KB LDS per 128x128 block, 2 blocks (2 waves/SIMD) per CU.
 // BK = 16: 32 KB, 3 blocks (3 waves/SIMD) per CU, twice the barriers.
@@ -291,29 +285,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     __syncthreads();
   }
 
-  // E_STORE epilogue geometry (used below); with a single slab the residual
-  // tile is fetched during the last k-tile, so its HBM latency hides under
-  // the final MFMAs instead of stalling the epilogue
-  constexpr int CAP = NSTAGE * BUF;
-  constexpr int P = (BM * BN + CAP - 1) / CAP;
-  constexpr int SLAB = BM / P;
-  constexpr int C4 = BN / 4;
-  constexpr int ITERS = SLAB * C4 / NT;
-  // (measured slower on MI355X: 64 VGPRs held over the last k-tile cost more
-  // than the hidden latency saves; kept off)
-  constexpr bool RES_PRE = false;
-  const bool vec_ok = ((g.N & 3) == 0) && ((g.ldc & 3) == 0);
-  f32x4 res_pre[RES_PRE ? ITERS : 1];
-  auto load_residual = [&](f32x4* res, int rbase) {
-#pragma unroll
-    for (int it = 0; it < ITERS; ++it) {
-      const int idx = tid + it * NT;
-      const int row = idx / C4, c4 = idx - row * C4;
-      const int m = m0 + rbase + row, n = n0 + c4 * 4;
-      if (m < g.M && n < g.N) res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
-    }
-  };
-
   for (int kt = 0; kt < nk; ++kt) {
     int cur;
     if constexpr (GL == 2) {
@@ -332,9 +303,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
         if constexpr (GL) glds_tile(kt + 1, cur ^ 1);
         else load_tile(kt + 1);
       }
-    }
-    if constexpr (RES_PRE) {
-      if (kt == nk - 1 && g.residual != nullptr && vec_ok) load_residual(res_pre, 0);
     }
     const float* la = lds + cur * BUF;
     const float* lb = la + BM * BK;
@@ -489,89 +457,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     }
   }
 
-  if constexpr (EMODE == E_STORE) {
-    // Stage the BMxBN accumulator tile through LDS (free after the last
-    // barrier of the k-loop), then write whole rows: each lane moves 16 B,
-    // 32 lanes cover a 512-B row run, residual read the same way.  When the
-    // tile exceeds the LDS image (BK = 16) it goes in P row slabs.
-    static_assert(WM % P == 0, "row slabs must align with wave rows");
-    static_assert(ITERS * NT == SLAB * C4, "epilogue tiling");
-    float* ct = lds;  // [SLAB][BN] row-major
-#pragma unroll
-    for (int p = 0; p < P; ++p) {
-      if (p > 0) __syncthreads();
-      if (wm / (WM / P) == p) {
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int j = 0; j < FN; ++j)
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-              const int row = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh - p * SLAB;
-              const int col = wn * WTN + j * 32 + lr;
-              ct[row * BN + col] = acc[i][j][r];
-            }
-      }
-      __syncthreads();
-      const int rbase = p * SLAB;
-      if (vec_ok) {
-        // all residual loads in flight before the first use (one HBM round
-        // trip per slab instead of one per row group)
-        f32x4 res_l[RES_PRE ? 1 : ITERS];
-        f32x4* res = RES_PRE ? res_pre : res_l;
-        if constexpr (!RES_PRE) {
-          if (g.residual != nullptr) load_residual(res, rbase);
-        }
-#pragma unroll
-        for (int it = 0; it < ITERS; ++it) {
-          const int idx = tid + it * NT;
-          const int row = idx / C4, c4 = idx - row * C4;
-          const int m = m0 + rbase + row, n = n0 + c4 * 4;
-          if (m >= g.M || n >= g.N) continue;
-          f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
-          if (g.bias != nullptr) v += *reinterpret_cast<const f32x4*>(g.bias + n);
-          if (g.residual != nullptr) v += res[it];
-          if (g.relu == 1) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-          } else if (g.relu == 2) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = quick_gelu(v[e]);
-          }
-          if (g.out_bf16) {
-            typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-            const bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-            *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(Cb) + (long long)m * g.ldc + n) = o;
-          } else {
-            *reinterpret_cast<f32x4*>(Cb + (long long)m * g.ldc + n) = v;
-          }
-        }
-      } else {
-        for (int idx = tid; idx < SLAB * C4; idx += NT) {
-          const int row = idx / C4, c4 = idx - row * C4;
-          const int m = m0 + rbase + row, n = n0 + c4 * 4;
-          if (m >= g.M || n >= g.N) continue;
-          const f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
-          const long long o = (long long)m * g.ldc + n;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            if (n + e >= g.N) break;
-            float x = v[e];
-            if (g.bias != nullptr) x += g.bias[n + e];
-            if (g.residual != nullptr) x += g.residual[o + e];
-            if (g.relu == 1) x = fmaxf(x, 0.f);
-            else if (g.relu == 2) x = quick_gelu(x);
-            if (g.out_bf16) {
-              const __bf16 xb = (__bf16)x;
-              reinterpret_cast<__bf16*>(Cb)[o + e] = xb;
-            } else {
-              Cb[o + e] = x;
-            }
-          }
-        }
-      }
-    }
-  }
+  if constexpr (EMODE == E_STORE) epilogue_store<WM, WN, FM, FN, NSTAGE * BUF>(g, Cb, acc, lds, m0, n0);
 }
 
 template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0>

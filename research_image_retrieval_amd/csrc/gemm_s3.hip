@@ -1,0 +1,349 @@
+// gemm_s3.hip — fp32-accurate GEMM on the bf16 matrix cores (3-way split).
+//
+// gfx950 has no xf32/TF32 MFMA, and its f32-input MFMA runs at 1/16 of the
+// bf16 rate (MI355X_MICROARCH.md: 157 vs 2500 TF/s dense).  Every fp32 value
+// is split EXACTLY into three bf16 pieces, x = x0 + x1 + x2:
+//   x0 = x with the low 16 bits cleared, x1 = the same of x - x0,
+//   x2 = x - x0 - x1 (at most 8 significant bits left, so exact in bf16);
+// |x1| < 2^-7 |x|, |x2| < 2^-15 |x|.  The product a.b keeps the six terms of
+// order >= 2^-15 — a0b0 + (a0b1 + a1b0) + (a0b2 + a1b1 + a2b0) — each a bf16
+// MFMA (exact products, fp32 accumulation); the dropped terms are < 2^-22
+// |a||b|, below fp32's own rounding of a long dot product.  a0b0 accumulates
+// in one register tile and the five small terms in a second one, so the small
+// terms never round against the large running sum; the two are added once in
+// the epilogue.  Measured against float64 (tests/test_gpu_s3.py), the error
+// is at or below the exact-fp32 MFMA fmaf chain's.  Six bf16 MFMAs cost 6/16
+// of one f32 MFMA: the fp32 convolutions of the ResNet trunk
+// (networks/backbone.py:60-109) run on this core.
+//
+// Operands: A = fp32 activations (dense rows or the implicit im2col of an
+// NHWC map with Cin % 32 == 0), split in registers while staging into LDS;
+// B = weights pre-split once on the host side into three bf16 planes
+// [3][N][K] (rr_split3_bf16), copied global -> LDS by LDS-DMA
+// (global_load_lds).  LDS per stage: 3 planes of A and 3 of B, BK bf16 per
+// plane row, 16-B slots XOR-swizzled so both the staging writes and the
+// fragment ds_read_b128 (v_mfma_f32_32x32x16_bf16 operands) are conflict-free.
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "gemm_epilogue.hpp"
+#include "rr_internal.hpp"
+
+namespace rr {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// exact 3-way split of x into bf16 pieces, returned as fp32 bit patterns
+// whose low 16 bits are zero
+__device__ __forceinline__ void split3(float x, uint32_t& h, uint32_t& m, uint32_t& l) {
+  const uint32_t hb = __float_as_uint(x) & 0xffff0000u;
+  const float r1 = x - __uint_as_float(hb);
+  const uint32_t mb = __float_as_uint(r1) & 0xffff0000u;
+  const float r2 = r1 - __uint_as_float(mb);
+  h = hb;
+  m = mb;
+  l = __float_as_uint(r2);
+}
+
+// two bf16 (the high halves of e0, e1) in one dword, e0 in the low half
+__device__ __forceinline__ uint32_t pack2(uint32_t e0, uint32_t e1) { return __builtin_amdgcn_perm(e1, e0, 0x07060302u); }
+
+// 16-B slot swizzle of a plane row of BK bf16: BK = 32 (64-B rows, 4 slots):
+// slot ^ ((row >> 2) & 3); BK = 16 (32-B rows, 2 slots): slot ^ ((row >> 3) & 1).
+// Every ds_read_b128 lane group (16 rows, one slot) and every ds_write_b128
+// group (8 lanes, contiguous) then hits distinct banks.
+template <int BK>
+__device__ __forceinline__ int pswz(int row, int slot) {
+  if constexpr (BK == 32) return slot ^ ((row >> 2) & 3);
+  else return slot ^ ((row >> 3) & 1);
+}
+
+template <int WM, int WN, int FM, int FN, int BK, int AMODE, int SEP, int MINB>
+__global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
+  constexpr int NT = 64 * WM * WN, NW = WM * WN;
+  constexpr int WTM = 32 * FM, WTN = 32 * FN;
+  constexpr int BM = WTM * WM, BN = WTN * WN;
+  constexpr int SL = BK / 8;                 // 16-B slots per plane row
+  constexpr int A_EL = 3 * BM * BK;          // bf16 per stage: A planes
+  constexpr int BUF = A_EL + 3 * BN * BK;    // bf16 per stage: A + B planes
+  constexpr int A_RPP = NT / SL;             // A rows staged per pass
+  constexpr int A_CH = BM / A_RPP;           // A chunks (8 k each) per thread
+  constexpr int B_RPI = 64 / SL;             // plane rows per LDS-DMA wave instruction
+  constexpr int B_TI = 3 * BN / B_RPI;       // LDS-DMA wave instructions per k-tile
+  constexpr int B_INS = (B_TI + NW - 1) / NW; // ... per wave (the last round may be partial)
+  static_assert(BM % A_RPP == 0 && (3 * BN) % B_RPI == 0, "staging must tile the block");
+  static_assert(BK == 16 || BK == 32, "BK");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  // XCD-aware bijective block remap (blocks b, b+8, ... share an XCD)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tn = wgid % tiles_n, tm = wgid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int nk = g.K / BK;  // K % BK == 0 (checked on the host)
+
+  // ---- A: per-chunk row state (fp32, register-staged, split on store) ----
+  const int a_slot = tid % SL, a_row = tid / SL;
+  const float* a_ptr[A_CH];
+  int a_ih0[A_CH], a_iw0[A_CH];
+  bool a_ok[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    const int m = m0 + a_row + i * A_RPP;
+    a_ok[i] = m < g.M;
+    const int mm = a_ok[i] ? m : 0;
+    if constexpr (AMODE == A_DENSE) {
+      a_ptr[i] = g.A + (long long)mm * g.lda + a_slot * 8;
+      a_ih0[i] = a_iw0[i] = 0;
+    } else {
+      const int ohw = g.OH * g.OW;
+      const int b = mm / ohw, rem = mm - b * ohw;
+      const int oh = rem / g.OW, ow = rem - oh * g.OW;
+      a_ptr[i] = g.A + (long long)b * g.H * g.W * g.Cin + a_slot * 8;
+      a_ih0[i] = oh * g.stride - g.pad;
+      a_iw0[i] = ow * g.stride - g.pad;
+    }
+  }
+  f32x4 ra[A_CH][2];
+  auto load_a = [&](int kt) {
+    const int k0 = kt * BK;
+    if constexpr (AMODE == A_DENSE) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const f32x4* p = reinterpret_cast<const f32x4*>(a_ptr[i] + k0);
+        ra[i][0] = a_ok[i] ? p[0] : f32x4{0.f, 0.f, 0.f, 0.f};
+        ra[i][1] = a_ok[i] ? p[1] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+      // Cin % 32 == 0: the whole k-tile lies in one (kh, kw) filter tap
+      const int khw = k0 / g.Cin, cin0 = k0 - khw * g.Cin;
+      const int kh = khw / g.KW, kw = khw - kh * g.KW;
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+        const bool ok = a_ok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+        const f32x4* p = reinterpret_cast<const f32x4*>(a_ptr[i] + ((long long)ih * g.W + iw) * g.Cin + cin0);
+        ra[i][0] = ok ? p[0] : f32x4{0.f, 0.f, 0.f, 0.f};
+        ra[i][1] = ok ? p[1] : f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+  };
+  auto store_a = [&](int buf) {
+    uint16_t* la = lds + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      uint32_t h[8], m[8], l[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) split3(ra[i][e >> 2][e & 3], h[e], m[e], l[e]);
+      const int row = a_row + i * A_RPP;
+      const int off = row * BK + pswz<BK>(row, a_slot) * 8;
+      *reinterpret_cast<u32x4*>(la + off) = u32x4{pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
+      *reinterpret_cast<u32x4*>(la + BM * BK + off) =
+          u32x4{pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7])};
+      *reinterpret_cast<u32x4*>(la + 2 * BM * BK + off) =
+          u32x4{pack2(l[0], l[1]), pack2(l[2], l[3]), pack2(l[4], l[5]), pack2(l[6], l[7])};
+    }
+  };
+
+  // ---- B: three bf16 planes, LDS-DMA (64 lanes x 16 B = B_RPI whole plane
+  // rows per instruction; the swizzle moves to the source slot) ----
+  const uint16_t* b_src[B_INS];
+  const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
+#pragma unroll
+  for (int i = 0; i < B_INS; ++i) {
+    const int prow = min(i * NW + wave, B_TI - 1) * B_RPI + lane / SL;
+    const int p = prow / BN, r = prow - p * BN;
+    const int n = min(n0 + r, g.N - 1);  // rows past N feed only unstored columns
+    b_src[i] = Bp + p * g.b_plane + (long long)n * g.ldb + pswz<BK>(r, lane % SL) * 8;
+  }
+  auto glds_b = [&](int kt, int buf) {
+    uint16_t* lb = lds + buf * BUF + A_EL;
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i)
+      if (B_TI % NW == 0 || i * NW + wave < B_TI)
+        __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + (long long)kt * BK),
+                                       (__attribute__((address_space(3))) void*)(lb + (i * NW + wave) * B_RPI * BK),
+                                       16, 0, 0);
+  };
+
+  f32x16 hi[FM][FN];
+  f32x16 lo[SEP ? FM : 1][SEP ? FN : 1];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        hi[i][j][r] = 0.f;
+        if constexpr (SEP) lo[i][j][r] = 0.f;
+      }
+
+  load_a(0);
+  glds_b(0, 0);
+  store_a(0);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      load_a(kt + 1);
+      glds_b(kt + 1, cur ^ 1);
+    }
+    const uint16_t* la = lds + cur * BUF;
+    const uint16_t* lb = la + A_EL;
+#pragma unroll
+    for (int st = 0; st < BK / 16; ++st) {
+      bf16x8 a[3][FM], b[3][FN];
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int row = wm * WTM + i * 32 + lr;
+          a[p][i] = *reinterpret_cast<const bf16x8*>(la + (p * BM + row) * BK + pswz<BK>(row, 2 * st + lh) * 8);
+        }
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn * WTN + j * 32 + lr;
+          b[p][j] = *reinterpret_cast<const bf16x8*>(lb + (p * BN + row) * BK + pswz<BK>(row, 2 * st + lh) * 8);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) hi[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], hi[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          f32x16& L = SEP ? lo[SEP ? i : 0][SEP ? j : 0] : hi[i][j];
+          L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], L, 0, 0, 0);
+          L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], L, 0, 0, 0);
+          L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], L, 0, 0, 0);
+          L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], L, 0, 0, 0);
+          L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], L, 0, 0, 0);
+        }
+    }
+    if (kt + 1 < nk) store_a(cur ^ 1);
+    __syncthreads();  // also retires the LDS-DMA of tile kt + 1
+  }
+
+  if constexpr (SEP) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) hi[i][j] += lo[i][j];
+  }
+  epilogue_store<WM, WN, FM, FN, BUF>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
+}
+
+template <int WM, int WN, int FM, int FN, int BK, int AM, int SEP, int MINB>
+static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
+  constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
+  const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
+  const long long nblk = tiles_m * tiles_n;
+  if (nblk <= 0) return hipSuccess;
+  if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, SEP, MINB>), dim3((unsigned)nblk), dim3(64 * WM * WN), 0,
+                     s, g, (int)tiles_n);
+  return hipGetLastError();
+}
+
+// Tile configs (waves WMxWN, MFMA tiles per wave FMxFN, BK, blocks per CU):
+//   1: 128x128, 4 waves of 64x64, BK 16, 2/CU (48 KB LDS)
+//   2: 128x128, 4 waves of 64x64, BK 32, 1/CU (96 KB)
+//   3: 256x128, 8 waves of 64x64, BK 32, 1/CU (144 KB)
+//   4: 128x256, 8 waves of 64x64, BK 32, 1/CU (144 KB)
+//   5: 256x64,  4 waves of 64x64, BK 32, 1/CU (120 KB)
+//   6: 256x64,  4 waves of 64x64, BK 16, 2/CU (60 KB)
+// Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the
+// fastest wherever N >= 128 (1.1-1.3x config 1 per FLOP).
+// RR_S3_CFG=1..6 forces one; RR_S3_SEP=0 accumulates all six terms in one
+// register tile (accuracy experiment: measured LESS accurate than exact fp32,
+// so the default keeps the small terms apart).
+static int s3_forced_cfg() {
+  static const int v = [] {
+    const char* e = getenv("RR_S3_CFG");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+static bool s3_sep() {
+  static const bool v = [] {
+    const char* e = getenv("RR_S3_SEP");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+
+static int pick_s3(const GemmArgs& g) {
+  const int f = s3_forced_cfg();
+  if (f >= 1 && f <= 6) return f;
+  // rounds of resident blocks x tile area per CU / relative per-FLOP speed
+  auto cost = [&](long long bm, long long bn, long long per_cu, double speed) {
+    const long long slots = 256 * per_cu;
+    const long long t = ((g.M + bm - 1) / bm) * ((g.N + bn - 1) / bn);
+    return (double)((t + slots - 1) / slots) * bm * bn * per_cu / speed;
+  };
+  double best = cost(128, 128, 2, 1.0);
+  int cfg = 1;
+  if (cost(256, 128, 1, 1.15) < best) best = cost(256, 128, 1, 1.15), cfg = 3;
+  if (cost(256, 64, 2, 1.0) < best) best = cost(256, 64, 2, 1.0), cfg = 6;
+  return cfg;
+}
+
+template <int AM>
+static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s) {
+  if (!s3_sep()) return launch_s3_t<2, 2, 2, 2, 16, AM, 0, 2>(g, s);
+  switch (pick_s3(g)) {
+    case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1, 1>(g, s);
+    case 3: return launch_s3_t<4, 2, 2, 2, 32, AM, 1, 1>(g, s);
+    case 4: return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1>(g, s);
+    case 5: return launch_s3_t<4, 1, 2, 2, 32, AM, 1, 1>(g, s);
+    case 6: return launch_s3_t<4, 1, 2, 2, 16, AM, 1, 2>(g, s);
+    default: return launch_s3_t<2, 2, 2, 2, 16, AM, 1, 2>(g, s);
+  }
+}
+
+int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls) {
+  if (g.M < 0 || g.N <= 0 || g.K <= 0) return set_error(h, RR_EINVAL, "gemm_s3: bad shape");
+  if (g.K % 32) return set_error(h, RR_EINVAL, "gemm_s3: K must be a multiple of 32");
+  if (amode == A_DENSE && ((g.lda & 3) || ((uintptr_t)g.A & 15)))
+    return set_error(h, RR_EINVAL, "gemm_s3: dense A needs lda % 4 == 0 and 16-B alignment");
+  if (amode == A_CONV && (g.Cin % 32)) return set_error(h, RR_EINVAL, "gemm_s3: conv A needs Cin % 32 == 0");
+  if (amode != A_DENSE && amode != A_CONV) return set_error(h, RR_EINVAL, "gemm_s3: unsupported A mode");
+  if ((g.ldb & 7) || (g.b_plane & 7) || ((uintptr_t)g.B & 15))
+    return set_error(h, RR_EINVAL, "gemm_s3: B planes need ldb % 8 == 0, plane stride % 8 == 0, 16-B alignment");
+  if (g.M == 0) return RR_OK;
+  hipError_t e;
+  {
+    TimedLaunch tl(h, timer_cls, s);
+    e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s) : launch_s3_am<A_CONV>(g, s);
+  }
+  return check_hip(h, e, "gemm_s3 launch");
+}
+
+// ---- weight split: x[n] -> planes [3][n] of bf16 (x0, x1, x2) ----
+__global__ void split3_kernel(const float* __restrict__ x, long long n, uint16_t* __restrict__ planes) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    uint32_t h, m, l;
+    split3(x[i], h, m, l);
+    planes[i] = (uint16_t)(h >> 16);
+    planes[n + i] = (uint16_t)(m >> 16);
+    planes[2 * n + i] = (uint16_t)(l >> 16);
+  }
+}
+
+int launch_split3(rr_handle_s* h, const float* x, long long n, uint16_t* planes, hipStream_t s) {
+  if (n <= 0) return RR_OK;
+  const long long blocks = std::min<long long>((n + 255) / 256, 4096);
+  hipLaunchKernelGGL(split3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, n, planes);
+  return check_hip(h, hipGetLastError(), "split3 launch");
+}
+
+}  // namespace rr

@@ -330,6 +330,75 @@ int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, c
   return launch_gemm(h, amode, E_STORE, g, (hipStream_t)stream, kTimeGemm);
 }
 
+int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, const void* w3,
+                 const float* bias, int cout, int kh, int kw, int stride, int pad, const float* residual, int relu,
+                 float* y, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !w3 || !y || b < 0 || hgt <= 0 || wid <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 ||
+      stride <= 0 || pad < 0 || relu < 0 || relu > 1)
+    return set_error(h, RR_EINVAL, "rr_conv2d_s3: bad argument");
+  if (cin % 32) return set_error(h, RR_EINVAL, "rr_conv2d_s3: cin must be a multiple of 32");
+  const int oh = (hgt + 2 * pad - kh) / stride + 1, ow = (wid + 2 * pad - kw) / stride + 1;
+  if (oh <= 0 || ow <= 0) return set_error(h, RR_EINVAL, "rr_conv2d_s3: empty output");
+  const long long M = (long long)b * oh * ow;
+  if (M > 0x7fffffffLL) return set_error(h, RR_EINVAL, "rr_conv2d_s3: too many output pixels");
+  if (((uintptr_t)x & 15) || ((uintptr_t)w3 & 15)) return set_error(h, RR_EINVAL, "rr_conv2d_s3: x/w3 must be 16-byte aligned");
+  GemmArgs g;
+  g.A = x;
+  g.M = (int)M;
+  g.K = kh * kw * cin;
+  g.H = hgt;
+  g.W = wid;
+  g.Cin = cin;
+  g.OH = oh;
+  g.OW = ow;
+  g.KH = kh;
+  g.KW = kw;
+  g.stride = stride;
+  g.pad = pad;
+  g.B = reinterpret_cast<const float*>(w3);
+  g.ldb = g.K;
+  g.b_plane = (long long)cout * g.K;
+  g.N = cout;
+  g.C = y;
+  g.ldc = cout;
+  g.bias = bias;
+  g.residual = residual;
+  g.relu = relu;
+  const bool dense = kh == 1 && kw == 1 && stride == 1 && pad == 0;
+  if (dense) g.lda = cin;
+  return launch_gemm_s3(h, dense ? A_DENSE : A_CONV, g, (hipStream_t)stream, kTimeGemm);
+}
+
+int rr_linear_s3(rr_handle_t h, const float* x, int m, int k, const void* w3, const float* bias, int n,
+                 const float* residual, int act, float* y, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !w3 || !y || m < 0 || k <= 0 || n <= 0 || act < 0 || act > 2) return set_error(h, RR_EINVAL, "rr_linear_s3: bad argument");
+  if (k % 32) return set_error(h, RR_EINVAL, "rr_linear_s3: k must be a multiple of 32");
+  GemmArgs g;
+  g.A = x;
+  g.lda = k;
+  g.M = m;
+  g.K = k;
+  g.B = reinterpret_cast<const float*>(w3);
+  g.ldb = k;
+  g.b_plane = (long long)n * k;
+  g.N = n;
+  g.C = y;
+  g.ldc = n;
+  g.bias = bias;
+  g.residual = residual;
+  g.relu = act;
+  return launch_gemm_s3(h, A_DENSE, g, (hipStream_t)stream, kTimeGemm);
+}
+
+int rr_split3_bf16(rr_handle_t h, const float* x, long long n, void* planes, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!x || !planes || n < 0) return set_error(h, RR_EINVAL, "rr_split3_bf16: bad argument");
+  TimedLaunch tl(h, kTimeElem, (hipStream_t)stream);
+  return launch_split3(h, x, n, reinterpret_cast<uint16_t*>(planes), (hipStream_t)stream);
+}
+
 int rr_linear(rr_handle_t h, const float* x, int m, int k, const float* w, const float* bias, int n, float* y,
               void* stream) {
   return rr_linear_ex(h, x, m, k, w, bias, n, nullptr, 0, y, stream);

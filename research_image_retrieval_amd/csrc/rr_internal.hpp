@@ -114,10 +114,17 @@ struct GemmArgs {
   int k_split = 0;
   long long c_split_stride = 0;
   int sym = 0;  // E_STORE of a symmetric product: skip tiles strictly below the diagonal
+  // split-bf16 GEMM (gemm_s3.hip): B = three bf16 planes, b_plane elements apart
+  long long b_plane = 0;
 };
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,
                 int dt = DT_F32);
+
+// fp32-accurate GEMM on bf16 MFMA (gemm_s3.hip): A fp32 (A_DENSE or A_CONV),
+// B = bf16 planes [3][N][ldb] from launch_split3, E_STORE epilogue
+int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls);
+int launch_split3(rr_handle_s* h, const float* x, long long n, uint16_t* planes, hipStream_t s);
 
 // ---- top-k kernels (topk.hip) -------------------------------------------
 // Dense scores, query-major [nq][ld] (first `rows` valid) -> per query the

@@ -20,12 +20,18 @@ class ResNet:
     """torchvision resnet children[:-2] trunk (networks/backbone.py:60-109:
     block1 = conv1/bn1/relu/maxpool, block2..5 = layer1..4), NHWC, BN folded.
 
-    forward(x_nhwc [B,H,W,3]) -> [B,H/32,W/32,2048] NHWC."""
+    forward(x_nhwc [B,H,W,3]) -> [B,H/32,W/32,2048] NHWC.
+
+    conv_math: "s3" (default) runs every conv with Cin % 32 == 0 on the
+    split-bf16 core (fp32-accurate, weights split once here); "f32" keeps all
+    convs on the exact-fp32 MFMA core.  The stem (Cin = 3) is always fp32."""
 
     outputdim_block5 = 2048
     outputdim_block4 = 1024
 
-    def __init__(self, name="resnet101", state_dict=None, seed=0, device="cuda"):
+    def __init__(self, name="resnet101", state_dict=None, seed=0, device="cuda", conv_math="s3"):
+        if conv_math not in ("s3", "f32"):
+            raise ValueError("conv_math must be 's3' or 'f32'")
         if name not in W.RESNET_LAYERS:
             raise ValueError(f"Unsupported or unknown architecture: {name}!")
         self.name = name
@@ -37,9 +43,16 @@ class ResNet:
         folded["conv1"] = (torch.nn.functional.pad(w1, (0, 1)).contiguous(), b1)
         self.convs = {k: (w.to(self.device), b.to(self.device)) for k, (w, b) in folded.items()}
         self.layers = W.RESNET_LAYERS[name]
+        self.conv_math = conv_math
+        self.convs_s3 = {}
+        if conv_math == "s3":
+            self.convs_s3 = {k: ops.split3_bf16(w) for k, (w, _) in self.convs.items() if w.shape[-1] % 32 == 0}
 
     def _conv(self, x, name, stride, pad, relu, residual=None):
         w, b = self.convs[name]
+        w3 = self.convs_s3.get(name)
+        if w3 is not None:
+            return ops.conv2d_s3(x, w3, b, stride, pad, residual, relu)
         return ops.conv2d(x, w, b, stride, pad, residual, relu)
 
     def forward(self, x):
@@ -115,12 +128,13 @@ class GeM(_Extractor):
 
     in_channels = 4
 
-    def __init__(self, outputdim=2048, backbone="resnet101", state_dict=None, whiten=None, seed=0, device="cuda"):
+    def __init__(self, outputdim=2048, backbone="resnet101", state_dict=None, whiten=None, seed=0, device="cuda",
+                 conv_math="s3"):
         if outputdim != 2048:
             raise ValueError("networks.GeM requires outputdim == 2048 (whiten is Conv2d(outputdim, 2048), "
                              "networks/RetrievalNet.py:332)")
         self.device = torch.device(device)
-        self.backbone = ResNet(backbone, state_dict, seed, device)
+        self.backbone = ResNet(backbone, state_dict, seed, device, conv_math)
         self.pooling = gem()
         if whiten is None:
             ww, wb = W.synthetic_linear(2048, outputdim, seed + 1)

@@ -89,6 +89,65 @@ def conv2d(x, w, bias, stride=1, pad=0, residual=None, relu=False):
     return y
 
 
+def split3_bf16(x):
+    """Exact 3-way bf16 split of an fp32 tensor: int16 planes [3, *x.shape]
+    (bf16 bit patterns) with x == p0 + p1 + p2 exactly (rr_split3_bf16)."""
+    x = _f32(x.contiguous(), "split3_bf16")
+    dev = _dev(x)
+    planes = torch.empty((3,) + tuple(x.shape), dtype=torch.int16, device=x.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_split3_bf16(hd, _ptr(x), x.numel(), _ptr(planes), _stream(dev)), hd, "rr_split3_bf16")
+    return planes
+
+
+def conv2d_s3(x, w3, bias, stride=1, pad=0, residual=None, relu=False):
+    """conv2d on the split-bf16 core: fp32-accurate, w3 = split3_bf16(w) with
+    w [Cout,KH,KW,Cin], Cin % 32 == 0."""
+    _f32(x, "conv2d_s3 x")
+    if w3.dtype != torch.int16 or w3.dim() != 5 or w3.shape[0] != 3 or not w3.is_contiguous():
+        raise ValueError("conv2d_s3: w3 must be contiguous int16 [3,Cout,KH,KW,Cin] (split3_bf16)")
+    dev = _dev(x)
+    b, h, wd, cin = x.shape
+    _, cout, kh, kw, cin_w = w3.shape
+    if cin_w != cin:
+        raise ValueError(f"conv2d_s3: Cin mismatch {cin} vs {cin_w}")
+    oh = (h + 2 * pad - kh) // stride + 1
+    ow = (wd + 2 * pad - kw) // stride + 1
+    y = torch.empty((b, oh, ow, cout), dtype=torch.float32, device=x.device)
+    if residual is not None:
+        _f32(residual, "conv2d_s3 residual")
+        if tuple(residual.shape) != tuple(y.shape):
+            raise ValueError("conv2d_s3: residual shape mismatch")
+    if bias is not None:
+        _f32(bias, "conv2d_s3 bias")
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_conv2d_s3(hd, _ptr(x), b, h, wd, cin, _ptr(w3), _ptr(bias), cout, kh, kw, stride, pad,
+                                       _ptr(residual), int(relu), _ptr(y), _stream(dev)), hd, "rr_conv2d_s3")
+    return y
+
+
+def linear_s3(x, w3, bias=None, residual=None, act=0):
+    """y = act(x @ w.T + bias + residual) on the split-bf16 core; w3 =
+    split3_bf16(w) with w [N,K], K % 32 == 0."""
+    _f32(x, "linear_s3 x")
+    if w3.dtype != torch.int16 or w3.dim() != 3 or w3.shape[0] != 3 or not w3.is_contiguous():
+        raise ValueError("linear_s3: w3 must be contiguous int16 [3,N,K] (split3_bf16)")
+    dev = _dev(x)
+    m, k = x.shape
+    n = w3.shape[1]
+    if w3.shape[2] != k:
+        raise ValueError("linear_s3: K mismatch")
+    y = torch.empty((m, n), dtype=torch.float32, device=x.device)
+    if residual is not None:
+        _f32(residual, "linear_s3 residual")
+        if tuple(residual.shape) != (m, n):
+            raise ValueError("linear_s3: residual shape mismatch")
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_linear_s3(hd, _ptr(x), m, k, _ptr(w3), _ptr(bias), n, _ptr(residual), int(act), _ptr(y),
+                                       _stream(dev)), hd, "rr_linear_s3")
+    return y
+
+
 def resize_bilinear(x_nhwc, out_h, out_w, scale_factor=None):
     """NHWC bilinear resize, align_corners=False.  With ``scale_factor`` the
     source index uses 1/scale_factor, as F.interpolate(scale_factor=s) does."""
