@@ -36,8 +36,10 @@ from research_image_retrieval_amd.networks import GeM, ConvDimReduction, GeMPCAw
 from research_image_retrieval_amd.extract import _rescale  # noqa: E402
 
 METRIC = "images embedded+ranked/sec on 1.6M×2048 gallery; mAP on ROxf/RPar"
-# MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) per input dtype, HBM3E peak
-PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "fp8": 5000.0}
+# MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) per input dtype, HBM3E peak.
+# "s3": fp32 products as six bf16 MFMA products (gemm_s3.hip), so its ceiling
+# in algorithmic fp32 FLOP/s is the bf16 peak / 6.
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "fp8": 5000.0, "s3": 2500.0 / 6}
 PEAK_HBM_GBS = 8000.0
 
 
@@ -61,8 +63,8 @@ def make_gallery(n_total, d, lo, hi, device, seed=0):
     return g
 
 
-def build_extractor(arch, device, seed=0):
-    net = GeM(2048, backbone=arch, seed=seed, device=device)
+def build_extractor(arch, device, seed=0, conv_math="s3"):
+    net = GeM(2048, backbone=arch, seed=seed, device=device, conv_math=conv_math)
     pw = ConvDimReduction(2048, 2048, device=device)
     w, b = W.synthetic_linear(2048, 2048, seed + 5, scale=1.0 / np.sqrt(2048))
     pw.set_params(w, b)
@@ -156,6 +158,9 @@ def main():
     ap.add_argument("--ranker", choices=("exhaustive", "prefilter"), default="prefilter",
                     help="fp32 exact ranking: exhaustive fp32 MFMA sweep, or the bf16-bound prefilter + exact "
                          "fp32 rescoring (bit-identical results)")
+    ap.add_argument("--conv-math", choices=("s3", "f32"), default="s3",
+                    help="ResNet trunk convs: s3 = fp32-accurate 3-way bf16 split on the bf16 matrix cores "
+                         "(error vs float64 <= the exact-fp32 core's, tests/test_gpu_s3.py); f32 = exact fp32 MFMA")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     a = ap.parse_args()
     if a.workload == "c4":
@@ -203,7 +208,7 @@ def main():
         net = VisionTransformer(224, 16, 768, 12, 12, a.dim, dtype="bf16" if a.dtype != "fp32" else "fp32",
                                 state_dict=W.synthetic_vit_state_dict(out_dim=a.dim, seed=0), device=dev)
     else:
-        net = build_extractor(a.arch, dev)
+        net = build_extractor(a.arch, dev, conv_math=a.conv_math)
     rs = np.random.RandomState(1234 + rank)
     imgs = torch.from_numpy(rs.randint(0, 256, size=(a.batch, 224, 224, 3), dtype=np.uint8)).to(dev)
     q_total = a.batch * world
@@ -340,8 +345,9 @@ def main():
         flop_filter = 2.0 * q_total * rows_filter * a.dim
     # (class, algorithmic FLOPs, algorithmic HBM bytes or None, dtype of its MFMA)
     searches = 2 if a.workload == "c5" else 1
+    conv_dt = a.dtype if a.workload == "c4" else ("s3" if a.conv_math == "s3" else "fp32")
     entries = (("cosine_filter", flop_filter, searches * float(rows_filter) * a.dim * esz, rank_dt),
-               ("conv_gemm", conv_flops_img * a.batch, None, a.dtype if a.workload == "c4" else "fp32"),
+               ("conv_gemm", conv_flops_img * a.batch, None, conv_dt),
                ("cosine_seed", flop_seed, searches * float(s_rows) * a.dim * esz, rank_dt),
                ("attention", attn_flops_img * a.batch, None, "fp32"))
     for name, fl_step, by_step, dt in entries:
@@ -360,11 +366,17 @@ def main():
             ach = fl_step / sec / 1e12
             e = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                  "frac": round(ach / peak, 4)}
-        e.update({"dtype": dt, "ms_per_step": round(ms / a.steps, 3), "launches_per_step": n / a.steps,
+        if dt == "s3":
+            e["math"] = ("fp32 via exact 3-way bf16 split: 6 bf16 MFMA products per fp32 product, fp32 accumulation; "
+                         "peak = bf16 dense peak / 6 (the stem conv, 1.5% of the FLOPs, runs on the exact-fp32 core)")
+            e["mfma_flop_per_launch"] = 6.0 * fl_step / max(1.0, n / a.steps)
+        e.update({"dtype": "fp32" if dt == "s3" else dt, "ms_per_step": round(ms / a.steps, 3),
+                  "launches_per_step": n / a.steps,
                   "algorithmic_flop_per_launch": fl_step / max(1.0, n / a.steps),
                   "algorithmic_bytes_per_launch": (by_step / max(1.0, n / a.steps)) if by_step else None,
                   "traffic": ((traffic or {}).get(name) or {}).get("hbm_bytes_per_launch")
-                  if (a.workload == "c3" and not pre) else None})
+                  if (traffic and traffic.get("workload") == a.workload and a.gallery == 1_600_000
+                      and a.batch == 320 and pre and a.conv_math == "s3") else None})
         rk[name] = e
     for name in ("select", "elementwise"):
         ms, n = cls[name]
@@ -387,7 +399,8 @@ def main():
                                      "exhaustive fp32 ranker)" if pre else ""),
                       "global_batch": q_total,
                       "images_per_gpu_per_step": a.batch, "gallery_rows": a.gallery, "dim": a.dim, "k": a.k,
-                      "parallelism": f"query-dp{world} + gallery-shard{world}"},
+                      "parallelism": f"query-dp{world} + gallery-shard{world}",
+                      "conv_math": a.conv_math if a.workload != "c4" else None},
            "roofline": roof, "roofline_by_kernel": rk}
     if exhaustive is not None:
         res["ranker"] = {"kind": "prefilter", "detail": "bf16-bound prefilter + exact fp32 rescoring; results "

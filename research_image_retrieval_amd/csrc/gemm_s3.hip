@@ -33,6 +33,7 @@
 namespace rr {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // exact 3-way split of x into bf16 pieces, returned as fp32 bit patterns
 // whose low 16 bits are zero
@@ -105,9 +106,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       const int ohw = g.OH * g.OW;
       const int b = mm / ohw, rem = mm - b * ohw;
       const int oh = rem / g.OW, ow = rem - oh * g.OW;
-      a_ptr[i] = g.A + (long long)b * g.H * g.W * g.Cin + a_slot * 8;
       a_ih0[i] = oh * g.stride - g.pad;
       a_iw0[i] = ow * g.stride - g.pad;
+      // the (possibly padded, out-of-image) top-left tap pixel; a k-tile adds a
+      // block-uniform offset (kh*W + kw)*Cin + cin0
+      a_ptr[i] = g.A + (((long long)b * g.H + a_ih0[i]) * g.W + a_iw0[i]) * g.Cin + a_slot * 8;
     }
   }
   f32x4 ra[A_CH][2];
@@ -124,31 +127,58 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       // Cin % 32 == 0: the whole k-tile lies in one (kh, kw) filter tap
       const int khw = k0 / g.Cin, cin0 = k0 - khw * g.Cin;
       const int kh = khw / g.KW, kw = khw - kh * g.KW;
+      const long long toff = (long long)(kh * g.W + kw) * g.Cin + cin0;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
         const bool ok = a_ok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        const f32x4* p = reinterpret_cast<const f32x4*>(a_ptr[i] + ((long long)ih * g.W + iw) * g.Cin + cin0);
+        const f32x4* p = reinterpret_cast<const f32x4*>(a_ptr[i] + toff);
         ra[i][0] = ok ? p[0] : f32x4{0.f, 0.f, 0.f, 0.f};
         ra[i][1] = ok ? p[1] : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
   };
-  auto store_a = [&](int buf) {
-    uint16_t* la = lds + buf * BUF;
+  // split the staged fp32 chunks into the three packed bf16 planes
+  u32x4 pk[A_CH][3];
+  auto split_a = [&]() {
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       uint32_t h[8], m[8], l[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) split3(ra[i][e >> 2][e & 3], h[e], m[e], l[e]);
+      for (int e = 0; e < 8; e += 2) {
+        // split3 on a pair: the subtractions as one v_pk_add_f32 each
+        const f32x2 x = {ra[i][e >> 2][e & 3], ra[i][e >> 2][(e & 3) + 1]};
+        const f32x2 xh = {__uint_as_float(__float_as_uint(x[0]) & 0xffff0000u),
+                          __uint_as_float(__float_as_uint(x[1]) & 0xffff0000u)};
+        const f32x2 r1 = x - xh;
+        const f32x2 r1h = {__uint_as_float(__float_as_uint(r1[0]) & 0xffff0000u),
+                           __uint_as_float(__float_as_uint(r1[1]) & 0xffff0000u)};
+        const f32x2 r2 = r1 - r1h;
+        h[e] = __float_as_uint(x[0]);  // pack2 keeps only the high halves
+        h[e + 1] = __float_as_uint(x[1]);
+        m[e] = __float_as_uint(r1[0]);
+        m[e + 1] = __float_as_uint(r1[1]);
+        l[e] = __float_as_uint(r2[0]);
+        l[e + 1] = __float_as_uint(r2[1]);
+      }
+      pk[i][0] = u32x4{pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
+      pk[i][1] = u32x4{pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7])};
+      pk[i][2] = u32x4{pack2(l[0], l[1]), pack2(l[2], l[3]), pack2(l[4], l[5]), pack2(l[6], l[7])};
+    }
+  };
+  auto write_a = [&](int buf) {
+    uint16_t* la = lds + buf * BUF;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
       const int row = a_row + i * A_RPP;
       const int off = row * BK + pswz<BK>(row, a_slot) * 8;
-      *reinterpret_cast<u32x4*>(la + off) = u32x4{pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
-      *reinterpret_cast<u32x4*>(la + BM * BK + off) =
-          u32x4{pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7])};
-      *reinterpret_cast<u32x4*>(la + 2 * BM * BK + off) =
-          u32x4{pack2(l[0], l[1]), pack2(l[2], l[3]), pack2(l[4], l[5]), pack2(l[6], l[7])};
+#pragma unroll
+      for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(la + p * BM * BK + off) = pk[i][p];
     }
+  };
+  auto store_a = [&](int buf) {
+    split_a();
+    write_a(buf);
   };
 
   // ---- B: three bf16 planes, LDS-DMA (64 lanes x 16 B = B_RPI whole plane
@@ -184,17 +214,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         if constexpr (SEP) lo[i][j][r] = 0.f;
       }
 
-  load_a(0);
-  glds_b(0, 0);
-  store_a(0);
-  __syncthreads();
-
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      load_a(kt + 1);
-      glds_b(kt + 1, cur ^ 1);
-    }
+  auto compute = [&](int cur) {
     const uint16_t* la = lds + cur * BUF;
     const uint16_t* lb = la + A_EL;
 #pragma unroll
@@ -229,8 +249,48 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
           L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], L, 0, 0, 0);
         }
     }
-    if (kt + 1 < nk) store_a(cur ^ 1);
-    __syncthreads();  // also retires the LDS-DMA of tile kt + 1
+  };
+
+  {
+    // Branch-free pipelined k-loop, raw barriers, counted vmcnt.  Entering
+    // iteration kt: tile kt is in LDS stage kt&1, the fp32 A chunks of tile
+    // kt+1 are in registers (loaded one iteration earlier).  The iteration
+    // splits them (pinned ahead of everything else by a scheduling barrier:
+    // while an LDS-DMA is in flight hipcc waits vmcnt(0) at the first use of
+    // a plain load's result, so that use must come before the next DMA is
+    // issued), issues the B DMA of tile kt+1 and the A loads of tile kt+2
+    // (indices clamped at the end: the extra copies land in a stage nobody
+    // reads), computes tile kt, writes the split A of tile kt+1 into the
+    // other stage, then waits for everything but the A loads of kt+2 before a
+    // raw barrier, so those stay in flight across it.
+    constexpr int A_LD = 2 * A_CH;  // A global loads per tile per thread
+    load_a(0);
+    glds_b(0, 0);
+    store_a(0);
+    load_a(nk > 1 ? 1 : 0);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      split_a();
+      // pin the split ahead of the DMA issue (an asm use of every result;
+      // volatile asm keeps its place relative to the DMA / loads below)
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) asm volatile("" ::"v"(pk[i][0]), "v"(pk[i][1]), "v"(pk[i][2]));
+      __builtin_amdgcn_sched_barrier(0);
+      glds_b(min(kt + 1, nk - 1), cur ^ 1);
+      load_a(min(kt + 2, nk - 1));
+      compute(cur);
+      write_a(cur ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of kt+1 landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
   }
 
   if constexpr (SEP) {
@@ -300,7 +360,8 @@ static int pick_s3(const GemmArgs& g) {
 template <int AM>
 static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s) {
   if (!s3_sep()) return launch_s3_t<2, 2, 2, 2, 16, AM, 0, 2>(g, s);
-  switch (pick_s3(g)) {
+  const int cfg = pick_s3(g);
+  switch (cfg) {
     case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1, 1>(g, s);
     case 3: return launch_s3_t<4, 2, 2, 2, 32, AM, 1, 1>(g, s);
     case 4: return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1>(g, s);

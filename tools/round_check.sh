@@ -1,6 +1,7 @@
 #!/bin/bash
-# One GPU call: parity tests, smoke, default bench, rocprofv3 kernel stats.
-# Every GPU step has its own time limit; steps are chained with && .
+# One GPU call: parity tests, smoke, default bench, rocprofv3 evidence
+# (kernel trace + stats, then one PMC pass per counter group).  Every GPU
+# step has its own time limit; steps are chained with && .
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/rc
@@ -9,5 +10,5 @@ cd $R
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 && \
 timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
 timeout -k 10 300 python -u bench.py > $O/bench_c3.json 2> $O/bench_c3.err && \
-(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run -- python3 $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $O/trace.log 2>&1) && \
+timeout -k 10 900 bash tools/profile.sh > $O/profile.log 2>&1 && \
 echo all-done

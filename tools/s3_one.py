@@ -1,0 +1,32 @@
+"""Run one conv shape on the split-bf16 core repeatedly (rocprofv3 counter
+passes).  usage: s3_one.py B H W Cin Cout K stride pad [res] [reps]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from research_image_retrieval_amd import ops  # noqa: E402
+
+b, h, w, cin, cout, k, s, p = (int(x) for x in sys.argv[1:9])
+res = len(sys.argv) > 9 and sys.argv[9] == "1"
+reps = int(sys.argv[10]) if len(sys.argv) > 10 else 20
+dev = torch.device("cuda:0")
+x = torch.relu(torch.randn(b, h, w, cin, device=dev))
+wt = torch.randn(cout, k, k, cin, device=dev) * 0.01
+w3 = ops.split3_bf16(wt)
+bias = torch.randn(cout, device=dev)
+oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+r = torch.randn(b, oh, ow, cout, device=dev) if res else None
+for _ in range(3):
+    ops.conv2d_s3(x, w3, bias, s, p, r, True)
+torch.cuda.synchronize()
+st = torch.cuda.Event(enable_timing=True)
+en = torch.cuda.Event(enable_timing=True)
+st.record()
+for _ in range(reps):
+    ops.conv2d_s3(x, w3, bias, s, p, r, True)
+en.record()
+torch.cuda.synchronize()
+ms = st.elapsed_time(en) / reps
+print({"ms": ms, "tflops": 2.0 * b * oh * ow * cout * k * k * cin / ms / 1e9})

@@ -13,20 +13,27 @@ import re
 import sys
 from collections import defaultdict
 
-CLASS = [(r"gemm_kernel<\d, \d, 0, 2[,>]", "cosine_filter"), (r"gemm_kernel<\d, \d, 0, 1[,>]", "cosine_seed"),
-         (r"gemm_kernel<\d, \d, [0-3], 0[,>]", "conv_gemm"), (r"select_|merge_kernel", "select"),
-         (r"attention_kernel", "attention"), (r"rr::", "elementwise")]
-
-
 def short(name):
     m = re.search(r"(rr::\w+(<[^>]*>)?)", name)
     return m.group(1) if m else name[:60]
 
 
 def cls_of(name):
-    for pat, c in CLASS:
-        if re.search(pat, name):
-            return c
+    """Kernel class as bench.py's timer classes: gemm_kernel<WM, WN, FM, FN,
+    AMODE, EMODE, ...> by its epilogue (EMODE 2 = cosine filter sweep, 1 =
+    seed scores, 0 = stored C: convs / linears); gemm_s3_kernel = convs."""
+    if "gemm_s3_kernel" in name:
+        return "conv_gemm"
+    m = re.search(r"gemm_kernel<([^>]*)>", name)
+    if m:
+        args = [int(x) for x in m.group(1).split(",")]
+        return {2: "cosine_filter", 1: "cosine_seed"}.get(args[5], "conv_gemm")
+    if re.search(r"select_|merge_kernel|prefilter_", name):
+        return "select"
+    if "attention_kernel" in name:
+        return "attention"
+    if "rr::" in name:
+        return "elementwise"
     return "other"
 
 
@@ -72,7 +79,12 @@ def main(src, tag):
     traffic = {}
     for c in ("cosine_filter", "cosine_seed", "conv_gemm"):
         rs = [r for r in rows if r["class"] == c and "read_bytes_per_launch" in r]
-        if c.startswith("cosine") and rs:  # one instantiation per step; others are side calls
+        if c.startswith("cosine") and rs:
+            # one instantiation per step, in the ranker's dtype (DT template
+            # arg: 1 = bf16 prefilter sweep, 0 = exhaustive fp32); the bench's
+            # side calls (exhaustive comparison, sanity search) are excluded
+            dt = os.environ.get("RR_PROFILE_RANK_DT", "1")
+            rs = [r for r in rs if r["kernel"].split(",")[7].strip() == dt] or rs
             rs = [max(rs, key=lambda r: r["total_ms"])]
         if rs:
             tot_calls = sum(r["calls"] for r in rs)
@@ -80,6 +92,7 @@ def main(src, tag):
             wb = sum(r.get("write_bytes_per_launch", 0) * r["calls"] for r in rs) / tot_calls
             traffic[c] = {"kernels": [r["kernel"] for r in rs], "hbm_read_bytes_per_launch": rb, "hbm_write_bytes_per_launch": wb,
                           "hbm_bytes_per_launch": rb + wb, "source": f"profiles/{tag}_kernel_summary.json"}
+    traffic["workload"] = os.environ.get("RR_PROFILE_WORKLOAD", "c3")
     with open(os.path.join(dst, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
     # raw rocprofv3 stats, committed verbatim
