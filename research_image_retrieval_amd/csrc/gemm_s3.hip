@@ -322,7 +322,10 @@ static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
 //   5: 256x64,  4 waves of 64x64, BK 32, 1/CU (120 KB)
 //   6: 256x64,  4 waves of 64x64, BK 16, 2/CU (60 KB)
 // Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the
-// fastest wherever N >= 128 (1.1-1.3x config 1 per FLOP).
+// fastest wherever N >= 128 (1.1-1.3x config 1 per FLOP).  An all-DMA ring
+// variant (A fp32 in LDS split at fragment-read time by an 8x1 wave layout,
+// BK 16, 5-6 stages, 3-4 k-tiles in flight) measured 10-15 % SLOWER than 3 on
+// every layer and was dropped (git history: "ring variant").
 // RR_S3_CFG=1..6 forces one; RR_S3_SEP=0 accumulates all six terms in one
 // register tile (accuracy experiment: measured LESS accurate than exact fp32,
 // so the default keeps the small terms apart).
