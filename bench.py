@@ -152,7 +152,7 @@ def main():
     ap.add_argument("--workload", choices=("c3", "c4", "c5"), default="c3",
                     help="c3: ResNet101-GeM 2048-d + PCA-w, fp32 (BASELINE metric config); "
                          "c4: ViT-B/16 CLS 512-d, bf16 GEMMs + bf16 cosine; "
-                         "c5: c3 extractor at 3 scales + fp8 cosine + alpha-QE re-rank (1 GPU)")
+                         "c5: c3 extractor at 3 scales + fp8 cosine + alpha-QE re-rank (sharded: neighbour rows fetched from their shards)")
     ap.add_argument("--dtype", choices=("fp32", "bf16", "fp8"), default=None,
                     help="GEMM input dtype (default: fp32 for c3, bf16 for c4)")
     ap.add_argument("--ranker", choices=("exhaustive", "prefilter"), default="prefilter",
@@ -192,8 +192,6 @@ def main():
     # one process per GPU; ranks beyond the visible devices share them (rehearsal)
     dev = torch.device("cuda", local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    if a.workload == "c5" and world > 1:
-        raise SystemExit("c5 is single-GPU in this round (sharded alpha-QE needs an all-reduce of partial expansions)")
     if world > 1:
         backend = os.environ.get("RR_DIST_BACKEND", "nccl")  # "gloo" only for 1-GPU rehearsals
         if backend == "nccl":
@@ -241,6 +239,10 @@ def main():
 
     def step():
         desc = embed()
+        if a.workload == "c5" and sharded is not None:
+            # sharded alpha-QE: neighbour rows fetched from their owning shards (bit-identical to 1 GPU)
+            s2, i2, _ = sharded.alpha_qe_search(desc, a.k, n=2, alpha=3.0)
+            return s2, i2
         if a.workload == "c5":
             q_lp, q_sc = ops.quantize_rows(desc, a.dtype)
             s1, i1 = ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws)

@@ -325,7 +325,7 @@ static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
 // fastest wherever N >= 128 (1.1-1.3x config 1 per FLOP).  An all-DMA ring
 // variant (A fp32 in LDS split at fragment-read time by an 8x1 wave layout,
 // BK 16, 5-6 stages, 3-4 k-tiles in flight) measured 10-15 % SLOWER than 3 on
-// every layer and was dropped (git history: "ring variant").
+// every layer and was dropped.
 // RR_S3_CFG=1..6 forces one; RR_S3_SEP=0 accumulates all six terms in one
 // register tile (accuracy experiment: measured LESS accurate than exact fp32,
 // so the default keeps the small terms apart).

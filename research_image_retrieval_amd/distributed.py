@@ -10,7 +10,17 @@ a contiguous gallery shard [lo_r, hi_r):
      receives, from every shard, the lists of its own B_r queries [W, B_r, k];
   4. k-way merge (rr_topk_merge), stable order (score desc, global idx asc).
 The collectives move Q*D*4 and B_r*W*k*12 bytes per rank: latency-bound next
-to the GEMM.  Ranking work per rank is Q x N/W, so the units (images embedded and
+to the GEMM.
+
+alpha-QE over the sharded gallery (config C5, ``alpha_qe_search``): after the
+first search each rank holds the merged top-n of its own queries; the n
+neighbour rows live on whichever shards own them.  Every rank learns all
+ranks' top-n indices (all-gather, Q*n*8 bytes), sends each other rank exactly
+the rows it owns for that rank's queries (one variable-split all-to-all,
+about B_r*n*D*4 bytes in per rank), and the receiver puts every row back in its
+(query, neighbour) slot.  The expansion then runs on copies of the very rows a
+single-GPU run reads, in the same order, so the expanded queries and the second
+search are bit-identical to the single-GPU path.  Ranking work per rank is Q x N/W, so the units (images embedded and
 ranked against the whole gallery) scale weakly with W.
 
 The reference has no distributed evaluation (NCCL is
@@ -93,6 +103,72 @@ class ShardedGallery:
             return ops.cosine_topk_lp(q_lp, q_sc, self.shard_lp, self.shard_scale, k, self.dtype,
                                       idx_offset=self.offset, workspace=self._ws)
         return ops.cosine_topk(q, self.shard, k, idx_offset=self.offset, workspace=self._ws)
+
+    def _bounds(self):
+        """[lo_r, hi_r) of every rank's shard (all-gathered once)."""
+        if getattr(self, "_his", None) is None:
+            group = self.group
+            t = torch.tensor([self.offset, self.offset + self.shard.shape[0]], dtype=torch.int64,
+                             device="cpu" if _host_staged(group) else self.shard.device)
+            parts = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+            dist.all_gather(parts, t, group=group)
+            self._his = torch.stack(parts)[:, 1].to(self.shard.device)
+        return self._his
+
+    def _owner(self, idx):
+        """Rank whose shard holds each global row index (shards are contiguous, in rank order)."""
+        return torch.bucketize(idx, self._bounds(), right=True)
+
+    def gather_rows(self, idx):
+        """Rows g[idx] of the global gallery for this rank's queries: idx
+        [B_r, n] int64 (global rows) -> [B_r, n, D] fp32, each row an exact
+        copy from the shard that owns it (one variable-split all-to-all)."""
+        group = self.group
+        world = dist.get_world_size(group)
+        rank = dist.get_rank(group)
+        dev = self.shard.device
+        b, n = idx.shape
+        d = self.shard.shape[1]
+        ids, sizes = _all_gather_var(idx.contiguous(), group)
+        send, send_counts = [], []
+        for t in range(world):
+            it = ids[t].reshape(-1).to(dev)
+            mine = it[self._owner(it) == rank] - self.offset  # row-major (query, neighbour) order
+            send.append(self.shard.index_select(0, mine))
+            send_counts.append(int(mine.numel()))
+        own = self._owner(idx.reshape(-1).to(dev))
+        recv_counts = [int((own == r).sum().item()) for r in range(world)]
+        sendbuf = torch.cat(send, 0) if send else self.shard.new_empty((0, d))
+        recvbuf = self.shard.new_empty((sum(recv_counts), d))
+        if _host_staged(group):
+            sendbuf, recvbuf = sendbuf.cpu(), recvbuf.cpu()
+        dist.all_to_all_single(recvbuf, sendbuf.contiguous(), recv_counts, send_counts, group=group)
+        recvbuf = recvbuf.to(dev)
+        out = self.shard.new_empty((b * n, d))
+        start = 0
+        for r in range(world):
+            pos = torch.nonzero(own == r).reshape(-1)
+            out[pos] = recvbuf[start:start + recv_counts[r]]
+            start += recv_counts[r]
+        return out.view(b, n, d)
+
+    def alpha_qe_search(self, queries, k=100, n=2, alpha=3.0, expand=None):
+        """Search, alpha-QE this rank's queries with their top-n neighbours
+        (rows fetched from their owning shards), search again (config C5).
+        Returns (scores [B_r,k], global idx [B_r,k], expanded queries)."""
+        s, i = self.search(queries, max(k, n))
+        rows = self.gather_rows(i[:, :n].contiguous())
+        top_s = s[:, :n].contiguous()
+        b = queries.shape[0]
+        if b == 0:  # no queries on this rank: still take part in the collectives
+            q2 = queries
+        elif expand is not None:
+            q2 = expand(queries, rows, top_s, n, alpha)
+        else:
+            local = torch.arange(b * n, dtype=torch.int64, device=queries.device).view(b, n)
+            q2 = ops.alpha_qe(queries.contiguous(), rows.view(b * n, rows.shape[-1]), local, top_s, n=n, alpha=alpha)
+        s2, i2 = self.search(q2, k)
+        return s2, i2, q2
 
     def _merge_parts(self, ps, pi, k):
         if self._merge is not None:

@@ -63,3 +63,57 @@ def test_sharded_search_world2_matches_single():
     i = np.concatenate([out[0][1], out[1][1]])
     np.testing.assert_array_equal(i, i_ref)
     np.testing.assert_array_equal(s, s_ref)
+
+
+def _expand(q, rows, top_s, n, alpha):
+    """alpha-QE on fetched rows with the oracle's float64 restatement."""
+    import oracle
+    b = q.shape[0]
+    idx = np.arange(b * n).reshape(b, n)
+    return torch.from_numpy(oracle.alpha_qe(q.numpy(), rows.reshape(b * n, rows.shape[-1]).numpy(), idx, top_s.numpy(), n, alpha))
+
+
+def _qe_worker(rank, world, port, q_all, g_all, k, sizes, out):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from research_image_retrieval_amd.distributed import ShardedGallery, shard_bounds
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = shard_bounds(g_all.shape[0], world, rank)
+    sg = ShardedGallery(g_all[lo:hi].contiguous(), lo, local_topk=_local_topk, merge=_merge)
+    qlo = sum(sizes[:rank])
+    mine = q_all[qlo:qlo + sizes[rank]].contiguous()
+    rows = sg.gather_rows(torch.tensor([[0, g_all.shape[0] - 1]] * sizes[rank], dtype=torch.int64).view(-1, 2))
+    s, i, q2 = sg.alpha_qe_search(mine, k, n=3, alpha=3.0, expand=_expand)
+    out[rank] = (s.numpy(), i.numpy(), q2.numpy(), rows.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sharded_alpha_qe_world3_matches_single():
+    """C5 over a sharded gallery: neighbour rows fetched from their owning
+    shards; expanded queries and the second search equal the single-process
+    pipeline bit for bit (3 ranks, ragged queries, one rank with none)."""
+    import oracle
+    rs = np.random.RandomState(1)
+    q = rs.standard_normal((6, 48)).astype(np.float32)
+    g = rs.standard_normal((700, 48)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    g[650] = q[0] * 0.9 + g[650] * 0.1  # a neighbour on the last shard
+    k, n = 15, 3
+    sizes = [4, 0, 2]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_qe_worker, args=(3, _free_port(), torch.from_numpy(q), torch.from_numpy(g), k, sizes, out),
+                       nprocs=3, join=True, start_method="spawn")
+    s1, i1 = oracle.cosine_topk(q, g, k)
+    q2 = oracle.alpha_qe(q, g, i1, s1, n, 3.0)
+    s2, i2 = oracle.cosine_topk(q2, g, k)
+    got = [out[r] for r in range(3)]
+    np.testing.assert_array_equal(np.concatenate([o[2] for o in got]), q2)
+    np.testing.assert_array_equal(np.concatenate([o[1] for o in got]), i2)
+    np.testing.assert_array_equal(np.concatenate([o[0] for o in got]), s2)
+    for o in got:  # gather_rows of the first and the last gallery row
+        assert np.array_equal(o[3][:, 0], np.broadcast_to(g[0], o[3][:, 0].shape))
+        assert np.array_equal(o[3][:, 1], np.broadcast_to(g[-1], o[3][:, 1].shape))

@@ -52,3 +52,47 @@ def test_sharded_search_real_kernels_world2(prefilter):
     s_o, i_o = oracle.cosine_topk(q, g, k)
     assert np.array_equal(i, i_o) and np.array_equal(s, s_o)
     assert list(i[0, :2]) == [10, 60_000]
+
+
+def _qe_worker(rank, world, port, q_all, g_all, k, sizes, dtype, out):
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from research_image_retrieval_amd.distributed import ShardedGallery, shard_bounds
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda:0")
+    lo, hi = shard_bounds(g_all.shape[0], world, rank)
+    sg = ShardedGallery(g_all[lo:hi].contiguous().to(dev), lo, dtype=dtype)
+    qlo = sum(sizes[:rank])
+    s, i, q2 = sg.alpha_qe_search(q_all[qlo:qlo + sizes[rank]].contiguous().to(dev), k, n=2, alpha=3.0)
+    out[rank] = (s.cpu().numpy(), i.cpu().numpy(), q2.cpu().numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dtype", ["fp8", "fp32"])
+def test_sharded_alpha_qe_real_kernels_world2(cuda, dtype):
+    """C5's alpha-QE re-search over a 2-way sharded gallery (rows fetched from
+    their owning shard) == the single-GPU alpha_qe_search, bit for bit."""
+    from test_distributed_gloo import _free_port
+    from research_image_retrieval_amd.search import GallerySearcher, alpha_qe_search
+    rs = np.random.RandomState(5)
+    d = 256
+    q = rs.standard_normal((7, d)).astype(np.float32)
+    g = rs.standard_normal((50_001, d)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    g[40_000] = q[1] * 0.8 + g[40_000] * 0.2  # a strong neighbour on shard 1 for a rank-0 query
+    g[40_000] /= np.linalg.norm(g[40_000])
+    k = 50
+    sizes = [3, 4]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_qe_worker, args=(2, _free_port(), torch.from_numpy(q), torch.from_numpy(g), k, sizes, dtype,
+                                         out), nprocs=2, join=True, start_method="spawn")
+    srch = GallerySearcher(torch.from_numpy(g), device=cuda, normalize=False, dtype=dtype)
+    s_ref, i_ref, q2_ref = alpha_qe_search(srch, torch.from_numpy(q), k=k, n=2, alpha=3.0, normalize=False)
+    got = [out[0], out[1]]
+    assert np.array_equal(np.concatenate([o[2] for o in got]), q2_ref.cpu().numpy())
+    assert np.array_equal(np.concatenate([o[1] for o in got]), i_ref.cpu().numpy())
+    assert np.array_equal(np.concatenate([o[0] for o in got]), s_ref.cpu().numpy())
