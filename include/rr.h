@@ -285,8 +285,15 @@ int rr_vit_tokens(rr_handle_t h, const float* patches, int b, int npatch,
 int rr_attention(rr_handle_t h, const float* qkv, int b, int seq, int heads,
                  int head_dim, float* out, void* stream);
 /* Same, output dtype 0 = fp32, 1 = bf16.                                   */
+/* (rr_attention_bf16 below: the C4 bf16 variant.)                          */
 int rr_attention_ex(rr_handle_t h, const float* qkv, int b, int seq, int heads,
                     int head_dim, int out_dtype, void* out, void* stream);
+
+/* The attention core on bf16 MFMA (config C4): q, k, v rounded to bf16 (RNE),
+ * fp32 accumulation and fp32 softmax, P rounded to bf16 for P.V; output fp32
+ * (out_dtype 0) or bf16 (1).  Same contract as rr_attention_ex.             */
+int rr_attention_bf16(rr_handle_t h, const float* qkv, int b, int seq, int heads,
+                      int head_dim, int out_dtype, void* out, void* stream);
 
 /* Row-wise L2 normalisation x / max(||x||_2, eps), in place allowed.
  * Replaces F.normalize (networks/RetrievalNet.py:343, models/gem_pooling.py:91,

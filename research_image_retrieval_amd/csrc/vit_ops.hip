@@ -10,6 +10,7 @@ namespace rr {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // One wave per row: y = (x - mean) / sqrt(var + eps) * gamma + beta, biased
 // variance, two-pass over the row held in registers (D <= 64 * 64).
@@ -219,6 +220,170 @@ __global__ __launch_bounds__(64 * NC) void attention_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fused attention on bf16 MFMA (v_mfma_f32_32x32x16_bf16), fp32 softmax: the
+// C4 (bf16) ViT.  Same structure as attention_kernel: workgroup = (batch,
+// head), wave w owns queries [32w, 32w+32), S^T = K . Q^T in NC accumulator
+// tiles (lane = query, registers = keys), exact fp32 softmax in registers,
+// then O = P . V with P packed to bf16 straight from the accumulator.  For PV
+// MFMA step (key tile kc, half s) lane half lh supplies the keys
+// kc*32 + 16s + 4lh + {0..3} and + 8 + {0..3} (the accumulator's own key
+// order); V is staged transposed (Vt[d][key], 520-B rows: row d starts at
+// bank 2d, so a lane group's ds_read_b64 of 32 d-rows is conflict-free) and
+// read at exactly those keys.  K rows are 128 B with 16-B slots swizzled by
+// (row >> 1) & 7 (conflict-free fragment reads, as the GEMM core).
+template <int NC, typename OutT>
+__global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const float* __restrict__ qkv, int B, int L, int NH,
+                                                                 OutT* __restrict__ out) {
+  constexpr int HD = 64, LP = NC * 32, VS = 260;
+  extern __shared__ __attribute__((aligned(16))) uint16_t sm16[];
+  uint16_t* Ks = sm16;            // [LP][HD] bf16
+  uint16_t* Vt = sm16 + LP * HD;  // [HD][VS] bf16
+  const int bh = blockIdx.x;
+  const int b = bh / NH, h = bh - (bh / NH) * NH;
+  const int width = NH * HD;
+  const long long ld = 3LL * width;
+  const float* base = qkv + (long long)b * L * ld;
+  const int tid = threadIdx.x;
+  for (int idx = tid; idx < LP * (HD / 4); idx += 64 * NC) {
+    const int row = idx / (HD / 4), s4 = idx - row * (HD / 4);
+    f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+    if (row < L) {
+      kv = *reinterpret_cast<const f32x4*>(base + (long long)row * ld + width + h * HD + s4 * 4);
+      vv = *reinterpret_cast<const f32x4*>(base + (long long)row * ld + 2 * width + h * HD + s4 * 4);
+    }
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const bf16x4 kb = {(__bf16)kv[0], (__bf16)kv[1], (__bf16)kv[2], (__bf16)kv[3]};
+    *reinterpret_cast<bf16x4*>(Ks + row * HD + (((s4 >> 1) ^ ((row >> 1) & 7)) * 8) + (s4 & 1) * 4) = kb;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const __bf16 v = (__bf16)vv[e];
+      Vt[(s4 * 4 + e) * VS + row] = __builtin_bit_cast(uint16_t, v);
+    }
+  }
+  const int wave = tid >> 6, lane = tid & 63;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int q0 = wave * 32;
+  // Q^T fragment (B operand): lane (query, lh) holds Q[query][16c + 8lh + e] / 8
+  bf16x8 qf[4];
+  {
+    const int q = q0 + lr;
+    const bool ok = q < L;
+    const float* qp = base + (long long)(ok ? q : 0) * ld + h * HD;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const f32x4 a = *reinterpret_cast<const f32x4*>(qp + 16 * c + 8 * lh);
+      const f32x4 bq = *reinterpret_cast<const f32x4*>(qp + 16 * c + 8 * lh + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        qf[c][e] = (__bf16)(ok ? a[e] * 0.125f : 0.f);
+        qf[c][4 + e] = (__bf16)(ok ? bq[e] * 0.125f : 0.f);
+      }
+    }
+  }
+  __syncthreads();
+  f32x16 st[NC];
+#pragma unroll
+  for (int kc = 0; kc < NC; ++kc) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) st[kc][r] = 0.f;
+    const int krow = kc * 32 + lr;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const bf16x8 kf =
+          *reinterpret_cast<const bf16x8*>(Ks + krow * HD + (((2 * c + lh) ^ ((krow >> 1) & 7)) * 8));
+      st[kc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[c], st[kc], 0, 0, 0);
+    }
+  }
+  float mx = -__builtin_inff();
+#pragma unroll
+  for (int kc = 0; kc < NC; ++kc)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int key = kc * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
+      if (key >= L) st[kc][r] = -__builtin_inff();
+      mx = fmaxf(mx, st[kc][r]);
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float sum = 0.f;
+#pragma unroll
+  for (int kc = 0; kc < NC; ++kc)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = expf(st[kc][r] - mx);
+      st[kc][r] = p;
+      sum += p;
+    }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.0f / sum;
+  f32x16 o[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
+  typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+#pragma unroll
+  for (int kc = 0; kc < NC; ++kc) {
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      bf16x8 pf;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) pf[e] = (__bf16)st[kc][8 * s2 + e];
+      const int k0 = kc * 32 + 16 * s2 + 4 * lh;
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const uint16_t* vr = Vt + (32 * t + lr) * VS + k0;
+        const u16x4 va = *reinterpret_cast<const u16x4*>(vr);
+        const u16x4 vb = *reinterpret_cast<const u16x4*>(vr + 8);
+        const u16x4 vv[2] = {va, vb};
+        bf16x8 vf;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) vf[e] = __builtin_bit_cast(__bf16, vv[e >> 2][e & 3]);
+        o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, vf, o[t], 0, 0, 0);
+      }
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int qi = (r & 3) + 8 * (r >> 2) + 4 * lh;
+    const float iq = __shfl(inv, qi, 64);
+    const int q = q0 + qi;
+    if (q < L) {
+      OutT* op = out + ((long long)b * L + q) * width + h * HD;
+      op[lr] = (OutT)(o[0][r] * iq);
+      op[32 + lr] = (OutT)(o[1][r] * iq);
+    }
+  }
+}
+
+template <int NC, typename OutT>
+static hipError_t launch_attn_bf16(const float* qkv, int B, int L, int NH, OutT* out, hipStream_t s) {
+  const size_t lds = ((size_t)NC * 32 * 64 + 64 * 260) * 2;
+  if (lds > 64 * 1024) {
+    hipError_t e = hipFuncSetAttribute((const void*)attention_bf16_kernel<NC, OutT>,
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
+  hipLaunchKernelGGL((attention_bf16_kernel<NC, OutT>), dim3((unsigned)(B * NH)), dim3(64 * NC), lds, s, qkv, B, L,
+                     NH, out);
+  return hipGetLastError();
+}
+
+template <typename OutT>
+static hipError_t launch_attn_bf16_nc(int nc, const float* qkv, int b, int seq, int heads, OutT* out,
+                                      hipStream_t s) {
+  switch (nc) {
+    case 1: return launch_attn_bf16<1>(qkv, b, seq, heads, out, s);
+    case 2: return launch_attn_bf16<2>(qkv, b, seq, heads, out, s);
+    case 3: return launch_attn_bf16<3>(qkv, b, seq, heads, out, s);
+    case 4: return launch_attn_bf16<4>(qkv, b, seq, heads, out, s);
+    case 5: return launch_attn_bf16<5>(qkv, b, seq, heads, out, s);
+    case 6: return launch_attn_bf16<6>(qkv, b, seq, heads, out, s);
+    case 7: return launch_attn_bf16<7>(qkv, b, seq, heads, out, s);
+    default: return launch_attn_bf16<8>(qkv, b, seq, heads, out, s);
+  }
+}
+
 static dim3 grid_for(long long n, int block) {
   long long g = (n + block - 1) / block;
   if (g > 256 * 16) g = 256 * 16;
@@ -337,4 +502,19 @@ extern "C" int rr_attention_ex(rr_handle_t h, const float* qkv, int b, int seq, 
   const hipError_t e = out_dtype == 1 ? launch_attn_nc<__bf16>(nc, qkv, b, seq, heads, (__bf16*)out, s)
                                       : launch_attn_nc<float>(nc, qkv, b, seq, heads, (float*)out, s);
   return check_hip(h, e, "attention launch");
+}
+
+extern "C" int rr_attention_bf16(rr_handle_t h, const float* qkv, int b, int seq, int heads, int head_dim,
+                                 int out_dtype, void* out, void* stream) {
+  if (!h) return RR_EINVAL;
+  if (!qkv || !out || b < 0 || heads <= 0 || head_dim != 64 || seq <= 0 || seq > 256 ||
+      (out_dtype != 0 && out_dtype != 1))
+    return set_error(h, RR_EINVAL, "rr_attention_bf16: supports head_dim == 64, 1 <= seq <= 256, out_dtype 0|1");
+  if (b == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeAttn, s);
+  const int nc = (seq + 31) / 32;
+  const hipError_t e = out_dtype == 1 ? launch_attn_bf16_nc<__bf16>(nc, qkv, b, seq, heads, (__bf16*)out, s)
+                                      : launch_attn_bf16_nc<float>(nc, qkv, b, seq, heads, (float*)out, s);
+  return check_hip(h, e, "attention_bf16 launch");
 }

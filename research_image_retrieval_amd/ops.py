@@ -416,13 +416,15 @@ def layernorm_bf16(x, gamma, beta, eps=1e-5):
     return y
 
 
-def attention_bf16(qkv, b, seq, heads, head_dim=64):
+def attention_bf16(qkv, b, seq, heads, head_dim=64, bf16_math=True):
+    """Attention core for the bf16 ViT: bf16 output; bf16 MFMA with fp32
+    softmax (rr_attention_bf16), or fp32 MFMA (bf16_math=False)."""
     _f32(qkv, "attention_bf16")
     dev = _dev(qkv)
     out = torch.empty((b * seq, heads * head_dim), dtype=torch.bfloat16, device=qkv.device)
     hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_attention_ex(hd, _ptr(qkv), b, seq, heads, head_dim, 1, _ptr(out), _stream(dev)), hd,
-               "rr_attention_ex")
+    fn = _lib.lib().rr_attention_bf16 if bf16_math else _lib.lib().rr_attention_ex
+    _lib.check(fn(hd, _ptr(qkv), b, seq, heads, head_dim, 1, _ptr(out), _stream(dev)), hd, "rr_attention_bf16")
     return out
 
 

@@ -61,3 +61,24 @@ def test_layernorm_and_quickgelu(cuda):
     refg = (z * torch.sigmoid(1.702 * z)).float()
     torch.testing.assert_close(ops.linear_ex(a.to(cuda), wt.to(cuda), b2.to(cuda), act=2).cpu(), refg,
                                rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.parametrize("seq", [197, 50, 256, 31])
+def test_attention_bf16_kernel_vs_float64(cuda, seq):
+    """bf16-MFMA attention (C4): q/k/v and P rounded to bf16, fp32 softmax.
+    Against the float64 attention of the bf16-rounded q/k/v: per-row cosine
+    >= 0.9999 and max-abs error <= 1e-2 (P's bf16 rounding is the error)."""
+    b, heads, hd = 3, 4, 64
+    g = torch.Generator().manual_seed(seq)
+    qkv = torch.randn(b * seq, 3 * heads * hd, generator=g)
+    out = ops.attention_bf16(qkv.to(cuda), b, seq, heads).float().cpu().double()
+    out32 = ops.attention_bf16(qkv.to(cuda), b, seq, heads, bf16_math=False).float().cpu().double()
+    x = qkv.bfloat16().double().view(b, seq, 3, heads, hd)
+    q, k, v = x[:, :, 0].transpose(1, 2), x[:, :, 1].transpose(1, 2), x[:, :, 2].transpose(1, 2)
+    ref = torch.softmax(q @ k.transpose(-1, -2) / 8.0, -1) @ v
+    ref = ref.transpose(1, 2).reshape(b * seq, heads * hd)
+    cos = torch.nn.functional.cosine_similarity(out.view(-1, hd), ref.view(-1, hd), dim=1)
+    err = (out - ref).abs().max().item()
+    print(f"seq {seq}: bf16-math max|err| {err:.3g} min cos {cos.min().item():.6f}; "
+          f"fp32-math max|err| {(out32 - ref).abs().max().item():.3g}")
+    assert cos.min().item() >= 0.9999 and err <= 1e-2
