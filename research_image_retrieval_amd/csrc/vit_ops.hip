@@ -321,7 +321,7 @@ __global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const float* __
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
-  typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 #pragma unroll
   for (int kc = 0; kc < NC; ++kc) {
 #pragma unroll
@@ -333,12 +333,11 @@ __global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const float* __
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
         const uint16_t* vr = Vt + (32 * t + lr) * VS + k0;
-        const u16x4 va = *reinterpret_cast<const u16x4*>(vr);
-        const u16x4 vb = *reinterpret_cast<const u16x4*>(vr + 8);
-        const u16x4 vv[2] = {va, vb};
-        bf16x8 vf;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) vf[e] = __builtin_bit_cast(__bf16, vv[e >> 2][e & 3]);
+        // (element-wise assembly from two u16x4 through bit_cast miscompiles
+        // to a broadcast of element 0 under hipcc -O3: concatenate instead)
+        const bf16x4 va = *reinterpret_cast<const bf16x4*>(vr);
+        const bf16x4 vb = *reinterpret_cast<const bf16x4*>(vr + 8);
+        const bf16x8 vf = __builtin_shufflevector(va, vb, 0, 1, 2, 3, 4, 5, 6, 7);
         o[t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(pf, vf, o[t], 0, 0, 0);
       }
     }
