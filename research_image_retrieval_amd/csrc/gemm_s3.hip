@@ -119,9 +119,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     if constexpr (AMODE == A_DENSE) {
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
-        const f32x4* p = reinterpret_cast<const f32x4*>(a_ptr[i] + k0);
-        ra[i][0] = a_ok[i] ? p[0] : f32x4{0.f, 0.f, 0.f, 0.f};
-        ra[i][1] = a_ok[i] ? p[1] : f32x4{0.f, 0.f, 0.f, 0.f};
+        // every load is issued (from the base when out of range, then zeroed):
+        // the counted vmcnt of the k-loop assumes A_LD loads per tile
+        const f32x4* p = reinterpret_cast<const f32x4*>(a_ok[i] ? a_ptr[i] + k0 : g.A);
+        const f32x4 v0 = p[0], v1 = p[1];
+        ra[i][0] = a_ok[i] ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
+        ra[i][1] = a_ok[i] ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     } else {
       // Cin % 32 == 0: the whole k-tile lies in one (kh, kw) filter tap
@@ -132,9 +135,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       for (int i = 0; i < A_CH; ++i) {
         const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
         const bool ok = a_ok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        const f32x4* p = reinterpret_cast<const f32x4*>(a_ptr[i] + toff);
-        ra[i][0] = ok ? p[0] : f32x4{0.f, 0.f, 0.f, 0.f};
-        ra[i][1] = ok ? p[1] : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4* p = reinterpret_cast<const f32x4*>(ok ? a_ptr[i] + toff : g.A);
+        const f32x4 v0 = p[0], v1 = p[1];
+        ra[i][0] = ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
+        ra[i][1] = ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
   };
@@ -325,7 +329,9 @@ static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
 // fastest wherever N >= 128 (1.1-1.3x config 1 per FLOP).  An all-DMA ring
 // variant (A fp32 in LDS split at fragment-read time by an 8x1 wave layout,
 // BK 16, 5-6 stages, 3-4 k-tiles in flight) measured 10-15 % SLOWER than 3 on
-// every layer and was dropped.
+// every layer and was dropped.  So was a one-wave-per-SIMD variant (4 waves,
+// 256x128, each wave 128x64 with two fragment sets in flight and the A split
+// interleaved between MFMAs): 1.16x slower over the trunk (36.3 vs 31.4 ms).
 // RR_S3_CFG=1..6 forces one; RR_S3_SEP=0 accumulates all six terms in one
 // register tile (accuracy experiment: measured LESS accurate than exact fp32,
 // so the default keeps the small terms apart).
