@@ -60,7 +60,33 @@ __device__ __forceinline__ int pswz(int row, int slot) {
   else return slot ^ ((row >> 3) & 1);
 }
 
-template <int WM, int WN, int FM, int FN, int BK, int AMODE, int SEP, int MINB>
+// 32 zero bytes in global memory: the A source of padding taps and rows past M
+__device__ f32x4 s3_zero_src[2];
+__device__ __forceinline__ const f32x4* s3_zero_page() { return s3_zero_src; }
+
+// Two consecutive 16-B loads.  ASYNC: issued by inline asm, so hipcc keeps no
+// scoreboard entry for them: with LDS-DMA in flight it otherwise waits
+// vmcnt(0) at the first use of any plain load's result (mixed VMEM event
+// types make it treat the counter as out of order), which drains the A
+// prefetch every iteration.  The caller waits with a counted vmcnt and
+// launders the registers (s3_launder) before using them.
+template <int ASYNC>
+__device__ __forceinline__ void s3_load2(const f32x4* p, f32x4 (&r)[2]) {
+  if constexpr (ASYNC) {
+    asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:16"
+                 : "=&v"(r[0]), "=&v"(r[1])
+                 : "v"(p)
+                 : "memory");
+  } else {
+    r[0] = p[0];
+    r[1] = p[1];
+  }
+}
+// a fresh definition of v after the preceding (volatile) wait: nothing that
+// reads v can be scheduled above it
+__device__ __forceinline__ void s3_launder(f32x4& v) { asm volatile("" : "+v"(v)); }
+
+template <int WM, int WN, int FM, int FN, int BK, int AMODE, int SEP, int MINB, int PIPE>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int WTM = 32 * FM, WTN = 32 * FN;
@@ -113,18 +139,19 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       a_ptr[i] = g.A + (((long long)b * g.H + a_ih0[i]) * g.W + a_iw0[i]) * g.Cin + a_slot * 8;
     }
   }
-  f32x4 ra[A_CH][2];
-  auto load_a = [&](int kt) {
+  f32x4 ra2[2][A_CH][2];
+  auto load_a = [&](int kt, int rb) {
+    f32x4(&ra)[A_CH][2] = ra2[rb];
     const int k0 = kt * BK;
     if constexpr (AMODE == A_DENSE) {
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
-        // every load is issued (from the base when out of range, then zeroed):
-        // the counted vmcnt of the k-loop assumes A_LD loads per tile
-        const f32x4* p = reinterpret_cast<const f32x4*>(a_ok[i] ? a_ptr[i] + k0 : g.A);
-        const f32x4 v0 = p[0], v1 = p[1];
-        ra[i][0] = a_ok[i] ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
-        ra[i][1] = a_ok[i] ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
+        // every load is issued (the counted vmcnt of the k-loop assumes A_LD
+        // loads per tile); out-of-range rows read the zero page, so the
+        // loaded registers are used as they are, no select after the load
+        // (a select right after it makes hipcc wait for the load at once)
+        const f32x4* p = a_ok[i] ? reinterpret_cast<const f32x4*>(a_ptr[i] + k0) : s3_zero_page();
+        s3_load2<PIPE>(p, ra[i]);
       }
     } else {
       // Cin % 32 == 0: the whole k-tile lies in one (kh, kw) filter tap
@@ -135,16 +162,15 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       for (int i = 0; i < A_CH; ++i) {
         const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
         const bool ok = a_ok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
-        const f32x4* p = reinterpret_cast<const f32x4*>(ok ? a_ptr[i] + toff : g.A);
-        const f32x4 v0 = p[0], v1 = p[1];
-        ra[i][0] = ok ? v0 : f32x4{0.f, 0.f, 0.f, 0.f};
-        ra[i][1] = ok ? v1 : f32x4{0.f, 0.f, 0.f, 0.f};
+        const f32x4* p = ok ? reinterpret_cast<const f32x4*>(a_ptr[i] + toff) : s3_zero_page();
+        s3_load2<PIPE>(p, ra[i]);
       }
     }
   };
   // split the staged fp32 chunks into the three packed bf16 planes
   u32x4 pk[A_CH][3];
-  auto split_a = [&]() {
+  auto split_a = [&](int rb) {
+    const f32x4(&ra)[A_CH][2] = ra2[rb];
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       uint32_t h[8], m[8], l[8];
@@ -180,8 +206,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(la + p * BM * BK + off) = pk[i][p];
     }
   };
-  auto store_a = [&](int buf) {
-    split_a();
+  auto store_a = [&](int rb, int buf) {
+    split_a(rb);
     write_a(buf);
   };
 
@@ -198,11 +224,13 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   }
   auto glds_b = [&](int kt, int buf) {
     uint16_t* lb = lds + buf * BUF + A_EL;
+    // every wave issues B_INS (the counted vmcnt assumes it): in a partial
+    // last round the surplus waves repeat the last row group (same source,
+    // same LDS destination)
 #pragma unroll
     for (int i = 0; i < B_INS; ++i)
-      if (B_TI % NW == 0 || i * NW + wave < B_TI)
-        __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + (long long)kt * BK),
-                                       (__attribute__((address_space(3))) void*)(lb + (i * NW + wave) * B_RPI * BK),
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + (long long)kt * BK),
+                                       (__attribute__((address_space(3))) void*)(lb + min(i * NW + wave, B_TI - 1) * B_RPI * BK),
                                        16, 0, 0);
   };
 
@@ -218,11 +246,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         if constexpr (SEP) lo[i][j][r] = 0.f;
       }
 
-  auto compute = [&](int cur) {
+  auto compute_st = [&](int cur, int st) {
     const uint16_t* la = lds + cur * BUF;
     const uint16_t* lb = la + A_EL;
-#pragma unroll
-    for (int st = 0; st < BK / 16; ++st) {
+    {
       bf16x8 a[3][FM], b[3][FN];
 #pragma unroll
       for (int p = 0; p < 3; ++p) {
@@ -254,38 +281,40 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         }
     }
   };
+  auto compute = [&](int cur) {
+#pragma unroll
+    for (int st = 0; st < BK / 16; ++st) compute_st(cur, st);
+  };
 
-  {
-    // Branch-free pipelined k-loop, raw barriers, counted vmcnt.  Entering
-    // iteration kt: tile kt is in LDS stage kt&1, the fp32 A chunks of tile
-    // kt+1 are in registers (loaded one iteration earlier).  The iteration
-    // splits them (pinned ahead of everything else by a scheduling barrier:
-    // while an LDS-DMA is in flight hipcc waits vmcnt(0) at the first use of
-    // a plain load's result, so that use must come before the next DMA is
-    // issued), issues the B DMA of tile kt+1 and the A loads of tile kt+2
-    // (indices clamped at the end: the extra copies land in a stage nobody
-    // reads), computes tile kt, writes the split A of tile kt+1 into the
-    // other stage, then waits for everything but the A loads of kt+2 before a
-    // raw barrier, so those stay in flight across it.
-    constexpr int A_LD = 2 * A_CH;  // A global loads per tile per thread
-    load_a(0);
+  constexpr int A_LD = 2 * A_CH;  // A global loads per tile per thread
+  if constexpr (PIPE == 0) {
+    // Pipelined k-loop, raw barriers, counted vmcnt, plain A loads.
+    // Entering iteration kt: tile kt is in LDS stage kt&1, the fp32 A chunks
+    // of tile kt+1 are in registers (loaded one iteration earlier).  The
+    // iteration splits them (pinned ahead of everything else: hipcc waits
+    // vmcnt(0) at the first use of a plain load's result while an LDS-DMA is
+    // in flight, so that use must come before the next DMA is issued), issues
+    // the B DMA of tile kt+1 and the A loads of tile kt+2 (indices clamped at
+    // the end: the extra copies land in a stage nobody reads), computes tile
+    // kt, writes the split A of tile kt+1 into the other stage, then waits
+    // for everything but the A loads of kt+2 before a raw barrier, so those
+    // stay in flight across it.
+    load_a(0, 0);
     glds_b(0, 0);
-    store_a(0);
-    load_a(nk > 1 ? 1 : 0);
+    store_a(0, 0);
+    load_a(nk > 1 ? 1 : 0, 0);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
-      split_a();
-      // pin the split ahead of the DMA issue (an asm use of every result;
-      // volatile asm keeps its place relative to the DMA / loads below)
+      split_a(0);
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) asm volatile("" ::"v"(pk[i][0]), "v"(pk[i][1]), "v"(pk[i][2]));
       __builtin_amdgcn_sched_barrier(0);
       glds_b(min(kt + 1, nk - 1), cur ^ 1);
-      load_a(min(kt + 2, nk - 1));
+      load_a(min(kt + 2, nk - 1), 0);
       compute(cur);
       write_a(cur ^ 1);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of kt+1 landed
@@ -293,9 +322,62 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
     }
+  } else {
+    // Pipelined k-loop with asynchronous A loads (s3_load2<1>), two register
+    // buffers: A(j) lives in buffer j&1.  Iteration kt issues the B DMA of
+    // tile kt+1 and the A loads of tile kt+2 (into the buffer A(kt) left),
+    // computes tile kt, then waits for everything but the A loads of kt+2
+    // (so A(kt+1) and B(kt+1) have landed), splits A(kt+1) into the other
+    // stage and crosses a raw barrier.  An A load thus has almost two
+    // iterations to land instead of one; its split runs between the MFMAs of
+    // the second 16-deep step.  The loop is unrolled by two so the stage and
+    // buffer indices are constants.
+    auto launder_a = [&](int rb) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) {
+        s3_launder(ra2[rb][i][0]);
+        s3_launder(ra2[rb][i][1]);
+      }
+    };
+    load_a(0, 0);
+    glds_b(0, 0);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_INS) : "memory");  // A(0) landed
+    launder_a(0);
+    store_a(0, 0);
+    load_a(nk > 1 ? 1 : 0, 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B(0) landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    auto iter = [&](int kt, int cur) __attribute__((always_inline)) {
+      glds_b(min(kt + 1, nk - 1), cur ^ 1);
+      load_a(min(kt + 2, nk - 1), cur);
+      compute_st(cur, 0);
+      // A(kt+1) landed (the B DMA of kt+1 and the A loads of kt+2 may not
+      // have): its split overlaps the remaining MFMAs of tile kt
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
+      launder_a(cur ^ 1);
+      split_a(cur ^ 1);
+#pragma unroll
+      for (int st = 1; st < BK / 16; ++st) compute_st(cur, st);
+      write_a(cur ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of kt+1 landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    for (int kt = 0; kt < nk; kt += 2) {
+      iter(kt, 0);
+      if (kt + 1 < nk) iter(kt + 1, 1);
+    }
+    // the clamped tail loads are still in flight: keep both buffers live
+    // until they have landed, so no later value is allocated to them
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    launder_a(0);
+    launder_a(1);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
 
   if constexpr (SEP) {
 #pragma unroll
@@ -306,6 +388,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   epilogue_store<WM, WN, FM, FN, BUF>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
 }
 
+static int s3_pipe();
+
 template <int WM, int WN, int FM, int FN, int BK, int AM, int SEP, int MINB>
 static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
@@ -313,8 +397,12 @@ static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, SEP, MINB>), dim3((unsigned)nblk), dim3(64 * WM * WN), 0,
-                     s, g, (int)tiles_n);
+  if (s3_pipe())
+    hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, SEP, MINB, 1>), dim3((unsigned)nblk), dim3(64 * WM * WN),
+                       0, s, g, (int)tiles_n);
+  else
+    hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, SEP, MINB, 0>), dim3((unsigned)nblk), dim3(64 * WM * WN),
+                       0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
 
@@ -339,6 +427,14 @@ static int s3_forced_cfg() {
   static const int v = [] {
     const char* e = getenv("RR_S3_CFG");
     return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+// RR_S3_PIPE=0 selects the plain-load k-loop (A prefetched one iteration ahead)
+static int s3_pipe() {
+  static const int v = [] {
+    const char* e = getenv("RR_S3_PIPE");
+    return e ? atoi(e) : 1;
   }();
   return v;
 }
