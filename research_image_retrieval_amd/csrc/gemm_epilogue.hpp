@@ -17,8 +17,8 @@ __device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f 
 // Stage the BM x BN accumulator tile (32x32 MFMA C/D layout: col = lane & 31,
 // row = (r&3) + 8(r>>2) + 4(lane>>5)) through LDS, then write whole rows: each
 // lane moves 16 B, 32 lanes cover a 512-B row run, the residual is read the
-// same way with every load in flight before the first use (one HBM round trip
-// per slab).  When the tile exceeds the CAPF floats of LDS it goes in P row
+// same way, every load of a slab issued before its accumulators are staged
+// (one HBM round trip per slab, overlapping the staging).  When the tile exceeds the CAPF floats of LDS it goes in P row
 // slabs.  Called by every thread of the block after the k-loop's last
 // barrier (the LDS is free).
 template <int WM, int WN, int FM, int FN, int CAPF>
@@ -40,6 +40,21 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
   float* ct = lds;  // [SLAB][BN] row-major
 #pragma unroll
   for (int p = 0; p < P; ++p) {
+    const int rbase = p * SLAB;
+    // single-slab tiles with registers to spare: the residual loads go out
+    // first, their HBM round trip overlapping the LDS staging of the
+    // accumulators and its barrier
+    constexpr bool PREF = P == 1 && ITERS * 4 + FM * FN * 16 <= 160;
+    f32x4 res[ITERS];
+    if (PREF && vec_ok && g.residual != nullptr) {
+#pragma unroll
+      for (int it = 0; it < ITERS; ++it) {
+        const int idx = tid + it * NT;
+        const int row = idx / C4, c4 = idx - row * C4;
+        const int m = m0 + rbase + row, n = n0 + c4 * 4;
+        if (m < g.M && n < g.N) res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
+      }
+    }
     if (p > 0) __syncthreads();
     if (wm / (WM / P) == p) {
 #pragma unroll
@@ -54,10 +69,8 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
           }
     }
     __syncthreads();
-    const int rbase = p * SLAB;
     if (vec_ok) {
-      f32x4 res[ITERS];
-      if (g.residual != nullptr) {
+      if (!PREF && g.residual != nullptr) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
           const int idx = tid + it * NT;
