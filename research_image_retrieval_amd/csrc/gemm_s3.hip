@@ -171,6 +171,17 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   u32x4 pk[A_CH][3];
   auto split_a = [&](int rb) {
     const f32x4(&ra)[A_CH][2] = ra2[rb];
+#ifdef RR_S3_ABLATE_SPLIT
+    // ablation build only (tools/build_variant.sh): no split VALU, wrong
+    // results; measured the split's cost at 7 % of the trunk (3x3: 13 %)
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      pk[i][0] = __builtin_bit_cast(u32x4, ra[i][0]);
+      pk[i][1] = __builtin_bit_cast(u32x4, ra[i][1]);
+      pk[i][2] = __builtin_bit_cast(u32x4, ra[i][0]);
+    }
+    return;
+#endif
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       uint32_t h[8], m[8], l[8];
