@@ -348,10 +348,16 @@ def main():
     # (class, algorithmic FLOPs, algorithmic HBM bytes or None, dtype of its MFMA)
     searches = 2 if a.workload == "c5" else 1
     conv_dt = a.dtype if a.workload == "c4" else ("s3" if a.conv_math == "s3" else "fp32")
+    # attention (C4): bf16 MFMA when the ViT runs in bf16; per layer it reads
+    # the QKV rows once and writes the head outputs
+    attn_dt = "bf16" if (a.workload == "c4" and a.dtype != "fp32") else "fp32"
+    # (the bf16 ViT's QKV linear writes bf16 rows, networks.VisionTransformer._forward_bf16)
+    attn_bytes = (12.0 * a.batch * 197 * 768 * (3 + 1) * (2 if attn_dt == "bf16" else 4)
+                  if a.workload == "c4" else None)
     entries = (("cosine_filter", flop_filter, searches * float(rows_filter) * a.dim * esz, rank_dt),
                ("conv_gemm", conv_flops_img * a.batch, None, conv_dt),
                ("cosine_seed", flop_seed, searches * float(s_rows) * a.dim * esz, rank_dt),
-               ("attention", attn_flops_img * a.batch, None, "fp32"))
+               ("attention", attn_flops_img * a.batch, attn_bytes, attn_dt))
     for name, fl_step, by_step, dt in entries:
         ms, n = cls[name]
         if n == 0 or ms <= 0:

@@ -294,6 +294,12 @@ int rr_attention_ex(rr_handle_t h, const float* qkv, int b, int seq, int heads,
  * (out_dtype 0) or bf16 (1).  Same contract as rr_attention_ex.             */
 int rr_attention_bf16(rr_handle_t h, const float* qkv, int b, int seq, int heads,
                       int head_dim, int out_dtype, void* out, void* stream);
+/* Same, with the QKV rows already in bf16 (the QKV linear's bf16 output,
+ * rr_linear_bf16 out_bf16 = 1: rounded RNE as rr_attention_bf16 rounds them,
+ * so the result is bit-identical at half the bytes read).                  */
+int rr_attention_bf16_qkv16(rr_handle_t h, const void* qkv_bf16, int b, int seq,
+                            int heads, int head_dim, int out_dtype, void* out,
+                            void* stream);
 
 /* Row-wise L2 normalisation x / max(||x||_2, eps), in place allowed.
  * Replaces F.normalize (networks/RetrievalNet.py:343, models/gem_pooling.py:91,

@@ -61,6 +61,7 @@ SIGNATURES = {
     "rr_attention": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "rr_attention_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "rr_attention_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
+    "rr_attention_bf16_qkv16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "rr_layernorm_ex": (_i, [_vp, _vp, _ll, _i, _i, _vp, _vp, _f, _i, _vp, _vp]),
     "rr_linear_bf16": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _vp]),
     "rr_alpha_qe": (_i, [_vp, _vp, _i, _vp, _i, _vp, _vp, _i, _i, _f, _ll, _vp, _vp]),

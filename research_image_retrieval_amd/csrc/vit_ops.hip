@@ -232,8 +232,22 @@ __global__ __launch_bounds__(64 * NC) void attention_kernel(const float* __restr
 // bank 2d, so a lane group's ds_read_b64 of 32 d-rows is conflict-free) and
 // read at exactly those keys.  K rows are 128 B with 16-B slots swizzled by
 // (row >> 1) & 7 (conflict-free fragment reads, as the GEMM core).
-template <int NC, typename OutT>
-__global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const float* __restrict__ qkv, int B, int L, int NH,
+// QKV rows come as fp32 (converted here, RNE) or already bf16 (InT = __bf16:
+// the QKV linear's epilogue rounded them the same way, so the result is
+// bit-identical and the kernel reads half the bytes)
+template <typename InT>
+__device__ __forceinline__ f32x4 ld4f(const InT* p) {
+  if constexpr (sizeof(InT) == 4) {
+    return *reinterpret_cast<const f32x4*>(p);
+  } else {
+    typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+    const bf16x4 v = *reinterpret_cast<const bf16x4*>(p);
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  }
+}
+
+template <int NC, typename OutT, typename InT>
+__global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const InT* __restrict__ qkv, int B, int L, int NH,
                                                                  OutT* __restrict__ out) {
   constexpr int HD = 64, LP = NC * 32, VS = 260;
   extern __shared__ __attribute__((aligned(16))) uint16_t sm16[];
@@ -243,14 +257,14 @@ __global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const float* __
   const int b = bh / NH, h = bh - (bh / NH) * NH;
   const int width = NH * HD;
   const long long ld = 3LL * width;
-  const float* base = qkv + (long long)b * L * ld;
+  const InT* base = qkv + (long long)b * L * ld;
   const int tid = threadIdx.x;
   for (int idx = tid; idx < LP * (HD / 4); idx += 64 * NC) {
     const int row = idx / (HD / 4), s4 = idx - row * (HD / 4);
     f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
     if (row < L) {
-      kv = *reinterpret_cast<const f32x4*>(base + (long long)row * ld + width + h * HD + s4 * 4);
-      vv = *reinterpret_cast<const f32x4*>(base + (long long)row * ld + 2 * width + h * HD + s4 * 4);
+      kv = ld4f(base + (long long)row * ld + width + h * HD + s4 * 4);
+      vv = ld4f(base + (long long)row * ld + 2 * width + h * HD + s4 * 4);
     }
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
     const bf16x4 kb = {(__bf16)kv[0], (__bf16)kv[1], (__bf16)kv[2], (__bf16)kv[3]};
@@ -269,11 +283,11 @@ __global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const float* __
   {
     const int q = q0 + lr;
     const bool ok = q < L;
-    const float* qp = base + (long long)(ok ? q : 0) * ld + h * HD;
+    const InT* qp = base + (long long)(ok ? q : 0) * ld + h * HD;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(qp + 16 * c + 8 * lh);
-      const f32x4 bq = *reinterpret_cast<const f32x4*>(qp + 16 * c + 8 * lh + 4);
+      const f32x4 a = ld4f(qp + 16 * c + 8 * lh);
+      const f32x4 bq = ld4f(qp + 16 * c + 8 * lh + 4);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         qf[c][e] = (__bf16)(ok ? a[e] * 0.125f : 0.f);
@@ -355,21 +369,21 @@ __global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const float* __
   }
 }
 
-template <int NC, typename OutT>
-static hipError_t launch_attn_bf16(const float* qkv, int B, int L, int NH, OutT* out, hipStream_t s) {
+template <int NC, typename OutT, typename InT>
+static hipError_t launch_attn_bf16(const InT* qkv, int B, int L, int NH, OutT* out, hipStream_t s) {
   const size_t lds = ((size_t)NC * 32 * 64 + 64 * 260) * 2;
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)attention_bf16_kernel<NC, OutT>,
+    hipError_t e = hipFuncSetAttribute((const void*)attention_bf16_kernel<NC, OutT, InT>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
-  hipLaunchKernelGGL((attention_bf16_kernel<NC, OutT>), dim3((unsigned)(B * NH)), dim3(64 * NC), lds, s, qkv, B, L,
-                     NH, out);
+  hipLaunchKernelGGL((attention_bf16_kernel<NC, OutT, InT>), dim3((unsigned)(B * NH)), dim3(64 * NC), lds, s, qkv, B,
+                     L, NH, out);
   return hipGetLastError();
 }
 
-template <typename OutT>
-static hipError_t launch_attn_bf16_nc(int nc, const float* qkv, int b, int seq, int heads, OutT* out,
+template <typename OutT, typename InT>
+static hipError_t launch_attn_bf16_nc(int nc, const InT* qkv, int b, int seq, int heads, OutT* out,
                                       hipStream_t s) {
   switch (nc) {
     case 1: return launch_attn_bf16<1>(qkv, b, seq, heads, out, s);
@@ -503,17 +517,36 @@ extern "C" int rr_attention_ex(rr_handle_t h, const float* qkv, int b, int seq, 
   return check_hip(h, e, "attention launch");
 }
 
-extern "C" int rr_attention_bf16(rr_handle_t h, const float* qkv, int b, int seq, int heads, int head_dim,
-                                 int out_dtype, void* out, void* stream) {
+static int attention_bf16_any(rr_handle_t h, const void* qkv, int qkv_bf16, int b, int seq, int heads, int head_dim,
+                              int out_dtype, void* out, void* stream, const char* what) {
   if (!h) return RR_EINVAL;
   if (!qkv || !out || b < 0 || heads <= 0 || head_dim != 64 || seq <= 0 || seq > 256 ||
       (out_dtype != 0 && out_dtype != 1))
-    return set_error(h, RR_EINVAL, "rr_attention_bf16: supports head_dim == 64, 1 <= seq <= 256, out_dtype 0|1");
+    return set_error(h, RR_EINVAL, std::string(what) + ": supports head_dim == 64, 1 <= seq <= 256, out_dtype 0|1");
   if (b == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeAttn, s);
   const int nc = (seq + 31) / 32;
-  const hipError_t e = out_dtype == 1 ? launch_attn_bf16_nc<__bf16>(nc, qkv, b, seq, heads, (__bf16*)out, s)
-                                      : launch_attn_bf16_nc<float>(nc, qkv, b, seq, heads, (float*)out, s);
+  hipError_t e;
+  if (qkv_bf16) {
+    const __bf16* q = (const __bf16*)qkv;
+    e = out_dtype == 1 ? launch_attn_bf16_nc(nc, q, b, seq, heads, (__bf16*)out, s)
+                       : launch_attn_bf16_nc(nc, q, b, seq, heads, (float*)out, s);
+  } else {
+    const float* q = (const float*)qkv;
+    e = out_dtype == 1 ? launch_attn_bf16_nc(nc, q, b, seq, heads, (__bf16*)out, s)
+                       : launch_attn_bf16_nc(nc, q, b, seq, heads, (float*)out, s);
+  }
   return check_hip(h, e, "attention_bf16 launch");
+}
+
+extern "C" int rr_attention_bf16(rr_handle_t h, const float* qkv, int b, int seq, int heads, int head_dim,
+                                 int out_dtype, void* out, void* stream) {
+  return attention_bf16_any(h, qkv, 0, b, seq, heads, head_dim, out_dtype, out, stream, "rr_attention_bf16");
+}
+
+extern "C" int rr_attention_bf16_qkv16(rr_handle_t h, const void* qkv_bf16, int b, int seq, int heads, int head_dim,
+                                       int out_dtype, void* out, void* stream) {
+  return attention_bf16_any(h, qkv_bf16, 1, b, seq, heads, head_dim, out_dtype, out, stream,
+                            "rr_attention_bf16_qkv16");
 }

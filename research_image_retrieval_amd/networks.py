@@ -282,7 +282,8 @@ class VisionTransformer(_Extractor):
         x = ops.layernorm(x, *self.ln_pre)
         for blk in self.blocks:
             y = ops.layernorm_bf16(x, blk["ln_1.weight"], blk["ln_1.bias"])
-            qkv = ops.linear_bf16(y, blk["attn.in_proj_weight.bf16"], blk["attn.in_proj_bias"])
+            # QKV rows in bf16 (RNE, exactly as the attention rounds fp32 rows): half the bytes
+            qkv = ops.linear_bf16(y, blk["attn.in_proj_weight.bf16"], blk["attn.in_proj_bias"], out_bf16=True)
             a = ops.attention_bf16(qkv, b, self.seq, self.heads)
             x = ops.linear_bf16(a, blk["attn.out_proj.weight.bf16"], blk["attn.out_proj.bias"], residual=x)
             y = ops.layernorm_bf16(x, blk["ln_2.weight"], blk["ln_2.bias"])

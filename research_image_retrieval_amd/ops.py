@@ -418,12 +418,18 @@ def layernorm_bf16(x, gamma, beta, eps=1e-5):
 
 def attention_bf16(qkv, b, seq, heads, head_dim=64, bf16_math=True):
     """Attention core for the bf16 ViT: bf16 output; bf16 MFMA with fp32
-    softmax (rr_attention_bf16), or fp32 MFMA (bf16_math=False)."""
-    _f32(qkv, "attention_bf16")
+    softmax (rr_attention_bf16; bf16 qkv rows: rr_attention_bf16_qkv16), or
+    fp32 MFMA (bf16_math=False, fp32 qkv)."""
     dev = _dev(qkv)
+    if qkv.dtype == torch.bfloat16 and bf16_math:
+        if not qkv.is_contiguous():
+            raise ValueError("attention_bf16: qkv must be contiguous")
+        fn = _lib.lib().rr_attention_bf16_qkv16
+    else:
+        _f32(qkv, "attention_bf16")
+        fn = _lib.lib().rr_attention_bf16 if bf16_math else _lib.lib().rr_attention_ex
     out = torch.empty((b * seq, heads * head_dim), dtype=torch.bfloat16, device=qkv.device)
     hd = _lib.handle(dev)
-    fn = _lib.lib().rr_attention_bf16 if bf16_math else _lib.lib().rr_attention_ex
     _lib.check(fn(hd, _ptr(qkv), b, seq, heads, head_dim, 1, _ptr(out), _stream(dev)), hd, "rr_attention_bf16")
     return out
 

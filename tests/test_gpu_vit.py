@@ -82,3 +82,22 @@ def test_attention_bf16_kernel_vs_float64(cuda, seq):
     print(f"seq {seq}: bf16-math max|err| {err:.3g} min cos {cos.min().item():.6f}; "
           f"fp32-math max|err| {(out32 - ref).abs().max().item():.3g}")
     assert cos.min().item() >= 0.9999 and err <= 1e-2
+    # bf16 QKV rows (the QKV linear's bf16 output): bit-identical to the fp32-input kernel
+    out16 = ops.attention_bf16(qkv.bfloat16().to(cuda), b, seq, heads).float().cpu().double()
+    assert torch.equal(out16, out)
+
+
+def test_vit_bf16_linear_bf16_qkv_matches_fp32_qkv(cuda):
+    """rr_linear_bf16 with bf16 output rounds (acc + bias) RNE, exactly as the
+    attention rounds fp32 QKV rows: the fused bf16 path equals the fp32 one."""
+    g = torch.Generator().manual_seed(5)
+    m, k, n = 2 * 197, 768, 3 * 768
+    x = torch.randn(m, k, generator=g).bfloat16().to(cuda)
+    w = (torch.randn(n, k, generator=g) / k ** 0.5).bfloat16().to(cuda)
+    bias = torch.randn(n, generator=g).to(cuda)
+    q32 = ops.linear_bf16(x, w, bias)
+    q16 = ops.linear_bf16(x, w, bias, out_bf16=True)
+    assert torch.equal(q32.bfloat16(), q16)
+    a32 = ops.attention_bf16(q32, 2, 197, 12)
+    a16 = ops.attention_bf16(q16, 2, 197, 12)
+    assert torch.equal(a32, a16)
