@@ -202,8 +202,10 @@ int rr_resize_bilinear(rr_handle_t h, const float* x, int b, int hgt, int wid,
  * as three bf16 planes w3 [3][cout][kh][kw][cin] from rr_split3_bf16 and the
  * activations split in-kernel (x = x0 + x1 + x2 exactly; six bf16 MFMA
  * products per fp32 product, error vs float64 at or below the exact-fp32
- * MFMA's).  Needs cin % 32 == 0.  Replaces the same reference ops as
- * rr_conv2d (networks/backbone.py:103-109, models/gem_pooling.py:44,61).   */
+ * MFMA's).  Needs cin % 32 == 0, or cin == 4 for the NHWC4 stem (RGB + a
+ * zero channel): then w3 is [3][cout][Kp], the flattened [kh][kw][4] filter
+ * zero-padded to Kp = kh*kw*4 rounded up to 32.  Replaces the same reference
+ * ops as rr_conv2d (networks/backbone.py:103-109, models/gem_pooling.py:44,61). */
 int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid,
                  int cin, const void* w3, const float* bias, int cout, int kh,
                  int kw, int stride, int pad, const float* residual, int relu,

@@ -82,6 +82,19 @@ __device__ __forceinline__ void s3_load2(const f32x4* p, f32x4 (&r)[2]) {
     r[1] = p[1];
   }
 }
+// two 16-B loads from unrelated addresses (the NHWC4 stem's two taps)
+template <int ASYNC>
+__device__ __forceinline__ void s3_load1x2(const f32x4* p0, const f32x4* p1, f32x4 (&r)[2]) {
+  if constexpr (ASYNC) {
+    asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %3, off"
+                 : "=&v"(r[0]), "=&v"(r[1])
+                 : "v"(p0), "v"(p1)
+                 : "memory");
+  } else {
+    r[0] = *p0;
+    r[1] = *p1;
+  }
+}
 // a fresh definition of v after the preceding (volatile) wait: nothing that
 // reads v can be scheduled above it
 __device__ __forceinline__ void s3_launder(f32x4& v) { asm volatile("" : "+v"(v)); }
@@ -136,7 +149,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       a_iw0[i] = ow * g.stride - g.pad;
       // the (possibly padded, out-of-image) top-left tap pixel; a k-tile adds a
       // block-uniform offset (kh*W + kw)*Cin + cin0
-      a_ptr[i] = g.A + (((long long)b * g.H + a_ih0[i]) * g.W + a_iw0[i]) * g.Cin + a_slot * 8;
+      a_ptr[i] = g.A + (((long long)b * g.H + a_ih0[i]) * g.W + a_iw0[i]) * g.Cin + (AMODE == A_CONV ? a_slot * 8 : 0);
     }
   }
   f32x4 ra2[2][A_CH][2];
@@ -153,6 +166,28 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         const f32x4* p = a_ok[i] ? reinterpret_cast<const f32x4*>(a_ptr[i] + k0) : s3_zero_page();
         s3_load2<PIPE>(p, ra[i]);
       }
+    } else if constexpr (AMODE == A_CONV_C4) {
+      // NHWC4 stem (RGB + a zero channel): a k-tile is 8 filter taps of 4
+      // channels, a thread's 8-k chunk the taps 8kt + 2 slot + {0, 1}, one
+      // 16-B load each; taps past KH*KW (K padded to a multiple of 32) and
+      // padding pixels read the zero page
+      const int tb = kt * 8, khb = tb / g.KW, kwb = tb - khb * g.KW;
+      const f32x4* p[A_CH][2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        int kh = khb, kw = kwb + 2 * a_slot + e;
+        while (kw >= g.KW) kw -= g.KW, ++kh;
+        const bool tap_ok = kh < g.KH;
+        const long long toff = (long long)(kh * g.W + kw) * 4;
+#pragma unroll
+        for (int i = 0; i < A_CH; ++i) {
+          const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
+          const bool ok = tap_ok && a_ok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+          p[i][e] = ok ? reinterpret_cast<const f32x4*>(a_ptr[i] + toff) : s3_zero_page();
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) s3_load1x2<PIPE>(p[i][0], p[i][1], ra[i]);
     } else {
       // Cin % 32 == 0: the whole k-tile lies in one (kh, kw) filter tap
       const int khw = k0 / g.Cin, cin0 = k0 - khw * g.Cin;
@@ -493,14 +528,19 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
   if (amode == A_DENSE && ((g.lda & 3) || ((uintptr_t)g.A & 15)))
     return set_error(h, RR_EINVAL, "gemm_s3: dense A needs lda % 4 == 0 and 16-B alignment");
   if (amode == A_CONV && (g.Cin % 32)) return set_error(h, RR_EINVAL, "gemm_s3: conv A needs Cin % 32 == 0");
-  if (amode != A_DENSE && amode != A_CONV) return set_error(h, RR_EINVAL, "gemm_s3: unsupported A mode");
+  if (amode == A_CONV_C4 && (g.Cin != 4 || g.K < g.KH * g.KW * 4 || ((uintptr_t)g.A & 15)))
+    return set_error(h, RR_EINVAL, "gemm_s3: NHWC4 A needs Cin == 4, K >= KH*KW*4, 16-B alignment");
+  if (amode != A_DENSE && amode != A_CONV && amode != A_CONV_C4)
+    return set_error(h, RR_EINVAL, "gemm_s3: unsupported A mode");
   if ((g.ldb & 7) || (g.b_plane & 7) || ((uintptr_t)g.B & 15))
     return set_error(h, RR_EINVAL, "gemm_s3: B planes need ldb % 8 == 0, plane stride % 8 == 0, 16-B alignment");
   if (g.M == 0) return RR_OK;
   hipError_t e;
   {
     TimedLaunch tl(h, timer_cls, s);
-    e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s) : launch_s3_am<A_CONV>(g, s);
+    e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s)
+        : amode == A_CONV ? launch_s3_am<A_CONV>(g, s)
+                          : launch_s3_am<A_CONV_C4>(g, s);
   }
   return check_hip(h, e, "gemm_s3 launch");
 }

@@ -337,7 +337,7 @@ int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin
   if (!x || !w3 || !y || b < 0 || hgt <= 0 || wid <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 ||
       stride <= 0 || pad < 0 || relu < 0 || relu > 1)
     return set_error(h, RR_EINVAL, "rr_conv2d_s3: bad argument");
-  if (cin % 32) return set_error(h, RR_EINVAL, "rr_conv2d_s3: cin must be a multiple of 32");
+  if (cin % 32 && cin != 4) return set_error(h, RR_EINVAL, "rr_conv2d_s3: cin must be a multiple of 32, or 4 (NHWC4 stem)");
   const int oh = (hgt + 2 * pad - kh) / stride + 1, ow = (wid + 2 * pad - kw) / stride + 1;
   if (oh <= 0 || ow <= 0) return set_error(h, RR_EINVAL, "rr_conv2d_s3: empty output");
   const long long M = (long long)b * oh * ow;
@@ -356,6 +356,8 @@ int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin
   g.KW = kw;
   g.stride = stride;
   g.pad = pad;
+  // NHWC4 stem: the weight planes hold K = KH*KW*4 padded with zeros to a multiple of 32
+  if (cin == 4) g.K = (g.K + 31) / 32 * 32;
   g.B = reinterpret_cast<const float*>(w3);
   g.ldb = g.K;
   g.b_plane = (long long)cout * g.K;
@@ -365,9 +367,9 @@ int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin
   g.bias = bias;
   g.residual = residual;
   g.relu = relu;
-  const bool dense = kh == 1 && kw == 1 && stride == 1 && pad == 0;
+  const bool dense = kh == 1 && kw == 1 && stride == 1 && pad == 0 && cin != 4;
   if (dense) g.lda = cin;
-  return launch_gemm_s3(h, dense ? A_DENSE : A_CONV, g, (hipStream_t)stream, kTimeGemm);
+  return launch_gemm_s3(h, dense ? A_DENSE : (cin == 4 ? A_CONV_C4 : A_CONV), g, (hipStream_t)stream, kTimeGemm);
 }
 
 int rr_linear_s3(rr_handle_t h, const float* x, int m, int k, const void* w3, const float* bias, int n,

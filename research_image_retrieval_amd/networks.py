@@ -24,7 +24,8 @@ class ResNet:
 
     conv_math: "s3" (default) runs every conv with Cin % 32 == 0 on the
     split-bf16 core (fp32-accurate, weights split once here); "f32" keeps all
-    convs on the exact-fp32 MFMA core.  The stem (Cin = 3) is always fp32."""
+    convs on the exact-fp32 MFMA core.  The stem runs on the split-bf16 core
+    too (NHWC4 taps, K padded to 224) unless conv_math == "f32"."""
 
     outputdim_block5 = 2048
     outputdim_block4 = 1024
@@ -45,11 +46,15 @@ class ResNet:
         self.layers = W.RESNET_LAYERS[name]
         self.conv_math = conv_math
         self.convs_s3 = {}
+        self.stem_s3 = None
         if conv_math == "s3":
             self.convs_s3 = {k: ops.split3_bf16(w) for k, (w, _) in self.convs.items() if w.shape[-1] % 32 == 0}
+            self.stem_s3 = ops.split3_stem(self.convs["conv1"][0])
 
     def _conv(self, x, name, stride, pad, relu, residual=None):
         w, b = self.convs[name]
+        if name == "conv1" and self.stem_s3 is not None:
+            return ops.conv2d_s3_stem(x, self.stem_s3[0], self.stem_s3[1], b, stride, pad, relu)
         w3 = self.convs_s3.get(name)
         if w3 is not None:
             return ops.conv2d_s3(x, w3, b, stride, pad, residual, relu)

@@ -100,6 +100,42 @@ def split3_bf16(x):
     return planes
 
 
+def split3_stem(w):
+    """Weight planes of an NHWC4 stem conv for conv2d_s3: w [Cout,KH,KW,4]
+    flattened to [Cout, KH*KW*4], zero-padded to a multiple of 32, split
+    (int16 [3, Cout, Kp]); the kernel shape travels in stem_shape."""
+    w = _f32(w.contiguous(), "split3_stem")
+    cout, kh, kw, c = w.shape
+    if c != 4:
+        raise ValueError("split3_stem: NHWC4 filters (4 input channels)")
+    k = kh * kw * 4
+    kp = (k + 31) // 32 * 32
+    flat = torch.nn.functional.pad(w.reshape(cout, k), (0, kp - k)).contiguous()
+    return split3_bf16(flat), (kh, kw)
+
+
+def conv2d_s3_stem(x, w3p, stem_shape, bias, stride, pad, relu=True):
+    """The NHWC4 stem conv on the split-bf16 core (rr_conv2d_s3, cin == 4)."""
+    _f32(x, "conv2d_s3_stem x")
+    if x.shape[-1] != 4:
+        raise ValueError("conv2d_s3_stem: x must be NHWC4")
+    kh, kw = stem_shape
+    cout, kp = w3p.shape[1], w3p.shape[2]
+    if w3p.dtype != torch.int16 or w3p.shape[0] != 3 or kp != (kh * kw * 4 + 31) // 32 * 32 or not w3p.is_contiguous():
+        raise ValueError("conv2d_s3_stem: w3p must be split3_stem planes")
+    dev = _dev(x)
+    b, h, wd, _ = x.shape
+    oh = (h + 2 * pad - kh) // stride + 1
+    ow = (wd + 2 * pad - kw) // stride + 1
+    y = torch.empty((b, oh, ow, cout), dtype=torch.float32, device=x.device)
+    if bias is not None:
+        _f32(bias, "conv2d_s3_stem bias")
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_conv2d_s3(hd, _ptr(x), b, h, wd, 4, _ptr(w3p), _ptr(bias), cout, kh, kw, stride, pad,
+                                       None, int(relu), _ptr(y), _stream(dev)), hd, "rr_conv2d_s3 (stem)")
+    return y
+
+
 def conv2d_s3(x, w3, bias, stride=1, pad=0, residual=None, relu=False):
     """conv2d on the split-bf16 core: fp32-accurate, w3 = split3_bf16(w) with
     w [Cout,KH,KW,Cin], Cin % 32 == 0."""

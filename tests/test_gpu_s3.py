@@ -107,6 +107,31 @@ def test_conv2d_s3_vs_float64(cuda, b, h, w, cin, cout, k, s, p, res):
     assert es3[0] <= max(ef32[0], 1e-7) and es3[1] <= ef32[1] * 1.05 + 1e-9
 
 
+@pytest.mark.parametrize("b,h,w", [(2, 224, 224), (3, 37, 53)])
+def test_stem_s3_vs_float64(cuda, b, h, w):
+    """The NHWC4 stem (7x7/2, pad 3, 3 channels + a zero channel, K padded to
+    224) on the split-bf16 core vs float64, next to the exact-fp32 core."""
+    g = torch.Generator().manual_seed(b * h + w)
+    x = torch.randn(b, h, w, 3, generator=g) * 1.5
+    x4 = F.pad(x, (0, 1)).contiguous()
+    wt = torch.randn(64, 7, 7, 3, generator=g) * (2.0 / 147) ** 0.5
+    w4 = F.pad(wt, (0, 1)).contiguous()
+    bias = torch.randn(64, generator=g) * 0.1
+    xn, wn = x.permute(0, 3, 1, 2).double(), wt.permute(0, 3, 1, 2).double()
+    ref = torch.relu(F.conv2d(xn, wn, None, 2, 3).permute(0, 2, 3, 1) + bias.double())
+    scale = F.conv2d(xn.abs(), wn.abs(), None, 2, 3).permute(0, 2, 3, 1)
+    w3p, shp = ops.split3_stem(w4.to(cuda))
+    y_s3 = ops.conv2d_s3_stem(x4.to(cuda), w3p, shp, bias.to(cuda), 2, 3, True).cpu()
+    y_f32 = ops.conv2d(x4.to(cuda), w4.to(cuda), bias.to(cuda), 2, 3, None, True).cpu()
+    assert y_s3.shape == ref.shape
+    live = ref > 0
+    es3 = _rel_err(y_s3[live], ref[live], scale[live])
+    ef32 = _rel_err(y_f32[live], ref[live], scale[live])
+    print(f"stem {b}x{h}x{w}: s3 max {es3[0]:.3g} mean {es3[1]:.3g} | f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
+    assert (y_s3 - torch.relu(ref).float()).abs().max().item() < 1e-4
+    assert es3[0] <= max(ef32[0], 1e-7) and es3[1] <= ef32[1] * 1.05 + 1e-9
+
+
 def test_resnet_s3_descriptors_vs_float64(cuda):
     """The whole R50-GeM extractor: split-bf16 trunk vs exact-fp32 trunk, both
     against the oracle evaluated in float64."""
