@@ -376,7 +376,7 @@ def main():
                  "frac": round(ach / peak, 4)}
         if dt == "s3":
             e["math"] = ("fp32 via exact 3-way bf16 split: 6 bf16 MFMA products per fp32 product, fp32 accumulation; "
-                         "peak = bf16 dense peak / 6 (the stem conv, 1.5% of the FLOPs, runs on the exact-fp32 core)")
+                         "peak = bf16 dense peak / 6 (every conv incl. the stem; the whiten and PCA-w linears, 0.2% of the FLOPs, run on the exact-fp32 core)")
             e["mfma_flop_per_launch"] = 6.0 * fl_step / max(1.0, n / a.steps)
         e.update({"dtype": "fp32" if dt == "s3" else dt, "ms_per_step": round(ms / a.steps, 3),
                   "launches_per_step": n / a.steps,
