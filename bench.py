@@ -126,6 +126,11 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
             "value_with_topk": 1.0 / (t_embed + t_rank_topk), "cpu_model": model}
 
 
+def seed_rows(n, k):
+    """Rows of the rankers' threshold-seeding sample (librr seed_sample_rows)."""
+    return min(n, max(k, 4096, min(32768, n // 48)))
+
+
 def load_traffic():
     """Per-launch HBM bytes measured by rocprofv3 --pmc (profiles/traffic.json),
     corrected per MI355X_MICROARCH.md §HBM; None if not collected."""
@@ -315,7 +320,7 @@ def main():
         timer.collect(_lib.TIME_GEMM), timer.collect(_lib.TIME_SELECT), timer.collect(_lib.TIME_ELEM)
         timer.collect(_lib.TIME_COSINE_SEED)
         timer.enable(False)
-        s_rows_x = min(hi - lo, max(32768, a.k))
+        s_rows_x = seed_rows(hi - lo, a.k)
         fl = 2.0 * q_total * max(0, (hi - lo) - s_rows_x) * a.dim
         ach = fl / (f_ms / 1e3 / max(1, f_n)) / 1e12 if f_n else 0.0
         exhaustive = {"value": round(a.batch * a.steps / el_x, 2), "ms_per_step": round(el_x / a.steps * 1e3, 3),
@@ -326,7 +331,7 @@ def main():
                       "bit_identical_to_prefilter": True}
 
     # ---- roofline (algorithmic FLOPs / measured kernel time) ----
-    s_rows = min(hi - lo, max(32768, a.k))
+    s_rows = seed_rows(hi - lo, a.k)
     flop_filter = 2.0 * q_total * max(0, (hi - lo) - s_rows) * a.dim  # per filter launch (one per step)
     flop_seed = 2.0 * q_total * s_rows * a.dim
     attn_flops_img = 0

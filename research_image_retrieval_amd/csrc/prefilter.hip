@@ -18,7 +18,7 @@
 // eps(q) for all rows, computed in fp64 and rounded up.
 //
 // Passes (one query = one column of the GEMMs):
-//   1. bf16 scores of the first s = 32768 rows; their k-th best s'_seed;
+//   1. bf16 scores of the first s rows (seed_sample_rows: <= 32768); their k-th best s'_seed;
 //      T1 = s'_seed - 2 eps.  At least k rows have s >= s'_seed - eps, so the
 //      exact k-th best S_k >= s'_seed - eps and any row of the exact top-k
 //      has s' >= S_k - eps >= T1.
@@ -131,8 +131,7 @@ static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
 static PrefilterWs prefilter_layout(int nq, long long n, int d, int k) {
   PrefilterWs w{};
-  const long long smax = std::max<long long>(32768, k);
-  w.s = n <= smax ? n : smax;
+  w.s = seed_sample_rows(n, k);
   w.ld = (w.s + 3) & ~3LL;
   w.cap = std::max<long long>(n, k);  // worst case: every row passes pass 1
   size_t o = 0;

@@ -34,10 +34,7 @@ TimedLaunch::~TimedLaunch() {
 }
 
 // Sample size of the threshold-seeding pass of rr_cosine_topk.
-static long long seed_rows(long long n, int k) {
-  const long long smax = std::max<long long>(32768, k);
-  return n <= smax ? n : smax;
-}
+static long long seed_rows(long long n, int k) { return seed_sample_rows(n, k); }
 
 static inline size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 

@@ -79,6 +79,19 @@ __host__ __device__ inline float key_score(unsigned long long k) {
 }
 
 // ---- GEMM core launchers (gemm_f32.hip) ---------------------------------
+// Rows of the threshold-seeding sample of the cosine top-k rankers (exact
+// for any sample >= k rows).  About 2 % of the shard, capped at 32768 and
+// floored at 4096: on a row-sharded gallery the seed GEMM + select cost per
+// rank, nq x s with nq = all ranks' queries, then stays constant as the node
+// grows (the later passes already scale as nq x n / ranks).
+inline long long seed_sample_rows(long long n, int k) {
+  long long s = n / 48;
+  if (s > 32768) s = 32768;
+  if (s < 4096) s = 4096;
+  if (s < k) s = k;
+  return n < s ? n : s;
+}
+
 enum AMode { A_DENSE = 0, A_CONV = 1, A_CONV_GENERIC = 2, A_CONV_C4 = 3 };
 enum EMode { E_STORE = 0, E_SCORES_T = 1, E_FILTER = 2 };
 enum DType { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2 };
