@@ -57,6 +57,22 @@ def test_linear_s3_accuracy_vs_float64(cuda, m, k, n):
     assert es3[0] <= ef32[0] and es3[1] <= ef32[1]
 
 
+@pytest.mark.parametrize("m,k,n", [(77, 32, 130), (300, 64, 64), (129, 96, 257), (513, 160, 64), (33, 32, 64)])
+def test_linear_s3_kloop_edges(cuda, m, k, n):
+    """Edges of the async-A k-loop (1, 2, 3, 5 k-tiles; ragged M and N on both
+    tile configs, N = 64 -> 256x64 tiles): fp32-grade against float64 (error
+    relative to sum |a||b| below 4e-7; at these short K the final hi + lo
+    rounding dominates, so no ordering against the fp32 core is asserted)."""
+    g = torch.Generator().manual_seed(7 * m + k + n)
+    a = torch.relu(torch.randn(m, k, generator=g))
+    w = torch.randn(n, k, generator=g) / k ** 0.5
+    ref = a.double() @ w.double().t()
+    scale = a.double().abs() @ w.double().abs().t()
+    y = ops.linear_s3(a.to(cuda), ops.split3_bf16(w.to(cuda))).cpu()
+    e = _rel_err(y, ref, scale)
+    assert e[0] < 4e-7, e
+
+
 def test_linear_s3_epilogue(cuda):
     g = torch.Generator().manual_seed(5)
     m, k, n = 200, 512, 320
