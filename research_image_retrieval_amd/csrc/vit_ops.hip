@@ -247,7 +247,7 @@ __device__ __forceinline__ f32x4 ld4f(const InT* p) {
 }
 
 template <int NC, typename OutT, typename InT>
-__global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const InT* __restrict__ qkv, int B, int L, int NH,
+__global__ __launch_bounds__(64 * NC, 2) void attention_bf16_kernel(const InT* __restrict__ qkv, int B, int L, int NH,
                                                                  OutT* __restrict__ out) {
   constexpr int HD = 64, LP = NC * 32, VS = 260;
   extern __shared__ __attribute__((aligned(16))) uint16_t sm16[];
@@ -296,53 +296,59 @@ __global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const InT* __re
     }
   }
   __syncthreads();
-  f32x16 st[NC];
+  // Two passes over the key chunks, one 32x32 score tile live at a time (the
+  // one-pass form held all NC tiles: 222 VGPRs, one workgroup per CU; now two
+  // fit, so one workgroup's K/V staging overlaps the other's MFMAs).  Pass 1:
+  // the row max; pass 2: the same scores again (deterministic), p = exp(s -
+  // max) summed in the one-pass order, P packed to bf16, O += P V.  Output
+  // bit-identical to the one-pass kernel.
+  auto s_chunk = [&](int kc) {
+    f32x16 st;
 #pragma unroll
-  for (int kc = 0; kc < NC; ++kc) {
-#pragma unroll
-    for (int r = 0; r < 16; ++r) st[kc][r] = 0.f;
+    for (int r = 0; r < 16; ++r) st[r] = 0.f;
     const int krow = kc * 32 + lr;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const bf16x8 kf =
           *reinterpret_cast<const bf16x8*>(Ks + krow * HD + (((2 * c + lh) ^ ((krow >> 1) & 7)) * 8));
-      st[kc] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[c], st[kc], 0, 0, 0);
+      st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[c], st, 0, 0, 0);
     }
-  }
-  float mx = -__builtin_inff();
-#pragma unroll
-  for (int kc = 0; kc < NC; ++kc)
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int key = kc * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
-      if (key >= L) st[kc][r] = -__builtin_inff();
-      mx = fmaxf(mx, st[kc][r]);
+      if (key >= L) st[r] = -__builtin_inff();
     }
+    return st;
+  };
+  float mx = -__builtin_inff();
+#pragma unroll 1
+  for (int kc = 0; kc < NC; ++kc) {
+    const f32x16 st = s_chunk(kc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) mx = fmaxf(mx, st[r]);
+  }
   mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
   float sum = 0.f;
-#pragma unroll
-  for (int kc = 0; kc < NC; ++kc)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float p = expf(st[kc][r] - mx);
-      st[kc][r] = p;
-      sum += p;
-    }
-  sum += __shfl_xor(sum, 32, 64);
-  const float inv = 1.0f / sum;
   f32x16 o[2];
 #pragma unroll
   for (int t = 0; t < 2; ++t)
 #pragma unroll
     for (int r = 0; r < 16; ++r) o[t][r] = 0.f;
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-#pragma unroll
+#pragma unroll 1
   for (int kc = 0; kc < NC; ++kc) {
+    f32x16 st = s_chunk(kc);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float p = expf(st[r] - mx);
+      st[r] = p;
+      sum += p;
+    }
 #pragma unroll
     for (int s2 = 0; s2 < 2; ++s2) {
       bf16x8 pf;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) pf[e] = (__bf16)st[kc][8 * s2 + e];
+      for (int e = 0; e < 8; ++e) pf[e] = (__bf16)st[8 * s2 + e];
       const int k0 = kc * 32 + 16 * s2 + 4 * lh;
 #pragma unroll
       for (int t = 0; t < 2; ++t) {
@@ -356,6 +362,8 @@ __global__ __launch_bounds__(64 * NC) void attention_bf16_kernel(const InT* __re
       }
     }
   }
+  sum += __shfl_xor(sum, 32, 64);
+  const float inv = 1.0f / sum;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
     const int qi = (r & 3) + 8 * (r >> 2) + 4 * lh;
