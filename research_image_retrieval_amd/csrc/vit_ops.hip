@@ -52,6 +52,58 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
   }
 }
 
+// Same, vectorised for D % 256 == 0 and 16-B aligned rows (ViT width 768):
+// lane l holds the float4s at columns 4l + 256i, so every load and store is
+// one 1-KB (fp32) or 512-B (bf16) coalesced wave instruction.
+template <int NV, typename OutT>
+__global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restrict__ x, long long ldx, int M,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float eps,
+                                                            OutT* __restrict__ y) {
+  constexpr int D = 256 * NV;
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (long long)row * ldx;
+  f32x4 v[NV];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    v[i] = *reinterpret_cast<const f32x4*>(xr + 4 * lane + 256 * i);
+    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  const float mean = s / (float)D;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float d = v[i][e] - mean;
+      q = fmaf(d, d, q);
+    }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
+  const float rstd = 1.0f / sqrtf(q / (float)D + eps);
+  OutT* yr = y + (long long)row * D;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * lane + 256 * i;
+    const f32x4 gm = *reinterpret_cast<const f32x4*>(gamma + c);
+    const f32x4 bt = *reinterpret_cast<const f32x4*>(beta + c);
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (v[i][e] - mean) * rstd * gm[e] + bt[e];
+    if constexpr (sizeof(OutT) == 4) {
+      *reinterpret_cast<f32x4*>(yr + c) = o;
+    } else {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<bf16x4*>(yr + c) = bf16x4{(__bf16)o[0], (__bf16)o[1], (__bf16)o[2], (__bf16)o[3]};
+    }
+  }
+}
+
 // NHWC [B][H][W][C] -> patch rows [B*(H/P)*(W/P)][P*P*C] in (kh, kw, c) order,
 // which matches conv weights permuted to [Cout][P][P][C].
 __global__ void patchify_kernel(const float* __restrict__ x, int B, int H, int W, int C, int P,
@@ -442,6 +494,15 @@ static hipError_t launch_attn_nc(int nc, const float* qkv, int b, int seq, int h
 template <typename OutT>
 static void launch_ln(int per, dim3 grid, hipStream_t s, const float* x, long long ldx, int m, int d,
                       const float* gamma, const float* beta, float eps, OutT* y) {
+  const bool vec = (ldx & 3) == 0 && (((uintptr_t)x | (uintptr_t)gamma | (uintptr_t)beta | (uintptr_t)y) & 15) == 0;
+  if (vec && d == 768) {
+    hipLaunchKernelGGL((layernorm_vec_kernel<3, OutT>), grid, dim3(256), 0, s, x, ldx, m, gamma, beta, eps, y);
+    return;
+  }
+  if (vec && d == 512) {
+    hipLaunchKernelGGL((layernorm_vec_kernel<2, OutT>), grid, dim3(256), 0, s, x, ldx, m, gamma, beta, eps, y);
+    return;
+  }
   if (per <= 4)
     hipLaunchKernelGGL((layernorm_kernel<4, OutT>), grid, dim3(256), 0, s, x, ldx, m, d, gamma, beta, eps, y);
   else if (per <= 12)
