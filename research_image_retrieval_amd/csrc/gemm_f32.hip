@@ -352,6 +352,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
         }
       };
       rd(0, af[0], bf[0]);
+      // MFMA cluster at raised priority (cdna_hip_programming.md T5; measured
+      // +2 % on the ViT linears and the bf16 sweep)
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int st = 0; st < S; ++st) {
         if (st + 1 < S) rd(st + 1, af[(st + 1) & 1], bf[(st + 1) & 1]);
@@ -362,6 +365,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[st & 1][i], bf[st & 1][j], acc[i][j], 0, 0, 0);
         if (st + 1 < S) interleave<FM + FN, FM * FN>();
       }
+      __builtin_amdgcn_s_setprio(0);
     } else {
       // fp8: BK/4 k-steps of 16; lane half h holds bytes 8h..8h+7 of 16-B slot s
       constexpr int S = BK / 4;
@@ -379,6 +383,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
         }
       };
       rd(0, af[0], bf[0]);
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int st = 0; st < S; ++st) {
         if (st + 1 < S) rd(st + 1, af[(st + 1) & 1], bf[(st + 1) & 1]);
@@ -389,6 +394,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(af[st & 1][i], bf[st & 1][j], acc[i][j], 0, 0, 0);
         if (st + 1 < S) interleave<FM + FN, FM * FN>();
       }
+      __builtin_amdgcn_s_setprio(0);
     }
     if constexpr (GL != 2) {
       if constexpr (!GL) {
