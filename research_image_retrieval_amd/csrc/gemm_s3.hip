@@ -152,6 +152,26 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       a_ptr[i] = g.A + (((long long)b * g.H + a_ih0[i]) * g.W + a_iw0[i]) * g.Cin + (AMODE == A_CONV ? a_slot * 8 : 0);
     }
   }
+  // conv tap of the k-tile the A loader is at, advanced incrementally (the
+  // loader requests k-tiles in non-decreasing order, one step at a time):
+  // no per-tile integer divisions
+  int tp_kt = 0, tp_kh = 0, tp_kw = 0, tp_cin = 0;
+  long long tp_off = 0;  // (kh * W + kw) * Cin + cin0
+  auto tap_to = [&](int kt) {
+    while (tp_kt < kt) {
+      ++tp_kt;
+      tp_off += BK;
+      tp_cin += BK;
+      if (tp_cin == g.Cin) {
+        tp_cin = 0;
+        if (++tp_kw == g.KW) {
+          tp_kw = 0;
+          ++tp_kh;
+          tp_off += (long long)(g.W - g.KW) * g.Cin;
+        }
+      }
+    }
+  };
   f32x4 ra2[2][A_CH][2];
   auto load_a = [&](int kt, int rb) {
     f32x4(&ra)[A_CH][2] = ra2[rb];
@@ -190,9 +210,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       for (int i = 0; i < A_CH; ++i) s3_load1x2<PIPE>(p[i][0], p[i][1], ra[i]);
     } else {
       // Cin % 32 == 0: the whole k-tile lies in one (kh, kw) filter tap
-      const int khw = k0 / g.Cin, cin0 = k0 - khw * g.Cin;
-      const int kh = khw / g.KW, kw = khw - kh * g.KW;
-      const long long toff = (long long)(kh * g.W + kw) * g.Cin + cin0;
+      tap_to(kt);
+      const int kh = tp_kh, kw = tp_kw;
+      const long long toff = tp_off;
 #pragma unroll
       for (int i = 0; i < A_CH; ++i) {
         const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
