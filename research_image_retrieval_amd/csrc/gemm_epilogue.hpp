@@ -10,6 +10,8 @@ namespace rr {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x8 __attribute__((ext_vector_type(8)));
 
 // QuickGELU, x * sigmoid(1.702 x) (networks/model.py:166-168)
 __device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f + expf(-(1.702f * x)))); }

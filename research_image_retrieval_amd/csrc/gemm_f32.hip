@@ -34,7 +34,8 @@
 namespace rr {
 
 // input element type of A/B: DT_F32 (v_mfma_f32_32x32x2_f32), DT_BF16
-// (v_mfma_f32_32x32x16_bf16), DT_FP8 (OCP e4m3, v_mfma_f32_32x32x16_fp8_fp8).
+// (v_mfma_f32_32x32x16_bf16), DT_FP8 (OCP e4m3, v_mfma_scale_f32_32x32x64_f8f6f4
+// with unit block scales).
 // LDS rows are 128 B for all three (32 fp32 / 64 bf16 / 128 fp8 per k-tile),
 // so staging, swizzle and epilogues are shared.
 template <int DT> struct ElemT { using T = float; };
@@ -62,6 +63,19 @@ __device__ __forceinline__ void interleave() {
     __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // 1 DS read
   }
   if constexpr (NM > NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
+}
+
+// Same with two DS reads per MFMA (NP pairs, NM >= NP MFMAs): the fp8 k-step
+// reads 32 bytes (two ds_read_b128) per fragment.
+template <int NP, int NM>
+__device__ __forceinline__ void interleave2() {
+  static_assert(NM >= NP, "interleave2: fewer MFMAs than read pairs");
+#pragma unroll
+  for (int x = 0; x < NP; ++x) {
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+    __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);  // 2 DS reads
+  }
+  if constexpr (NM > NP) __builtin_amdgcn_sched_group_barrier(0x008, NM - NP, 0);
 }
 
 // BK = 32: 64 KB LDS per 128x128 block, 2 blocks (2 waves/SIMD) per CU.
@@ -367,20 +381,24 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
       }
       __builtin_amdgcn_s_setprio(0);
     } else {
-      // fp8: BK/4 k-steps of 16; lane half h holds bytes 8h..8h+7 of 16-B slot s
-      constexpr int S = BK / 4;
-      long af[2][FM], bf[2][FN];
-      auto rd = [&](int st, long* a, long* b) {
+      // fp8 on the block-scaled v_mfma_scale_f32_32x32x64_f8f6f4 (e4m3 both
+      // operands, every E8M0 block scale = 127 = 1.0; the per-row fp32 scales
+      // stay in the epilogue): 2x the k per clock of the non-scaled
+      // 32x32x16_fp8 form.  BK/16 k-steps of 64; lane half h holds the 32
+      // bytes of 16-B slots 4s+2h, 4s+2h+1.  A and B fragments are read by
+      // the same lane->k map, so each dot product covers every k once.
+      constexpr int S = BK / 16;
+      i32x8 af[2][FM], bf[2][FN];
+      auto rd32 = [&](const float* base, int row, int st) {
+        const i32x4 lo = *reinterpret_cast<const i32x4*>(base + row * BK + swz<BK>(row, 4 * st + 2 * lh) * 4);
+        const i32x4 hi = *reinterpret_cast<const i32x4*>(base + row * BK + swz<BK>(row, 4 * st + 2 * lh + 1) * 4);
+        return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      };
+      auto rd = [&](int st, i32x8* a, i32x8* b) {
 #pragma unroll
-        for (int i = 0; i < FM; ++i) {
-          const int row = wm * WTM + i * 32 + lr;
-          a[i] = *reinterpret_cast<const long*>(la + row * BK + swz<BK>(row, st) * 4 + 2 * lh);
-        }
+        for (int i = 0; i < FM; ++i) a[i] = rd32(la, wm * WTM + i * 32 + lr, st);
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
-          const int row = wn * WTN + j * 32 + lr;
-          b[j] = *reinterpret_cast<const long*>(lb + row * BK + swz<BK>(row, st) * 4 + 2 * lh);
-        }
+        for (int j = 0; j < FN; ++j) b[j] = rd32(lb, wn * WTN + j * 32 + lr, st);
       };
       rd(0, af[0], bf[0]);
       __builtin_amdgcn_s_setprio(1);
@@ -391,8 +409,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
         for (int i = 0; i < FM; ++i)
 #pragma unroll
           for (int j = 0; j < FN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_fp8_fp8(af[st & 1][i], bf[st & 1][j], acc[i][j], 0, 0, 0);
-        if (st + 1 < S) interleave<FM + FN, FM * FN>();
+            acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[st & 1][i], bf[st & 1][j], acc[i][j],
+                                                                         0, 0, 0, 127, 0, 127);
+        if (st + 1 < S) interleave2<FM + FN, FM * FN>();
       }
       __builtin_amdgcn_s_setprio(0);
     }
