@@ -13,6 +13,21 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
+// Accumulator register r of MFMA tile (i, j), lane `lane` -> (row, col) in
+// the wave's block.  32x32x16 C/D map: col = lane & 31, row = (r&3) + 8(r>>2)
+// + 4(lane>>5).  MF16 (four 16x16x32 tiles, sub-tile t = r >> 2 = 2a + b):
+// row = 16a + 4(lane>>4) + (r&3), col = 16b + (lane&15).
+template <bool MF16>
+__device__ __forceinline__ int acc_row(int i, int r, int lane) {
+  if constexpr (MF16) return 32 * i + 16 * (r >> 3) + 4 * ((lane >> 4) & 3) + (r & 3);
+  else return 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+}
+template <bool MF16>
+__device__ __forceinline__ int acc_col(int j, int r, int lane) {
+  if constexpr (MF16) return 32 * j + 16 * ((r >> 2) & 1) + (lane & 15);
+  else return 32 * j + (lane & 31);
+}
+
 // QuickGELU, x * sigmoid(1.702 x) (networks/model.py:166-168)
 __device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f + expf(-(1.702f * x)))); }
 
@@ -23,7 +38,7 @@ __device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f 
 // (one HBM round trip per slab, overlapping the staging).  When the tile exceeds the CAPF floats of LDS it goes in P row
 // slabs.  Called by every thread of the block after the k-loop's last
 // barrier (the LDS is free).
-template <int WM, int WN, int FM, int FN, int CAPF>
+template <int WM, int WN, int FM, int FN, int CAPF, bool MF16 = false>
 __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, const f32x16 (&acc)[FM][FN], float* lds,
                                                int m0, int n0) {
   constexpr int NT = 64 * WM * WN;
@@ -37,7 +52,6 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
   static_assert(ITERS * NT == SLAB * C4, "epilogue tiling");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
-  const int lr = lane & 31, lh = lane >> 5;
   const bool vec_ok = ((g.N & 3) == 0) && ((g.ldc & 3) == 0);
   float* ct = lds;  // [SLAB][BN] row-major
 #pragma unroll
@@ -65,8 +79,8 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
-            const int row = wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh - p * SLAB;
-            const int col = wn * WTN + j * 32 + lr;
+            const int row = wm * WTM + acc_row<MF16>(i, r, lane) - p * SLAB;
+            const int col = wn * WTN + acc_col<MF16>(j, r, lane);
             ct[row * BN + col] = acc[i][j][r];
           }
     }

@@ -80,9 +80,15 @@ __device__ __forceinline__ void interleave2() {
 
 // BK = 32: 64 KB LDS per 128x128 block, 2 blocks (2 waves/SIMD) per CU.
 // BK = 16: 32 KB, 3 blocks (3 waves/SIMD) per CU, twice the barriers.
-template <int WM, int WN, int FM, int FN, int AMODE, int EMODE, int BK, int DT, int MINB, int GL>
+// MF16 (bf16 only): each 32x32 tile of a wave's block is computed as four
+// v_mfma_f32_16x16x32_bf16 tiles (same cycles per FLOP as 32x32x16; the
+// 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
+// 'DVFS give-back' item 7).  Register r of tile (i, j) then maps through
+// acc_row / acc_col<true> (gemm_epilogue.hpp) instead of the 32x32 map.
+template <int WM, int WN, int FM, int FN, int AMODE, int EMODE, int BK, int DT, int MINB, int GL, int MF16 = 0>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, int tiles_n) {
   using ET = typename ElemT<DT>::T;
+  static_assert(!MF16 || DT == DT_BF16, "MF16: bf16 only");
   static_assert(DT == DT_F32 || (AMODE == A_DENSE && (BK == 32 || (BK == 16 && GL == 2))),
                 "low-precision GEMM: dense A, 128-B rows (64-B rows in the 4-stage pipeline)");
   static_assert(!GL || AMODE == A_DENSE, "LDS-DMA staging: dense A/B");
@@ -282,6 +288,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // MF16: sub-tile t = 2a + b (row half a, column half b) of tile (i, j)
+  f32x4 acc4[MF16 ? FM : 1][MF16 ? FN : 1][4];
+  if constexpr (MF16) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   const int lr = lane & 31, lh = lane >> 5;
 
@@ -347,6 +363,44 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
                                                              acc[i][j], 0, 0, 0);
       }
     }
+    } else if constexpr (DT == DT_BF16 && MF16) {
+      // BK/16 k-steps of 32; lane group g = lane>>4 holds k = 32s + 8g .. +7
+      // = 16-B slot 4s + g of rows (lane & 15) of each 16-row half.
+      constexpr int S = BK / 16;
+      const int l16 = lane & 15, lg = lane >> 4;
+      bf16x8 af[2][FM][2], bf[2][FN][2];
+      auto rd = [&](int st, bf16x8 (*a)[2], bf16x8 (*b)[2]) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = wm * WTM + i * 32 + h * 16 + l16;
+            a[i][h] = *reinterpret_cast<const bf16x8*>(la + row * BK + swz<BK>(row, 4 * st + lg) * 4);
+          }
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = wn * WTN + j * 32 + h * 16 + l16;
+            b[j][h] = *reinterpret_cast<const bf16x8*>(lb + row * BK + swz<BK>(row, 4 * st + lg) * 4);
+          }
+      };
+      rd(0, af[0], bf[0]);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int st = 0; st < S; ++st) {
+        if (st + 1 < S) rd(st + 1, af[(st + 1) & 1], bf[(st + 1) & 1]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              acc4[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[st & 1][i][t >> 1], bf[st & 1][j][t & 1],
+                                                                      acc4[i][j][t], 0, 0, 0);
+        if (st + 1 < S) interleave<2 * (FM + FN), 4 * FM * FN>();
+      }
+      __builtin_amdgcn_s_setprio(0);
     } else if constexpr (DT == DT_BF16) {
       // BK/8 k-steps of 16; lane half h holds k = 16s + 8h .. +7 = 16-B slot 2s + h.
       // Fragments are double-buffered in registers: step s+1's ds_reads are
@@ -423,10 +477,20 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     }
   }
   if constexpr (GL == 2) __syncthreads();  // epilogues reuse the LDS
+  if constexpr (MF16) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[i][j][4 * t + r] = acc4[i][j][t][r];
+  }
 
   // ---- epilogue ----
   // 32x32 C/D map: col (N index) = lane & 31, row (M index) = (r&3) + 8(r>>2) + 4(lane>>5)
-  if (g.scale_a != nullptr || g.scale_b != nullptr) {  // per-row dequantisation (fp8)
+  if (!MF16 && (g.scale_a != nullptr || g.scale_b != nullptr)) {  // per-row dequantisation (fp8)
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = n0 + wn * WTN + j * 32 + lr;
@@ -441,6 +505,51 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
         }
     }
   }
+  if constexpr (MF16 && EMODE == E_SCORES_T) {
+    // sub-tile t: rows acc_row(i, 4t) .. +3 (consecutive), one column
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = n0 + wn * WTN + acc_col<true>(j, 4 * q, lane);
+          const int mb = m0 + wm * WTM + acc_row<true>(i, 4 * q, lane);
+          if (n >= g.N) continue;
+          float* dst = g.C + (long long)n * g.ldc + mb;
+          if (mb + 3 < g.M) {
+            *reinterpret_cast<f32x4*>(dst) =
+                f32x4{acc[i][j][4 * q], acc[i][j][4 * q + 1], acc[i][j][4 * q + 2], acc[i][j][4 * q + 3]};
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (mb + e < g.M) dst[e] = acc[i][j][4 * q + e];
+          }
+        }
+  } else if constexpr (MF16 && EMODE == E_FILTER) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) {
+        const int n = n0 + wn * WTN + acc_col<true>(j, 4 * b, lane);
+        const bool nok = n < g.N;
+        const float t = nok ? g.tau[n] : __builtin_inff();
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int a = 0; a < 2; ++a)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = 8 * a + 4 * b + e;
+              const int m = m0 + wm * WTM + acc_row<true>(i, r, lane);
+              const float v = acc[i][j][r];
+              if (v > t && m < g.M) {
+                const int pos = atomicAdd(g.cnt + n, 1);
+                if (pos < g.cap) g.cand[(long long)n * g.cap + pos] = make_key(v, (uint32_t)(g.row_offset + m));
+              }
+            }
+      }
+  } else {
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = n0 + wn * WTN + j * 32 + lr;
@@ -481,11 +590,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
       }
     }
   }
+  }
 
-  if constexpr (EMODE == E_STORE) epilogue_store<WM, WN, FM, FN, NSTAGE * BUF>(g, Cb, acc, lds, m0, n0);
+  if constexpr (EMODE == E_STORE) epilogue_store<WM, WN, FM, FN, NSTAGE * BUF, (bool)MF16>(g, Cb, acc, lds, m0, n0);
 }
 
-template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0>
+template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0>
 static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM;
@@ -494,7 +604,7 @@ static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
   const unsigned splits = g.k_split > 0 ? (unsigned)((g.K + g.k_split - 1) / g.k_split) : 1u;
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL>), dim3((unsigned)nblk, splits),
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16>), dim3((unsigned)nblk, splits),
                      dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
@@ -601,21 +711,41 @@ static int pick_lp(const GemmArgs& g, int emode) {
   return cfg;
 }
 
-template <int EM, int DT>
-static hipError_t launch_lp(const GemmArgs& g, hipStream_t s) {
+// bf16 MFMA shape: four 16x16x32 per 32x32 tile (default; measured on MI355X,
+// tools/mf16_cmd.sh: ViT-B/16 linears +4-7 %, 128x128 cosine sweeps +2-5 %)
+// or 32x32x16 (RR_BF16_MF16=0).  The 256x320 sweep tile stays on 32x32x16:
+// its 16x16 fragments spill (180 B/lane).
+static bool bf16_mf16() {
+  static const bool on = [] {
+    const char* e = getenv("RR_BF16_MF16");
+    return e == nullptr || atoi(e) != 0;
+  }();
+  return on;
+}
+
+template <int EM, int DT, int MF16>
+static hipError_t launch_lp_mf(const GemmArgs& g, hipStream_t s) {
   constexpr int EPR = DT == DT_BF16 ? 64 : 128;  // elements per 128-B k-tile row
   int cfg = pick_lp(g, EM);
   if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles
   if (cfg == 5 && (g.K % (EPR / 2)) != 0) cfg = 1;
   switch (cfg) {
-    case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2>(g, s);
-    case 3: return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1>(g, s);
+    case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF16>(g, s);
+    case 3: return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF16>(g, s);
     case 4:
-      if constexpr (EM != E_STORE) return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1>(g, s);
+      if constexpr (EM != E_STORE) return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0>(g, s);
       return hipErrorInvalidValue;
-    case 5: return launch_t<2, 4, 4, 2, A_DENSE, EM, 16, DT, 1, 2>(g, s);
-    default: return launch_t<2, 2, 2, 2, A_DENSE, EM, 32, DT, 2>(g, s);
+    case 5: return launch_t<2, 4, 4, 2, A_DENSE, EM, 16, DT, 1, 2, MF16>(g, s);
+    default: return launch_t<2, 2, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF16>(g, s);
   }
+}
+
+template <int EM, int DT>
+static hipError_t launch_lp(const GemmArgs& g, hipStream_t s) {
+  if constexpr (DT == DT_BF16) {
+    if (bf16_mf16()) return launch_lp_mf<EM, DT, 1>(g, s);
+  }
+  return launch_lp_mf<EM, DT, 0>(g, s);
 }
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStream_t s, int timer_cls, int dt) {

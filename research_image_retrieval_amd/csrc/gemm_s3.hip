@@ -99,8 +99,14 @@ __device__ __forceinline__ void s3_load1x2(const f32x4* p0, const f32x4* p1, f32
 // reads v can be scheduled above it
 __device__ __forceinline__ void s3_launder(f32x4& v) { asm volatile("" : "+v"(v)); }
 
-template <int WM, int WN, int FM, int FN, int BK, int AMODE, int SEP, int MINB, int PIPE>
+// MF16 (BK = 32, SEP): each 32x32 tile is four v_mfma_f32_16x16x32_bf16
+// tiles (one 32-deep k-step per k-tile instead of two 16-deep ones; the
+// 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
+// 'DVFS give-back' item 7).  The k-tile's MFMAs go in two parts around the A
+// split: a0b0 + a1b1 + a0b1 + a1b0 (planes 0-1), then a0b2 + a2b0 (plane 2).
+template <int WM, int WN, int FM, int FN, int BK, int AMODE, int SEP, int MINB, int PIPE, int MF16 = 0>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
+  static_assert(!MF16 || (BK == 32 && SEP), "MF16: BK 32, separate small-term accumulator");
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int WTM = 32 * FM, WTN = 32 * FN;
   constexpr int BM = WTM * WM, BN = WTN * WN;
@@ -347,9 +353,92 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         }
     }
   };
-  auto compute = [&](int cur) {
+  // ---- MF16: 16x16x32 tiles, sub-tile t = 2a + b (row half a, column half b) ----
+  f32x4 hi4[MF16 ? FM : 1][MF16 ? FN : 1][4], lo4[MF16 ? FM : 1][MF16 ? FN : 1][4];
+  bf16x8 fa[MF16 ? 3 : 1][MF16 ? FM : 1][2], fb[MF16 ? 3 : 1][MF16 ? FN : 1][2];
+  if constexpr (MF16) {
 #pragma unroll
-    for (int st = 0; st < BK / 16; ++st) compute_st(cur, st);
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          hi4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+          lo4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+  }
+  const int l16 = lane & 15, lg = lane >> 4;
+  // plane p fragments of one 32-deep k-tile: lane group lg holds k = 8lg..8lg+7
+  // (16-B slot lg) of row l16 of each 16-row half
+  auto rd_mf = [&](int cur, int p) {
+    const uint16_t* la = lds + cur * BUF;
+    const uint16_t* lb = la + A_EL;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = wm * WTM + i * 32 + h * 16 + l16;
+        fa[MF16 ? p : 0][i][h] = *reinterpret_cast<const bf16x8*>(la + (p * BM + row) * BK + pswz<BK>(row, lg) * 8);
+      }
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = wn * WTN + j * 32 + h * 16 + l16;
+        fb[MF16 ? p : 0][j][h] = *reinterpret_cast<const bf16x8*>(lb + (p * BN + row) * BK + pswz<BK>(row, lg) * 8);
+      }
+  };
+#define RR_MF16(a, b, c) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
+  auto mf_part0 = [&](int cur) {
+    if constexpr (MF16) {
+      rd_mf(cur, 0);
+      rd_mf(cur, 1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) RR_MF16(fa[0][i][t >> 1], fb[0][j][t & 1], hi4[i][j][t]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            RR_MF16(fa[1][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
+            RR_MF16(fa[0][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
+            RR_MF16(fa[1][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
+          }
+    }
+  };
+  // with two A chunks per thread the plane-0 fragments are re-read in part 1
+  // rather than held across the A split (holding them spills)
+  constexpr bool MF_REREAD = A_CH >= 2;
+  auto mf_part1 = [&](int cur) {
+    if constexpr (MF16) {
+      if constexpr (MF_REREAD) rd_mf(cur, 0);
+      rd_mf(cur, 2);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            RR_MF16(fa[0][i][t >> 1], fb[2][j][t & 1], lo4[i][j][t]);
+            RR_MF16(fa[2][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
+          }
+    }
+  };
+#undef RR_MF16
+
+  auto compute = [&](int cur) {
+    if constexpr (MF16) {
+      mf_part0(cur);
+      mf_part1(cur);
+    } else {
+#pragma unroll
+      for (int st = 0; st < BK / 16; ++st) compute_st(cur, st);
+    }
   };
 
   constexpr int A_LD = 2 * A_CH;  // A global loads per tile per thread
@@ -418,14 +507,19 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     auto iter = [&](int kt, int cur) __attribute__((always_inline)) {
       glds_b(min(kt + 1, nk - 1), cur ^ 1);
       load_a(min(kt + 2, nk - 1), cur);
-      compute_st(cur, 0);
+      if constexpr (MF16) mf_part0(cur);
+      else compute_st(cur, 0);
       // A(kt+1) landed (the B DMA of kt+1 and the A loads of kt+2 may not
       // have): its split overlaps the remaining MFMAs of tile kt
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
       launder_a(cur ^ 1);
       split_a(cur ^ 1);
+      if constexpr (MF16) {
+        mf_part1(cur);
+      } else {
 #pragma unroll
-      for (int st = 1; st < BK / 16; ++st) compute_st(cur, st);
+        for (int st = 1; st < BK / 16; ++st) compute_st(cur, st);
+      }
       write_a(cur ^ 1);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of kt+1 landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -445,24 +539,41 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
-  if constexpr (SEP) {
+  if constexpr (MF16) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) hi[i][j][4 * t + e] = hi4[i][j][t][e] + lo4[i][j][t][e];
+  } else if constexpr (SEP) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) hi[i][j] += lo[i][j];
   }
-  epilogue_store<WM, WN, FM, FN, BUF>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
+  epilogue_store<WM, WN, FM, FN, BUF, (bool)MF16>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
 }
 
 static int s3_pipe();
+static bool s3_mf16();
 
-template <int WM, int WN, int FM, int FN, int BK, int AM, int SEP, int MINB>
+template <int WM, int WN, int FM, int FN, int BK, int AM, int SEP, int MINB, int MF16 = 0>
 static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
+  if constexpr (MF16) {
+    if (s3_pipe()) {
+      hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, SEP, MINB, 1, 1>), dim3((unsigned)nblk),
+                         dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
+      return hipGetLastError();
+    }
+  }
   if (s3_pipe())
     hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, SEP, MINB, 1>), dim3((unsigned)nblk), dim3(64 * WM * WN),
                        0, s, g, (int)tiles_n);
@@ -504,6 +615,20 @@ static int s3_pipe() {
   }();
   return v;
 }
+// 16x16x32 MFMA tiles in config 4 (128x256, 8 waves, 2 per SIMD), used for
+// every layer with N % 256 == 0.  Measured per R101 layer at 320 images
+// (tools/s3mf_cmd.sh, gpurun_out/s3mf): config 4 on 16x16x32 runs every
+// N >= 256 layer 3-14 % faster than the previous pick (mostly config 3) — the
+// 3x3 256@14 layers (x22) 0.372 -> 0.336 ms — so the trunk 31.5 -> 29.5 ms.
+// The same shape is slower in the one-wave-per-SIMD configs 2 and 5 and
+// spills in config 3.  RR_S3_MF16=0 restores the 32x32x16 picks.
+static bool s3_mf16() {
+  static const bool v = [] {
+    const char* e = getenv("RR_S3_MF16");
+    return !(e != nullptr && atoi(e) == 0);
+  }();
+  return v;
+}
 static bool s3_sep() {
   static const bool v = [] {
     const char* e = getenv("RR_S3_SEP");
@@ -515,6 +640,7 @@ static bool s3_sep() {
 static int pick_s3(const GemmArgs& g) {
   const int f = s3_forced_cfg();
   if (f >= 1 && f <= 6) return f;
+  if (s3_mf16() && s3_pipe() && (g.N % 256) == 0) return 4;
   // rounds of resident blocks x tile area per CU / relative per-FLOP speed
   auto cost = [&](long long bm, long long bn, long long per_cu, double speed) {
     const long long slots = 256 * per_cu;
@@ -535,7 +661,9 @@ static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s) {
   switch (cfg) {
     case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1, 1>(g, s);
     case 3: return launch_s3_t<4, 2, 2, 2, 32, AM, 1, 1>(g, s);
-    case 4: return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1>(g, s);
+    case 4:
+      if (s3_mf16()) return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1, 1>(g, s);
+      return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1>(g, s);
     case 5: return launch_s3_t<4, 1, 2, 2, 32, AM, 1, 1>(g, s);
     case 6: return launch_s3_t<4, 1, 2, 2, 16, AM, 1, 2>(g, s);
     default: return launch_s3_t<2, 2, 2, 2, 16, AM, 1, 2>(g, s);
