@@ -706,6 +706,12 @@ static int pick_lp(const GemmArgs& g, int emode) {
   int cfg = 1;
   if (cost(256, 64, 512, 1.0) < best) best = cost(256, 64, 512, 1.0), cfg = 2;
   if (emode == E_STORE && cost(256, 256, 256, 1.25) < best) best = cost(256, 256, 256, 1.25), cfg = 3;
+  // filter sweeps other than the long-K bf16 one (which takes q320 below):
+  // the 8-wave 256x256 tile wins at >= 1024 queries (measured at 1280 queries
+  // x 1.6 M rows: bf16 d = 512 3.27 -> 2.39 ms, fp8 d = 2048 11.2 -> 8.1 ms
+  // per C5 step); at 320 queries the cost model keeps 128x128
+  if (emode == E_FILTER && (g.K < 1024 || g.scale_a != nullptr) && cost(256, 256, 256, 1.25) < best)
+    best = cost(256, 256, 256, 1.25), cfg = 3;
   if (emode != E_STORE && g.K >= 1024 && g.scale_a == nullptr && cost(256, 320, 256, 1.35) < best)
     best = cost(256, 320, 256, 1.35), cfg = 4;
   return cfg;
