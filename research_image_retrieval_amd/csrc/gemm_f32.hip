@@ -746,9 +746,20 @@ static hipError_t launch_lp_mf(const GemmArgs& g, hipStream_t s) {
   }
 }
 
+// RR_GEMM_8P=1: bf16 GEMMs that pick the 256x256 tile run on the 8-phase
+// pipeline of gemm_8p.hip instead
+static bool use_8p() {
+  static const bool on = [] {
+    const char* e = getenv("RR_GEMM_8P");
+    return e != nullptr && atoi(e) != 0;
+  }();
+  return on;
+}
+
 template <int EM, int DT>
 static hipError_t launch_lp(const GemmArgs& g, hipStream_t s) {
   if constexpr (DT == DT_BF16) {
+    if (use_8p() && pick_lp(g, EM) == 3 && gemm_8p_eligible(g)) return launch_gemm_8p(g, EM, s);
     if (bf16_mf16()) return launch_lp_mf<EM, DT, 1>(g, s);
   }
   return launch_lp_mf<EM, DT, 0>(g, s);

@@ -134,6 +134,11 @@ struct GemmArgs {
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,
                 int dt = DT_F32);
 
+// bf16 GEMM on the 256x256 8-phase LDS-DMA pipeline (gemm_8p.hip): dense A/B,
+// K % 128 == 0, no split-K / scales
+bool gemm_8p_eligible(const GemmArgs& g);
+hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s);
+
 // fp32-accurate GEMM on bf16 MFMA (gemm_s3.hip): A fp32 (A_DENSE or A_CONV),
 // B = bf16 planes [3][N][ldb] from launch_split3, E_STORE epilogue
 int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls);

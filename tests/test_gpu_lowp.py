@@ -67,6 +67,33 @@ def test_lowp_cosine_recall_at_100(cuda, dtype, min_recall):
     assert (i[:6, 0] == i_ref[:6, 0]).all()  # planted near-duplicates stay first
 
 
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+def test_lowp_topk_many_queries_vs_dequantised(cuda, dtype):
+    """>= 1024 queries over 200 k rows: the filter sweep runs on the 8-wave
+    256x256 tile (16x16x32 bf16 / block-scaled fp8 MFMA).  The returned scores
+    are the fp32 dot products of the dequantised rows, and the returned lists
+    are the top-100 of those scores (torch on the same dequantised rows)."""
+    g = torch.Generator(device=cuda).manual_seed(11)
+    n, d, q, k = 200_000, 512, 1100, 100
+    gal = torch.nn.functional.normalize(torch.randn(n, d, device=cuda, generator=g), dim=1)
+    qs_ = torch.nn.functional.normalize(torch.randn(q, d, device=cuda, generator=g), dim=1)
+    gl, gs = ops.quantize_rows(gal, dtype)
+    ql, qs = ops.quantize_rows(qs_, dtype)
+    s, i = ops.cosine_topk_lp(ql, qs, gl, gs, k, dtype)
+    if dtype == "bf16":
+        gd, qd = gl.float(), ql.float()
+    else:
+        gd = gl.view(torch.float8_e4m3fn).float() * gs[:, None]
+        qd = ql.view(torch.float8_e4m3fn).float() * qs[:, None]
+    ref = qd @ gd.t()
+    got = torch.gather(ref, 1, i)
+    torch.testing.assert_close(s, got, rtol=1e-4, atol=1e-5)
+    kth = torch.topk(ref, k, dim=1).values[:, -1:]
+    assert bool((s >= kth - 1e-5).all())  # every returned row is in the top-k up to ties
+    assert bool((s[:, :-1] >= s[:, 1:]).all())  # descending
+    del ref
+
+
 def test_vit_b16_bf16_vs_reference(cuda):
     fx = np.load(os.path.join(GOLD, "vit.npz"))
     res, patch, width, layers, heads, out_dim, seed = (int(v) for v in fx["b16_cfg"])

@@ -57,10 +57,12 @@ def test_linear_s3_accuracy_vs_float64(cuda, m, k, n):
     assert es3[0] <= ef32[0] and es3[1] <= ef32[1]
 
 
-@pytest.mark.parametrize("m,k,n", [(77, 32, 130), (300, 64, 64), (129, 96, 257), (513, 160, 64), (33, 32, 64)])
+@pytest.mark.parametrize("m,k,n", [(77, 32, 130), (300, 64, 64), (129, 96, 257), (513, 160, 64), (33, 32, 64),
+                                   (77, 32, 256), (129, 96, 512), (33, 160, 256), (300, 64, 768)])
 def test_linear_s3_kloop_edges(cuda, m, k, n):
     """Edges of the async-A k-loop (1, 2, 3, 5 k-tiles; ragged M and N on both
-    tile configs, N = 64 -> 256x64 tiles): fp32-grade against float64 (error
+    tile configs, N = 64 -> 256x64 tiles, N % 256 == 0 -> the 128x256 tile on
+    16x16x32 MFMAs): fp32-grade against float64 (error
     relative to sum |a||b| below 4e-7; at these short K the final hi + lo
     rounding dominates, so no ordering against the fp32 core is asserted)."""
     g = torch.Generator().manual_seed(7 * m + k + n)
@@ -73,9 +75,12 @@ def test_linear_s3_kloop_edges(cuda, m, k, n):
     assert e[0] < 4e-7, e
 
 
-def test_linear_s3_epilogue(cuda):
+@pytest.mark.parametrize("n", [320, 256])
+def test_linear_s3_epilogue(cuda, n):
+    """bias / residual / ReLU / QuickGELU through the stored-C epilogue, on the
+    32x32x16 accumulator map (n = 320) and the 16x16x32 one (n = 256)."""
     g = torch.Generator().manual_seed(5)
-    m, k, n = 200, 512, 320
+    m, k = 200, 512
     a, w = torch.randn(m, k, generator=g), torch.randn(n, k, generator=g) / k ** 0.5
     b, r = torch.randn(n, generator=g), torch.randn(m, n, generator=g)
     w3 = ops.split3_bf16(w.to(cuda))
