@@ -101,9 +101,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   constexpr int SLOTS = BK / 4;
   constexpr int ROWS_PER_PASS = NT / SLOTS;
   constexpr int A_CH = BM / ROWS_PER_PASS;
-  constexpr int B_CH = BN / ROWS_PER_PASS;
+  // B rows may end in a partial staging pass (320 rows in 128-row passes):
+  // only the waves whose rows fall inside it issue that pass (LDS-DMA only)
+  constexpr int B_CH = (BN + ROWS_PER_PASS - 1) / ROWS_PER_PASS;
+  constexpr int B_TAIL = BN - (B_CH - 1) * ROWS_PER_PASS;
+  constexpr bool B_PART = B_TAIL != ROWS_PER_PASS;
   static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for block");
-  static_assert(BM % ROWS_PER_PASS == 0 && BN % ROWS_PER_PASS == 0, "staging passes must tile the block");
+  static_assert(BM % ROWS_PER_PASS == 0, "staging passes must tile the block");
+  static_assert(!B_PART || (GL && B_TAIL % (64 / SLOTS) == 0), "partial B pass: LDS-DMA, whole waves");
   constexpr int BUF = (BM + BN) * BK;  // floats per LDS buffer
   // GL == 2: 4-stage LDS-DMA ring, three k-tiles in flight across raw
   // barriers with counted vmcnt (never drained to 0 in the steady state)
@@ -259,6 +264,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
+      if (B_PART && i == B_CH - 1 && wv * (64 / SLOTS) >= B_TAIL) continue;  // wave-uniform
       const int row = crow + i * ROWS_PER_PASS;
       __builtin_amdgcn_global_load_lds(
           (const void*)(b_ptr[i] + (long long)kt * EPR + swz<BK>(row, slot) * CH),
@@ -302,6 +308,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   const int lr = lane & 31, lh = lane >> 5;
 
   constexpr int LPT = A_CH + B_CH;  // LDS-DMA instructions per k-tile per wave
+  constexpr int LPT_S = B_PART ? LPT - 1 : LPT;  // ... for waves outside the partial B pass
+  const bool short_w = B_PART && __builtin_amdgcn_readfirstlane(wave) * (64 / SLOTS) >= B_TAIL;
   if constexpr (GL == 2) {
 #pragma unroll
     for (int t = 0; t < NSTAGE - 1; ++t)
@@ -321,9 +329,15 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
       cur = kt & (NSTAGE - 1);
       // tile kt is retired once at most the younger tiles' DMAs are pending
       const int younger = nk - 1 - kt;
-      if (younger >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPT) : "memory");
-      else if (younger == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (younger >= 2) {
+        if (short_w) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPT_S) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPT) : "memory");
+      } else if (younger == 1) {
+        if (short_w) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT_S) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
       __builtin_amdgcn_s_barrier();  // all waves' DMAs for kt landed; all reads of kt-1 done
       asm volatile("" ::: "memory");
       if (kt + NSTAGE - 1 < nk) glds_tile(kt + NSTAGE - 1, (kt + NSTAGE - 1) & (NSTAGE - 1));
@@ -689,8 +703,10 @@ static int pick_lp(const GemmArgs& g, int emode) {
     if (!strcmp(e, "big")) return 3;
     if (!strcmp(e, "q320")) return 4;
     if (!strcmp(e, "big4")) return 5;
+    if (!strcmp(e, "q320r")) return 6;
     return 0;
   }();
+  if (forced == 6 && emode == E_STORE) return 3;
   if (forced == 4 && emode == E_STORE) return 3;
   if (forced) return forced;
   // rounds x tile area / relative per-FLOP speed (measured, tools/lp_bench.py:
@@ -734,7 +750,7 @@ static hipError_t launch_lp_mf(const GemmArgs& g, hipStream_t s) {
   constexpr int EPR = DT == DT_BF16 ? 64 : 128;  // elements per 128-B k-tile row
   int cfg = pick_lp(g, EM);
   if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles
-  if (cfg == 5 && (g.K % (EPR / 2)) != 0) cfg = 1;
+  if ((cfg == 5 || cfg == 6) && (g.K % (EPR / 2)) != 0) cfg = 1;
   switch (cfg) {
     case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF16>(g, s);
     case 3: return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF16>(g, s);
@@ -742,6 +758,11 @@ static hipError_t launch_lp_mf(const GemmArgs& g, hipStream_t s) {
       if constexpr (EM != E_STORE) return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0>(g, s);
       return hipErrorInvalidValue;
     case 5: return launch_t<2, 4, 4, 2, A_DENSE, EM, 16, DT, 1, 2, MF16>(g, s);
+    case 6:
+      // q320 on the 4-stage LDS-DMA ring (64-B rows, three k-tiles in flight;
+      // B staged in 128-row passes, the last one half-issued)
+      if constexpr (EM != E_STORE) return launch_t<4, 2, 2, 5, A_DENSE, EM, 16, DT, 1, 2, 0>(g, s);
+      return hipErrorInvalidValue;
     default: return launch_t<2, 2, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF16>(g, s);
   }
 }
