@@ -17,7 +17,9 @@
  *     except the explicit *_collect / *_sync helpers.
  *   - Return value: 0 on success, a negative RR_E* code on error; the message
  *     is available from rr_last_error(h).  The library never aborts.
- *   - One handle per device; handles are independent across threads.
+ *   - One handle per device; handles are independent across threads.  Every
+ *     entry point runs on its handle's device: the calling thread's current
+ *     HIP device is switched to it for the call and restored afterwards.
  */
 #ifndef RR_H_
 #define RR_H_
@@ -54,6 +56,23 @@ const char* rr_last_error(rr_handle_t h);
  *          5 = fused attention (ViT). */
 int rr_timing_enable(rr_handle_t h, int enable);
 int rr_timing_collect(rr_handle_t h, int cls, double* ms, long long* launches);
+
+/* The device a handle was created for (rr_create's `device`). */
+int rr_get_device(rr_handle_t h, int* device);
+
+/* Kernel tile-config overrides for this handle (tests and tuning tools; the
+ * default 0 = the library's own pick, which the product path always uses).
+ *   RR_TUNE_GEMM_CFG: exact-fp32 core tile, 22 (128x128), 41 (256x64), 88 (256x256)
+ *   RR_TUNE_GEMM_BK:  exact-fp32 core k-tile depth, 16 or 32
+ *   RR_TUNE_LP_CFG:   bf16/fp8 core, 1 (128x128), 2 (256x64), 3 (256x256),
+ *                     4 (256x320 for filter / score sweeps, 256x256 otherwise)
+ *   RR_TUNE_S3_CFG:   split-bf16 core, 1..6 (gemm_s3.hip tile table)
+ * Any other key or value: RR_EINVAL. */
+#define RR_TUNE_GEMM_CFG 1
+#define RR_TUNE_GEMM_BK 2
+#define RR_TUNE_LP_CFG 3
+#define RR_TUNE_S3_CFG 4
+int rr_set_tuning(rr_handle_t h, int key, int value);
 
 /* ---- search (ranker) ----------------------------------------------------
  * Replaces iris_evaluate.py:383 `torch.mm(q, g.t())` + :386

@@ -9,17 +9,22 @@ Reference sites restated (src/benchmark/):
     layer1..4; Bottleneck v1.5, stride on the 3x3)
                                        networks/backbone.py:60-109,
                                        models/gem_pooling.py:34-44
-    torchvision 0.22.1 (requirements.txt:9) is not installed here; this is a
-    restatement of its published architecture: "parity unpinned" at that
-    boundary.
+    torchvision 0.22.1 (requirements.txt:9) is not installed here.  The trunk
+    is pinned through the reference's own torchvision-free R101, ResNet_DOLG
+    (networks/backbone.py:218-274, ResBlock/BottleneckTransform :305-345),
+    which is the same stem / maxpool / eval-BN / residual+ReLU composition at
+    depth (3,4,23,3) with the stride on the 1x1 (stride_on="1x1"):
+    tests/golden/resnet_dolg.npz holds its (x3, x4).  The v1.5 stride
+    placement differs only in which conv of the first block of a stage
+    carries stride 2.
   * gem (p=3.0 python float)           networks/RetrievalNet.py:318-325
   * GeMPooling (tensor p)              models/gem_pooling.py:12-23
   * whiten 1x1 conv + F.normalize      networks/RetrievalNet.py:337-344
   * feature_proj Linear + F.normalize  models/gem_pooling.py:58-92
   * ConvDimReduction apply             networks/spca.py:205-227
   * extract_vectors multi-scale        utils/helpfunc.py:18-48
-The pieces other than the trunk are pinned by tests/golden fixtures generated
-from the reference's own functions.
+Every piece is pinned by tests/golden fixtures generated from the reference's
+own functions (tests/golden/make_golden.py).
 """
 import torch
 import torch.nn.functional as F
@@ -40,39 +45,51 @@ def _bn(x, sd, p):
                         False, 0.0, BN_EPS)
 
 
-def resnet_trunk(x, sd, layers):
-    """torchvision ResNet forward up to layer4 (eval mode), NCHW."""
+def resnet_trunk(x, sd, layers, stride_on="3x3", return_x3=False):
+    """ResNet forward up to layer4 (eval mode), NCHW, torchvision keys.
+
+    stride_on="3x3": torchvision v1.5 Bottleneck (stride on conv2);
+    stride_on="1x1": the reference's own ResNet_DOLG / ResBlock +
+    BottleneckTransform (networks/backbone.py:218-274, :305-345; stride on the
+    1x1 `a` conv; ResBlock adds bn(proj(x)) + f(x) then ReLU, :340-346).
+    return_x3: also return layer3's output (ResNet_DOLG.forward returns (x3, x4))."""
+    if stride_on not in ("3x3", "1x1"):
+        raise ValueError("stride_on must be '3x3' or '1x1'")
     x = F.relu(_bn(F.conv2d(x, sd["conv1.weight"], None, 2, 3), sd, "bn1"))
     x = F.max_pool2d(x, 3, 2, 1)
+    x3 = None
     for li, nb in enumerate(layers):
         for bi in range(nb):
             p = f"layer{li + 1}.{bi}"
             s = 2 if (bi == 0 and li > 0) else 1
+            s1, s2 = (1, s) if stride_on == "3x3" else (s, 1)
             idn = x
             if bi == 0:
                 idn = _bn(F.conv2d(x, sd[p + ".downsample.0.weight"], None, s), sd, p + ".downsample.1")
-            y = F.relu(_bn(F.conv2d(x, sd[p + ".conv1.weight"]), sd, p + ".bn1"))
-            y = F.relu(_bn(F.conv2d(y, sd[p + ".conv2.weight"], None, s, 1), sd, p + ".bn2"))
+            y = F.relu(_bn(F.conv2d(x, sd[p + ".conv1.weight"], None, s1), sd, p + ".bn1"))
+            y = F.relu(_bn(F.conv2d(y, sd[p + ".conv2.weight"], None, s2, 1), sd, p + ".bn2"))
             y = _bn(F.conv2d(y, sd[p + ".conv3.weight"]), sd, p + ".bn3")
-            x = F.relu(y + idn)
-    return x
+            x = F.relu(idn + y)
+        if li == 2:
+            x3 = x
+    return (x3, x) if return_x3 else x
 
 
 def gem(x, p=3.0, eps=1e-6):
     return F.avg_pool2d(x.clamp(min=eps).pow(p), (x.size(-2), x.size(-1))).pow(1.0 / p)
 
 
-def gem_net_forward_test(x, sd, layers, whiten_w, whiten_b):
+def gem_net_forward_test(x, sd, layers, whiten_w, whiten_b, stride_on="3x3"):
     """networks.GeM.forward_test: trunk -> gem -> whiten 1x1 conv -> F.normalize."""
-    f = resnet_trunk(x, sd, layers)
+    f = resnet_trunk(x, sd, layers, stride_on)
     f = gem(f)
     f = F.conv2d(f, whiten_w.view(whiten_w.shape[0], -1, 1, 1), whiten_b).squeeze(-1).squeeze(-1)
     return F.normalize(f, dim=-1)
 
 
-def gem_model_descriptor(x, sd, layers, proj_w, proj_b, p=3.0):
+def gem_model_descriptor(x, sd, layers, proj_w, proj_b, p=3.0, stride_on="3x3"):
     """GeMModel.extract_descriptor: trunk -> GeMPooling -> Linear -> F.normalize(p=2, dim=1)."""
-    f = resnet_trunk(x, sd, layers)
+    f = resnet_trunk(x, sd, layers, stride_on)
     pt = torch.ones(1) * p
     f = F.avg_pool2d(f.clamp(min=1e-6).pow(pt), (f.size(-2), f.size(-1))).pow(1.0 / pt)
     f = F.linear(f.view(f.size(0), -1), proj_w, proj_b)

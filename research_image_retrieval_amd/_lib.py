@@ -19,6 +19,8 @@ RR_OK, RR_EINVAL, RR_EHIP, RR_EWORKSPACE, RR_EOVERFLOW = 0, -1, -2, -3, -4
 
 # timing classes (rr_timing_enable / rr_timing_collect)
 TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM, TIME_COSINE_SEED, TIME_ATTN = 0, 1, 2, 3, 4, 5
+# rr_set_tuning keys
+TUNE_GEMM_CFG, TUNE_GEMM_BK, TUNE_LP_CFG, TUNE_S3_CFG = 1, 2, 3, 4
 
 _lib = None
 _lock = threading.RLock()
@@ -37,6 +39,8 @@ SIGNATURES = {
     "rr_last_error": (ctypes.c_char_p, [_vp]),
     "rr_timing_enable": (_i, [_vp, _i]),
     "rr_timing_collect": (_i, [_vp, _i, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(_ll)]),
+    "rr_get_device": (_i, [_vp, ctypes.POINTER(_i)]),
+    "rr_set_tuning": (_i, [_vp, _i, _i]),
     "rr_cosine_topk_workspace_size": (_sz, [_i, _ll, _i, _i]),
     "rr_cosine_topk": (_i, [_vp, _vp, _i, _vp, _ll, _i, _i, _ll, _vp, _vp, _vp, _sz, _vp]),
     "rr_cosine_scores": (_i, [_vp, _vp, _i, _vp, _ll, _i, _vp, _vp]),

@@ -181,7 +181,7 @@ extern "C" int rr_preprocess_u8(rr_handle_t h, const uint8_t* img, int b, int hg
 
 extern "C" int rr_preprocess_u8_ex(rr_handle_t h, const uint8_t* img, int b, int hgt, int wid, const float* mean3,
                                    const float* std3, int out_c, float* out, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!img || !out || !mean3 || !std3 || b < 0 || hgt < 0 || wid < 0 || (out_c != 3 && out_c != 4) ||
       (out_c == 4 && ((uintptr_t)out & 15)))
     return set_error(h, RR_EINVAL, "rr_preprocess_u8: bad argument (out_c 3 or 4, 16-B aligned out)");
@@ -201,7 +201,7 @@ extern "C" int rr_nchw_to_nhwc(rr_handle_t h, const float* in, int b, int c, int
 
 extern "C" int rr_nchw_to_nhwc_ex(rr_handle_t h, const float* in, int b, int c, int hgt, int wid, int out_c,
                                   float* out, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!in || !out || b < 0 || c <= 0 || hgt < 0 || wid < 0 || out_c < c)
     return set_error(h, RR_EINVAL, "rr_nchw_to_nhwc: bad argument");
   const long long total = (long long)b * out_c * hgt * wid;
@@ -215,7 +215,7 @@ extern "C" int rr_nchw_to_nhwc_ex(rr_handle_t h, const float* in, int b, int c, 
 
 extern "C" int rr_maxpool2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int c, int k, int stride, int pad,
                             float* y, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !y || b < 0 || c <= 0 || k <= 0 || stride <= 0 || pad < 0 || 2 * pad > k)
     return set_error(h, RR_EINVAL, "rr_maxpool2d: bad argument");
   const int oh = (hgt + 2 * pad - k) / stride + 1, ow = (wid + 2 * pad - k) / stride + 1;
@@ -235,7 +235,7 @@ extern "C" int rr_maxpool2d(rr_handle_t h, const float* x, int b, int hgt, int w
 
 extern "C" int rr_gem_pool(rr_handle_t h, const float* x, int b, int hw, int c, float p, float eps, float* out,
                            void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !out || b < 0 || hw <= 0 || c <= 0 || !(p > 0.f)) return set_error(h, RR_EINVAL, "rr_gem_pool: bad argument");
   const long long total = (long long)b * c;
   if (total == 0) return RR_OK;
@@ -246,7 +246,7 @@ extern "C" int rr_gem_pool(rr_handle_t h, const float* x, int b, int hw, int c, 
 }
 
 extern "C" int rr_l2_normalize(rr_handle_t h, const float* x, int m, int d, float eps, float* y, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !y || m < 0 || d <= 0) return set_error(h, RR_EINVAL, "rr_l2_normalize: bad argument");
   if (m == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
@@ -258,7 +258,7 @@ extern "C" int rr_l2_normalize(rr_handle_t h, const float* x, int m, int d, floa
 
 extern "C" int rr_resize_bilinear(rr_handle_t h, const float* x, int b, int hgt, int wid, int c, int out_h, int out_w,
                                   float inv_scale_h, float inv_scale_w, float* y, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !y || b < 0 || hgt <= 0 || wid <= 0 || c <= 0 || out_h <= 0 || out_w <= 0)
     return set_error(h, RR_EINVAL, "rr_resize_bilinear: bad argument");
   const float sh = inv_scale_h > 0.f ? inv_scale_h : (float)hgt / (float)out_h;
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void alpha_qe_kernel(const float* __restrict__
 extern "C" int rr_alpha_qe(rr_handle_t h, const float* queries, int nq, const float* gallery, int d,
                            const long long* top_idx, const float* top_scores, int k, int n, float alpha,
                            long long idx_offset, float* out, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!queries || !gallery || !top_idx || !top_scores || !out || nq < 0 || d <= 0 || (d & 3) || k <= 0 || n < 0 ||
       n > k || ((uintptr_t)queries & 15) || ((uintptr_t)gallery & 15) || ((uintptr_t)out & 15))
     return set_error(h, RR_EINVAL, "rr_alpha_qe: bad argument (d % 4 == 0, 0 <= n <= k, 16-B aligned rows)");

@@ -89,8 +89,7 @@ template <int WM, int WN, int FM, int FN, int AMODE, int EMODE, int BK, int DT, 
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, int tiles_n) {
   using ET = typename ElemT<DT>::T;
   static_assert(!MF16 || DT == DT_BF16, "MF16: bf16 only");
-  static_assert(DT == DT_F32 || (AMODE == A_DENSE && (BK == 32 || (BK == 16 && GL == 2))),
-                "low-precision GEMM: dense A, 128-B rows (64-B rows in the 4-stage pipeline)");
+  static_assert(DT == DT_F32 || (AMODE == A_DENSE && BK == 32), "low-precision GEMM: dense A, 128-B rows");
   static_assert(!GL || AMODE == A_DENSE, "LDS-DMA staging: dense A/B");
   constexpr int ES = (int)sizeof(ET);
   constexpr int EPR = BK * 4 / ES;  // elements per LDS row (= k per k-tile)
@@ -101,19 +100,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   constexpr int SLOTS = BK / 4;
   constexpr int ROWS_PER_PASS = NT / SLOTS;
   constexpr int A_CH = BM / ROWS_PER_PASS;
-  // B rows may end in a partial staging pass (320 rows in 128-row passes):
-  // only the waves whose rows fall inside it issue that pass (LDS-DMA only)
-  constexpr int B_CH = (BN + ROWS_PER_PASS - 1) / ROWS_PER_PASS;
-  constexpr int B_TAIL = BN - (B_CH - 1) * ROWS_PER_PASS;
-  constexpr bool B_PART = B_TAIL != ROWS_PER_PASS;
+  constexpr int B_CH = BN / ROWS_PER_PASS;
   static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for block");
-  static_assert(BM % ROWS_PER_PASS == 0, "staging passes must tile the block");
-  static_assert(!B_PART || (GL && B_TAIL % (64 / SLOTS) == 0), "partial B pass: LDS-DMA, whole waves");
+  static_assert(BM % ROWS_PER_PASS == 0 && BN % ROWS_PER_PASS == 0, "staging passes must tile the block");
   constexpr int BUF = (BM + BN) * BK;  // floats per LDS buffer
-  // GL == 2: 4-stage LDS-DMA ring, three k-tiles in flight across raw
-  // barriers with counted vmcnt (never drained to 0 in the steady state)
-  constexpr int NSTAGE = GL == 2 ? 4 : 2;
-  __shared__ __attribute__((aligned(16))) float lds[NSTAGE * BUF];
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -264,7 +255,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     }
 #pragma unroll
     for (int i = 0; i < B_CH; ++i) {
-      if (B_PART && i == B_CH - 1 && wv * (64 / SLOTS) >= B_TAIL) continue;  // wave-uniform
       const int row = crow + i * ROWS_PER_PASS;
       __builtin_amdgcn_global_load_lds(
           (const void*)(b_ptr[i] + (long long)kt * EPR + swz<BK>(row, slot) * CH),
@@ -307,14 +297,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
 
   const int lr = lane & 31, lh = lane >> 5;
 
-  constexpr int LPT = A_CH + B_CH;  // LDS-DMA instructions per k-tile per wave
-  constexpr int LPT_S = B_PART ? LPT - 1 : LPT;  // ... for waves outside the partial B pass
-  const bool short_w = B_PART && __builtin_amdgcn_readfirstlane(wave) * (64 / SLOTS) >= B_TAIL;
-  if constexpr (GL == 2) {
-#pragma unroll
-    for (int t = 0; t < NSTAGE - 1; ++t)
-      if (t < nk) glds_tile(t, t);
-  } else if constexpr (GL == 1) {
+  if constexpr (GL) {
     glds_tile(0, 0);
     __syncthreads();
   } else {
@@ -324,29 +307,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   }
 
   for (int kt = 0; kt < nk; ++kt) {
-    int cur;
-    if constexpr (GL == 2) {
-      cur = kt & (NSTAGE - 1);
-      // tile kt is retired once at most the younger tiles' DMAs are pending
-      const int younger = nk - 1 - kt;
-      if (younger >= 2) {
-        if (short_w) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPT_S) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPT) : "memory");
-      } else if (younger == 1) {
-        if (short_w) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT_S) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(LPT) : "memory");
-      } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_s_barrier();  // all waves' DMAs for kt landed; all reads of kt-1 done
-      asm volatile("" ::: "memory");
-      if (kt + NSTAGE - 1 < nk) glds_tile(kt + NSTAGE - 1, (kt + NSTAGE - 1) & (NSTAGE - 1));
-    } else {
-      cur = kt & 1;
-      if (kt + 1 < nk) {
-        if constexpr (GL) glds_tile(kt + 1, cur ^ 1);
-        else load_tile(kt + 1);
-      }
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      if constexpr (GL) glds_tile(kt + 1, cur ^ 1);
+      else load_tile(kt + 1);
     }
     const float* la = lds + cur * BUF;
     const float* lb = la + BM * BK;
@@ -483,14 +447,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
       }
       __builtin_amdgcn_s_setprio(0);
     }
-    if constexpr (GL != 2) {
-      if constexpr (!GL) {
-        if (kt + 1 < nk) store_tile(cur ^ 1);
-      }
-      __syncthreads();  // with GL: also the vmcnt(0) that retires the DMA
+    if constexpr (!GL) {
+      if (kt + 1 < nk) store_tile(cur ^ 1);
     }
+    __syncthreads();  // with GL: also the vmcnt(0) that retires the DMA
   }
-  if constexpr (GL == 2) __syncthreads();  // epilogues reuse the LDS
   if constexpr (MF16) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -606,7 +567,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   }
   }
 
-  if constexpr (EMODE == E_STORE) epilogue_store<WM, WN, FM, FN, NSTAGE * BUF, (bool)MF16>(g, Cb, acc, lds, m0, n0);
+  if constexpr (EMODE == E_STORE) epilogue_store<WM, WN, FM, FN, 2 * BUF, (bool)MF16>(g, Cb, acc, lds, m0, n0);
 }
 
 template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0>
@@ -625,13 +586,9 @@ static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
 
 // k-tile depth.  Measured on MI355X (same device, interleaved A/B): BK = 16
 // (3 blocks per CU) is +2.5 % on the long-K, huge-grid cosine GEMM, BK = 32
-// (2 blocks per CU) is +4.8 % on the ResNet convs.  RR_GEMM_BK=16|32 forces.
-static int pick_bk(int emode) {
-  static const int forced = [] {
-    const char* e = getenv("RR_GEMM_BK");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced == 16 || forced == 32) return forced;
+// (2 blocks per CU) is +4.8 % on the ResNet convs.
+static int pick_bk(int emode, const rr_handle_s::Tuning& t) {
+  if (t.gemm_bk == 16 || t.gemm_bk == 32) return t.gemm_bk;
   return emode == E_STORE ? 32 : 16;
 }
 
@@ -639,32 +596,20 @@ static int pick_bk(int emode) {
 // on 256 CUs).  Estimated time ~ rounds x tile area, rounds = ceil(tiles /
 // 512): this charges both the padding of N (e.g. 320 queries on 128-wide
 // tiles) and the last partially-filled round (wave quantization).
-// RR_GEMM_CFG=22|41 forces a config (tuning experiments).
-static bool allow88() {
-  static const bool on = [] {
-    const char* e = getenv("RR_GEMM_NO88");
-    return !(e && atoi(e));
-  }();
-  return on;
-}
-
-static int pick_cfg(const GemmArgs& g, int emode) {
-  static const int forced = [] {
-    const char* e = getenv("RR_GEMM_CFG");
-    return e ? atoi(e) : 0;
-  }();
-  if (forced == 22 || forced == 41 || forced == 88) return forced;
-  const long long slots = pick_bk(emode) == 16 ? 768 : 512;
+static int pick_cfg(const GemmArgs& g, int emode, const rr_handle_s::Tuning& tu) {
+  if (tu.gemm_cfg == 22 || tu.gemm_cfg == 41) return tu.gemm_cfg;
+  if (tu.gemm_cfg == 88) return (emode == E_STORE && pick_bk(emode, tu) == 32) ? 88 : 22;
+  const long long slots = pick_bk(emode, tu) == 16 ? 768 : 512;
   const long long t22 = ((g.M + 127) / 128) * ((g.N + 127) / 128);
   const long long t41 = ((g.M + 255) / 256) * ((g.N + 63) / 64);
   const long long c22 = ((t22 + slots - 1) / slots) * 128 * 128;
   const long long c41 = ((t41 + slots - 1) / slots) * 256 * 64;
-  // 88 (256x256, 1 block/CU) measured per R101 layer (tools/conv_cfg_cmp.sh):
-  // +3-7 % on long-K GEMMs without a residual (3x3 256@14, 1024->512/2048),
-  // -5..-30 % on residual epilogues and short K, -40 % when the grid leaves
-  // CUs idle.  So: no residual, K >= 1024, N a multiple of 256, ~a full round.
+  // 88 (256x256, 1 block/CU) measured per R101 layer: +3-7 % on long-K GEMMs
+  // without a residual (3x3 256@14, 1024->512/2048), -5..-30 % on residual
+  // epilogues and short K, -40 % when the grid leaves CUs idle.  So: no
+  // residual, K >= 1024, N a multiple of 256, ~a full round.
   if (emode == E_STORE && g.k_split == 0 && g.residual == nullptr && g.K >= 1024 && (g.N % 256) == 0 &&
-      allow88()) {
+      pick_bk(emode, tu) == 32) {
     const long long t88 = ((g.M + 255) / 256) * (g.N / 256);
     const long long c88 = ((t88 + 255) / 256) * 256 * 256;  // 1 block/CU vs 2 for 22: compare per CU
     if (t88 >= 240 && (double)c88 / 1.05 < (double)std::min(c22, c41) * 2.0) return 88;
@@ -673,15 +618,15 @@ static int pick_cfg(const GemmArgs& g, int emode) {
 }
 
 template <int AM, int EM>
-static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
-  const int cfg = pick_cfg(g, EM);
-  if (pick_bk(EM) == 16) {
+static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s, const rr_handle_s::Tuning& tu) {
+  const int cfg = pick_cfg(g, EM, tu);
+  if (pick_bk(EM, tu) == 16) {
     if (cfg == 41) return launch_t<4, 1, 2, 2, AM, EM, 16, DT_F32, 3>(g, s);
     return launch_t<2, 2, 2, 2, AM, EM, 16, DT_F32, 3>(g, s);
   }
   if (cfg == 41) return launch_t<4, 1, 2, 2, AM, EM, 32, DT_F32, 2>(g, s);
   if constexpr (EM == E_STORE && (AM == A_DENSE || AM == A_CONV)) {
-    // 88: 256x256, 8 waves of 128x64, 1 block per CU (experimental)
+    // 88: 256x256, 8 waves of 128x64, 1 block per CU
     if (cfg == 88) return launch_t<2, 4, 4, 2, AM, EM, 32, DT_F32, 1>(g, s);
   }
   return launch_t<2, 2, 2, 2, AM, EM, 32, DT_F32, 2>(g, s);
@@ -689,26 +634,18 @@ static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s) {
 
 // Low precision (dense A only, 128-B LDS rows).  Configs (waves WMxWN, MFMA
 // tiles per wave FMxFN, blocks per CU):
-//   22: 128x128, 4 waves of 64x64, 2/CU      41: 256x64, 4 waves of 64x64, 2/CU
-//   big: 256x256, 8 waves of 128x64, 1/CU (128 KB LDS) — the large GEMMs
-//   q320: 256x320, 8 waves of 64x160, 1/CU (144 KB) — a 320-query batch in
-//         one tile column: the streamed gallery is read exactly once
-// picked by estimated rounds x tile area (RR_GEMM_LPCFG=22|41|big|q320 forces).
-static int pick_lp(const GemmArgs& g, int emode) {
-  static const int forced = [] {
-    const char* e = getenv("RR_GEMM_LPCFG");
-    if (!e) return 0;
-    if (!strcmp(e, "22")) return 1;
-    if (!strcmp(e, "41")) return 2;
-    if (!strcmp(e, "big")) return 3;
-    if (!strcmp(e, "q320")) return 4;
-    if (!strcmp(e, "big4")) return 5;
-    if (!strcmp(e, "q320r")) return 6;
-    return 0;
-  }();
-  if (forced == 6 && emode == E_STORE) return 3;
-  if (forced == 4 && emode == E_STORE) return 3;
-  if (forced) return forced;
+//   1: 128x128, 4 waves of 64x64, 2/CU      2: 256x64, 4 waves of 64x64, 2/CU
+//   3: 256x256, 8 waves of 128x64, 1/CU (128 KB LDS) — the large GEMMs
+//   4: 256x320, 8 waves of 64x160, 1/CU (144 KB) — a 320-query batch in
+//      one tile column: the streamed gallery is read exactly once (filter
+//      and score sweeps only)
+// picked by estimated rounds x tile area (rr_set_tuning(RR_TUNE_LP_CFG) forces).
+// Not kept: an 8-phase 256x256 pipeline (2-4 % slower on the ViT
+// linears) and the 256x320 tile on a 4-stage 64-B-row LDS-DMA ring (7.59 vs
+// 6.94 ms per C3 sweep).
+static int pick_lp(const GemmArgs& g, int emode, const rr_handle_s::Tuning& tu) {
+  if (tu.lp_cfg >= 1 && tu.lp_cfg <= 3) return tu.lp_cfg;
+  if (tu.lp_cfg == 4) return emode == E_STORE ? 3 : 4;
   // rounds x tile area / relative per-FLOP speed (measured, tools/lp_bench.py:
   // the 8-wave tiles run ViT linears 1.2-1.3x faster than 128x128; the
   // 320-query tile runs the bf16 d=2048 sweep 1.35x faster, but not d=512 or
@@ -722,7 +659,7 @@ static int pick_lp(const GemmArgs& g, int emode) {
   int cfg = 1;
   if (cost(256, 64, 512, 1.0) < best) best = cost(256, 64, 512, 1.0), cfg = 2;
   if (emode == E_STORE && cost(256, 256, 256, 1.25) < best) best = cost(256, 256, 256, 1.25), cfg = 3;
-  // filter sweeps other than the long-K bf16 one (which takes q320 below):
+  // filter sweeps other than the long-K bf16 one (which takes 4 below):
   // the 8-wave 256x256 tile wins at >= 1024 queries (measured at 1280 queries
   // x 1.6 M rows: bf16 d = 512 3.27 -> 2.39 ms, fp8 d = 2048 11.2 -> 8.1 ms
   // per C5 step); at 320 queries the cost model keeps 128x128
@@ -733,57 +670,23 @@ static int pick_lp(const GemmArgs& g, int emode) {
   return cfg;
 }
 
-// bf16 MFMA shape: four 16x16x32 per 32x32 tile (default; measured on MI355X,
-// tools/mf16_cmd.sh: ViT-B/16 linears +4-7 %, 128x128 cosine sweeps +2-5 %)
-// or 32x32x16 (RR_BF16_MF16=0).  The 256x320 sweep tile stays on 32x32x16:
-// its 16x16 fragments spill (180 B/lane).
-static bool bf16_mf16() {
-  static const bool on = [] {
-    const char* e = getenv("RR_BF16_MF16");
-    return e == nullptr || atoi(e) != 0;
-  }();
-  return on;
-}
-
-template <int EM, int DT, int MF16>
-static hipError_t launch_lp_mf(const GemmArgs& g, hipStream_t s) {
+// bf16 runs on four v_mfma_f32_16x16x32_bf16 per 32x32 tile (MF16; measured:
+// ViT-B/16 linears +4-7 %, 128x128 cosine sweeps +2-5 % over 32x32x16), except
+// the 256x320 sweep tile, whose 16x16 fragments spill (180 B/lane).
+template <int EM, int DT>
+static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s::Tuning& tu) {
   constexpr int EPR = DT == DT_BF16 ? 64 : 128;  // elements per 128-B k-tile row
-  int cfg = pick_lp(g, EM);
+  constexpr int MF = DT == DT_BF16 ? 1 : 0;
+  int cfg = pick_lp(g, EM, tu);
   if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles
-  if ((cfg == 5 || cfg == 6) && (g.K % (EPR / 2)) != 0) cfg = 1;
   switch (cfg) {
-    case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF16>(g, s);
-    case 3: return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF16>(g, s);
+    case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF>(g, s);
+    case 3: return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);
     case 4:
       if constexpr (EM != E_STORE) return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0>(g, s);
       return hipErrorInvalidValue;
-    case 5: return launch_t<2, 4, 4, 2, A_DENSE, EM, 16, DT, 1, 2, MF16>(g, s);
-    case 6:
-      // q320 on the 4-stage LDS-DMA ring (64-B rows, three k-tiles in flight;
-      // B staged in 128-row passes, the last one half-issued)
-      if constexpr (EM != E_STORE) return launch_t<4, 2, 2, 5, A_DENSE, EM, 16, DT, 1, 2, 0>(g, s);
-      return hipErrorInvalidValue;
-    default: return launch_t<2, 2, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF16>(g, s);
+    default: return launch_t<2, 2, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF>(g, s);
   }
-}
-
-// RR_GEMM_8P=1: bf16 GEMMs that pick the 256x256 tile run on the 8-phase
-// pipeline of gemm_8p.hip instead
-static bool use_8p() {
-  static const bool on = [] {
-    const char* e = getenv("RR_GEMM_8P");
-    return e != nullptr && atoi(e) != 0;
-  }();
-  return on;
-}
-
-template <int EM, int DT>
-static hipError_t launch_lp(const GemmArgs& g, hipStream_t s) {
-  if constexpr (DT == DT_BF16) {
-    if (use_8p() && pick_lp(g, EM) == 3 && gemm_8p_eligible(g)) return launch_gemm_8p(g, EM, s);
-    if (bf16_mf16()) return launch_lp_mf<EM, DT, 1>(g, s);
-  }
-  return launch_lp_mf<EM, DT, 0>(g, s);
 }
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStream_t s, int timer_cls, int dt) {
@@ -799,13 +702,13 @@ int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStre
     {
       TimedLaunch tl(h, timer_cls, s);
       if (dt == DT_BF16) {
-        if (emode == E_STORE) e = launch_lp<E_STORE, DT_BF16>(g, s);
-        else if (emode == E_SCORES_T) e = launch_lp<E_SCORES_T, DT_BF16>(g, s);
-        else e = launch_lp<E_FILTER, DT_BF16>(g, s);
+        if (emode == E_STORE) e = launch_lp<E_STORE, DT_BF16>(g, s, h->tune);
+        else if (emode == E_SCORES_T) e = launch_lp<E_SCORES_T, DT_BF16>(g, s, h->tune);
+        else e = launch_lp<E_FILTER, DT_BF16>(g, s, h->tune);
       } else {
-        if (emode == E_STORE) e = launch_lp<E_STORE, DT_FP8>(g, s);
-        else if (emode == E_SCORES_T) e = launch_lp<E_SCORES_T, DT_FP8>(g, s);
-        else e = launch_lp<E_FILTER, DT_FP8>(g, s);
+        if (emode == E_STORE) e = launch_lp<E_STORE, DT_FP8>(g, s, h->tune);
+        else if (emode == E_SCORES_T) e = launch_lp<E_SCORES_T, DT_FP8>(g, s, h->tune);
+        else e = launch_lp<E_FILTER, DT_FP8>(g, s, h->tune);
       }
     }
     return check_hip(h, e, "gemm launch");
@@ -822,12 +725,12 @@ int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStre
   hipError_t e = hipSuccess;
   {
     TimedLaunch tl(h, timer_cls, s);
-    if (amode == A_DENSE && emode == E_STORE) e = launch_cfg<A_DENSE, E_STORE>(g, s);
-    else if (amode == A_DENSE && emode == E_SCORES_T) e = launch_cfg<A_DENSE, E_SCORES_T>(g, s);
-    else if (amode == A_DENSE && emode == E_FILTER) e = launch_cfg<A_DENSE, E_FILTER>(g, s);
-    else if (amode == A_CONV && emode == E_STORE) e = launch_cfg<A_CONV, E_STORE>(g, s);
-    else if (amode == A_CONV_GENERIC && emode == E_STORE) e = launch_cfg<A_CONV_GENERIC, E_STORE>(g, s);
-    else if (amode == A_CONV_C4 && emode == E_STORE) e = launch_cfg<A_CONV_C4, E_STORE>(g, s);
+    if (amode == A_DENSE && emode == E_STORE) e = launch_cfg<A_DENSE, E_STORE>(g, s, h->tune);
+    else if (amode == A_DENSE && emode == E_SCORES_T) e = launch_cfg<A_DENSE, E_SCORES_T>(g, s, h->tune);
+    else if (amode == A_DENSE && emode == E_FILTER) e = launch_cfg<A_DENSE, E_FILTER>(g, s, h->tune);
+    else if (amode == A_CONV && emode == E_STORE) e = launch_cfg<A_CONV, E_STORE>(g, s, h->tune);
+    else if (amode == A_CONV_GENERIC && emode == E_STORE) e = launch_cfg<A_CONV_GENERIC, E_STORE>(g, s, h->tune);
+    else if (amode == A_CONV_C4 && emode == E_STORE) e = launch_cfg<A_CONV_C4, E_STORE>(g, s, h->tune);
     else return set_error(h, RR_EINVAL, "gemm: unsupported mode combination");
   }
   return check_hip(h, e, "gemm launch");

@@ -99,14 +99,14 @@ __device__ __forceinline__ void s3_load1x2(const f32x4* p0, const f32x4* p1, f32
 // reads v can be scheduled above it
 __device__ __forceinline__ void s3_launder(f32x4& v) { asm volatile("" : "+v"(v)); }
 
-// MF16 (BK = 32, SEP): each 32x32 tile is four v_mfma_f32_16x16x32_bf16
+// MF16 (BK = 32): each 32x32 tile is four v_mfma_f32_16x16x32_bf16
 // tiles (one 32-deep k-step per k-tile instead of two 16-deep ones; the
 // 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
 // 'DVFS give-back' item 7).  The k-tile's MFMAs go in two parts around the A
 // split: a0b0 + a1b1 + a0b1 + a1b0 (planes 0-1), then a0b2 + a2b0 (plane 2).
-template <int WM, int WN, int FM, int FN, int BK, int AMODE, int SEP, int MINB, int PIPE, int MF16 = 0>
+template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
-  static_assert(!MF16 || (BK == 32 && SEP), "MF16: BK 32, separate small-term accumulator");
+  static_assert(!MF16 || BK == 32, "MF16: BK 32");
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int WTM = 32 * FM, WTN = 32 * FN;
   constexpr int BM = WTM * WM, BN = WTN * WN;
@@ -190,14 +190,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         // loaded registers are used as they are, no select after the load
         // (a select right after it makes hipcc wait for the load at once)
         const f32x4* p = a_ok[i] ? reinterpret_cast<const f32x4*>(a_ptr[i] + k0) : s3_zero_page();
-        s3_load2<PIPE>(p, ra[i]);
+        s3_load2<1>(p, ra[i]);
       }
     } else if constexpr (AMODE == A_CONV_C4) {
-      // NHWC4 stem (RGB + a zero channel): a k-tile is 8 filter taps of 4
-      // channels, a thread's 8-k chunk the taps 8kt + 2 slot + {0, 1}, one
-      // 16-B load each; taps past KH*KW (K padded to a multiple of 32) and
+      // NHWC4 stem (RGB + a zero channel): a k-tile is BK/4 filter taps of 4
+      // channels, a thread's 8-k chunk the taps (BK/4) kt + 2 slot + {0, 1},
+      // one 16-B load each; taps past KH*KW (K padded to a multiple of 32) and
       // padding pixels read the zero page
-      const int tb = kt * 8, khb = tb / g.KW, kwb = tb - khb * g.KW;
+      const int tb = kt * (BK / 4), khb = tb / g.KW, kwb = tb - khb * g.KW;
       const f32x4* p[A_CH][2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
@@ -213,7 +213,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         }
       }
 #pragma unroll
-      for (int i = 0; i < A_CH; ++i) s3_load1x2<PIPE>(p[i][0], p[i][1], ra[i]);
+      for (int i = 0; i < A_CH; ++i) s3_load1x2<1>(p[i][0], p[i][1], ra[i]);
     } else {
       // Cin % 32 == 0: the whole k-tile lies in one (kh, kw) filter tap
       tap_to(kt);
@@ -224,7 +224,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         const int ih = a_ih0[i] + kh, iw = a_iw0[i] + kw;
         const bool ok = a_ok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
         const f32x4* p = ok ? reinterpret_cast<const f32x4*>(a_ptr[i] + toff) : s3_zero_page();
-        s3_load2<PIPE>(p, ra[i]);
+        s3_load2<1>(p, ra[i]);
       }
     }
   };
@@ -232,17 +232,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   u32x4 pk[A_CH][3];
   auto split_a = [&](int rb) {
     const f32x4(&ra)[A_CH][2] = ra2[rb];
-#ifdef RR_S3_ABLATE_SPLIT
-    // ablation build only (tools/build_variant.sh): no split VALU, wrong
-    // results; measured the split's cost at 7 % of the trunk (3x3: 13 %)
-#pragma unroll
-    for (int i = 0; i < A_CH; ++i) {
-      pk[i][0] = __builtin_bit_cast(u32x4, ra[i][0]);
-      pk[i][1] = __builtin_bit_cast(u32x4, ra[i][1]);
-      pk[i][2] = __builtin_bit_cast(u32x4, ra[i][0]);
-    }
-    return;
-#endif
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       uint32_t h[8], m[8], l[8];
@@ -307,7 +296,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   };
 
   f32x16 hi[FM][FN];
-  f32x16 lo[SEP ? FM : 1][SEP ? FN : 1];
+  f32x16 lo[FM][FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -315,7 +304,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         hi[i][j][r] = 0.f;
-        if constexpr (SEP) lo[i][j][r] = 0.f;
+        lo[i][j][r] = 0.f;
       }
 
   auto compute_st = [&](int cur, int st) {
@@ -344,7 +333,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-          f32x16& L = SEP ? lo[SEP ? i : 0][SEP ? j : 0] : hi[i][j];
+          f32x16& L = lo[i][j];
           L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], L, 0, 0, 0);
           L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], L, 0, 0, 0);
           L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], L, 0, 0, 0);
@@ -431,53 +420,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   };
 #undef RR_MF16
 
-  auto compute = [&](int cur) {
-    if constexpr (MF16) {
-      mf_part0(cur);
-      mf_part1(cur);
-    } else {
-#pragma unroll
-      for (int st = 0; st < BK / 16; ++st) compute_st(cur, st);
-    }
-  };
-
   constexpr int A_LD = 2 * A_CH;  // A global loads per tile per thread
-  if constexpr (PIPE == 0) {
-    // Pipelined k-loop, raw barriers, counted vmcnt, plain A loads.
-    // Entering iteration kt: tile kt is in LDS stage kt&1, the fp32 A chunks
-    // of tile kt+1 are in registers (loaded one iteration earlier).  The
-    // iteration splits them (pinned ahead of everything else: hipcc waits
-    // vmcnt(0) at the first use of a plain load's result while an LDS-DMA is
-    // in flight, so that use must come before the next DMA is issued), issues
-    // the B DMA of tile kt+1 and the A loads of tile kt+2 (indices clamped at
-    // the end: the extra copies land in a stage nobody reads), computes tile
-    // kt, writes the split A of tile kt+1 into the other stage, then waits
-    // for everything but the A loads of kt+2 before a raw barrier, so those
-    // stay in flight across it.
-    load_a(0, 0);
-    glds_b(0, 0);
-    store_a(0, 0);
-    load_a(nk > 1 ? 1 : 0, 0);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    for (int kt = 0; kt < nk; ++kt) {
-      const int cur = kt & 1;
-      split_a(0);
-#pragma unroll
-      for (int i = 0; i < A_CH; ++i) asm volatile("" ::"v"(pk[i][0]), "v"(pk[i][1]), "v"(pk[i][2]));
-      __builtin_amdgcn_sched_barrier(0);
-      glds_b(min(kt + 1, nk - 1), cur ^ 1);
-      load_a(min(kt + 2, nk - 1), 0);
-      compute(cur);
-      write_a(cur ^ 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of kt+1 landed
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    }
-  } else {
+  {
     // Pipelined k-loop with asynchronous A loads (s3_load2<1>), two register
     // buffers: A(j) lives in buffer j&1.  Iteration kt issues the B DMA of
     // tile kt+1 and the A loads of tile kt+2 (into the buffer A(kt) left),
@@ -548,7 +492,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         for (int t = 0; t < 4; ++t)
 #pragma unroll
           for (int e = 0; e < 4; ++e) hi[i][j][4 * t + e] = hi4[i][j][t][e] + lo4[i][j][t][e];
-  } else if constexpr (SEP) {
+  } else {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -557,29 +501,15 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   epilogue_store<WM, WN, FM, FN, BUF, (bool)MF16>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
 }
 
-static int s3_pipe();
-static bool s3_mf16();
-
-template <int WM, int WN, int FM, int FN, int BK, int AM, int SEP, int MINB, int MF16 = 0>
+template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0>
 static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  if constexpr (MF16) {
-    if (s3_pipe()) {
-      hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, SEP, MINB, 1, 1>), dim3((unsigned)nblk),
-                         dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
-      return hipGetLastError();
-    }
-  }
-  if (s3_pipe())
-    hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, SEP, MINB, 1>), dim3((unsigned)nblk), dim3(64 * WM * WN),
-                       0, s, g, (int)tiles_n);
-  else
-    hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, SEP, MINB, 0>), dim3((unsigned)nblk), dim3(64 * WM * WN),
-                       0, s, g, (int)tiles_n);
+  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16>), dim3((unsigned)nblk), dim3(64 * WM * WN),
+                     0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
 
@@ -587,60 +517,22 @@ static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
 //   1: 128x128, 4 waves of 64x64, BK 16, 2/CU (48 KB LDS)
 //   2: 128x128, 4 waves of 64x64, BK 32, 1/CU (96 KB)
 //   3: 256x128, 8 waves of 64x64, BK 32, 1/CU (144 KB)
-//   4: 128x256, 8 waves of 64x64, BK 32, 1/CU (144 KB)
+//   4: 128x256, 8 waves of 64x64, BK 32, 1/CU (144 KB), v_mfma_f32_16x16x32_bf16
 //   5: 256x64,  4 waves of 64x64, BK 32, 1/CU (120 KB)
 //   6: 256x64,  4 waves of 64x64, BK 16, 2/CU (60 KB)
-// Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the
-// fastest wherever N >= 128 (1.1-1.3x config 1 per FLOP).  An all-DMA ring
-// variant (A fp32 in LDS split at fragment-read time by an 8x1 wave layout,
-// BK 16, 5-6 stages, 3-4 k-tiles in flight) measured 10-15 % SLOWER than 3 on
-// every layer and was dropped.  So was a one-wave-per-SIMD variant (4 waves,
-// 256x128, each wave 128x64 with two fragment sets in flight and the A split
-// interleaved between MFMAs): 1.16x slower over the trunk (36.3 vs 31.4 ms).
-// RR_S3_CFG=1..6 forces one; RR_S3_SEP=0 accumulates all six terms in one
-// register tile (accuracy experiment: measured LESS accurate than exact fp32,
-// so the default keeps the small terms apart).
-static int s3_forced_cfg() {
-  static const int v = [] {
-    const char* e = getenv("RR_S3_CFG");
-    return e ? atoi(e) : 0;
-  }();
-  return v;
-}
-// RR_S3_PIPE=0 selects the plain-load k-loop (A prefetched one iteration ahead)
-static int s3_pipe() {
-  static const int v = [] {
-    const char* e = getenv("RR_S3_PIPE");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-// 16x16x32 MFMA tiles in config 4 (128x256, 8 waves, 2 per SIMD), used for
-// every layer with N % 256 == 0.  Measured per R101 layer at 320 images
-// (tools/s3mf_cmd.sh, gpurun_out/s3mf): config 4 on 16x16x32 runs every
-// N >= 256 layer 3-14 % faster than the previous pick (mostly config 3) — the
-// 3x3 256@14 layers (x22) 0.372 -> 0.336 ms — so the trunk 31.5 -> 29.5 ms.
-// The same shape is slower in the one-wave-per-SIMD configs 2 and 5 and
-// spills in config 3.  RR_S3_MF16=0 restores the 32x32x16 picks.
-static bool s3_mf16() {
-  static const bool v = [] {
-    const char* e = getenv("RR_S3_MF16");
-    return !(e != nullptr && atoi(e) == 0);
-  }();
-  return v;
-}
-static bool s3_sep() {
-  static const bool v = [] {
-    const char* e = getenv("RR_S3_SEP");
-    return !(e && atoi(e) == 0);
-  }();
-  return v;
-}
-
-static int pick_s3(const GemmArgs& g) {
-  const int f = s3_forced_cfg();
-  if (f >= 1 && f <= 6) return f;
-  if (s3_mf16() && s3_pipe() && (g.N % 256) == 0) return 4;
+// (all others on v_mfma_f32_32x32x16_bf16).  Measured per R101 layer at 320
+// images (tools/s3_bench.py): 3 is the fastest wherever N >= 128 (1.1-1.3x
+// config 1 per FLOP); 4 on 16x16x32 runs every N % 256 == 0 layer 3-14 %
+// faster than 3 (the 16x16 shape holds a higher clock on random operands,
+// MI355X_MICROARCH.md 'DVFS give-back' item 7; the same shape is slower in the
+// one-wave-per-SIMD configs 2 and 5 and spills in 3).  Not kept:
+// an all-DMA ring with the A split at fragment-read time (10-15 % slower), a
+// one-wave-per-SIMD 256x128 variant (1.16x slower), a single accumulator for
+// all six terms (less accurate than exact fp32).  rr_set_tuning(RR_TUNE_S3_CFG)
+// forces a config (tests, tools).
+static int pick_s3(const GemmArgs& g, int forced) {
+  if (forced >= 1 && forced <= 6) return forced;
+  if ((g.N % 256) == 0) return 4;
   // rounds of resident blocks x tile area per CU / relative per-FLOP speed
   auto cost = [&](long long bm, long long bn, long long per_cu, double speed) {
     const long long slots = 256 * per_cu;
@@ -655,18 +547,14 @@ static int pick_s3(const GemmArgs& g) {
 }
 
 template <int AM>
-static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s) {
-  if (!s3_sep()) return launch_s3_t<2, 2, 2, 2, 16, AM, 0, 2>(g, s);
-  const int cfg = pick_s3(g);
-  switch (cfg) {
-    case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1, 1>(g, s);
-    case 3: return launch_s3_t<4, 2, 2, 2, 32, AM, 1, 1>(g, s);
-    case 4:
-      if (s3_mf16()) return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1, 1>(g, s);
-      return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1>(g, s);
-    case 5: return launch_s3_t<4, 1, 2, 2, 32, AM, 1, 1>(g, s);
-    case 6: return launch_s3_t<4, 1, 2, 2, 16, AM, 1, 2>(g, s);
-    default: return launch_s3_t<2, 2, 2, 2, 16, AM, 1, 2>(g, s);
+static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced) {
+  switch (pick_s3(g, forced)) {
+    case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1>(g, s);
+    case 3: return launch_s3_t<4, 2, 2, 2, 32, AM, 1>(g, s);
+    case 4: return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1>(g, s);
+    case 5: return launch_s3_t<4, 1, 2, 2, 32, AM, 1>(g, s);
+    case 6: return launch_s3_t<4, 1, 2, 2, 16, AM, 2>(g, s);
+    default: return launch_s3_t<2, 2, 2, 2, 16, AM, 2>(g, s);
   }
 }
 
@@ -686,9 +574,10 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
   hipError_t e;
   {
     TimedLaunch tl(h, timer_cls, s);
-    e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s)
-        : amode == A_CONV ? launch_s3_am<A_CONV>(g, s)
-                          : launch_s3_am<A_CONV_C4>(g, s);
+    const int f = h->tune.s3_cfg;
+    e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s, f)
+        : amode == A_CONV ? launch_s3_am<A_CONV>(g, s, f)
+                          : launch_s3_am<A_CONV_C4>(g, s, f);
   }
   return check_hip(h, e, "gemm_s3 launch");
 }

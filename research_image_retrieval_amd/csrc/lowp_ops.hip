@@ -57,7 +57,7 @@ using namespace rr;
 
 extern "C" int rr_quantize_rows(rr_handle_t h, const float* x, long long rows, int d, int dtype, void* y,
                                 float* row_scale, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !y || rows < 0 || d <= 0 || (d & 3) || (dtype != DT_BF16 && dtype != DT_FP8) ||
       ((uintptr_t)x & 15) || (dtype == DT_FP8 && !row_scale))
     return set_error(h, RR_EINVAL, "rr_quantize_rows: bad argument (d % 4 == 0, dtype 1|2, fp8 needs row_scale)");

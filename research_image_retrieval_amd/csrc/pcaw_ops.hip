@@ -122,7 +122,7 @@ extern "C" size_t rr_pcaw_gram_workspace_size(long long n, int d) {
 
 extern "C" int rr_pcaw_gram(rr_handle_t h, const float* x, long long n, int d, void* workspace,
                             size_t workspace_bytes, double* mean_out, double* gram_out, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || n <= 0 || d <= 0 || !mean_out || !gram_out || !workspace)
     return set_error(h, RR_EINVAL, "rr_pcaw_gram: bad argument (n > 0, d > 0, non-null buffers)");
   if (d > 65535 * 64) return set_error(h, RR_EINVAL, "rr_pcaw_gram: d too large");

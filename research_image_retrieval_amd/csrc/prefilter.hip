@@ -161,7 +161,7 @@ extern "C" {
 
 int rr_prefilter_gallery_bound(rr_handle_t h, const float* gallery, const void* gallery_bf16, long long n, int d,
                                double* bound3, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (n < 0 || d <= 0 || !bound3 || (n > 0 && (!gallery || !gallery_bf16)))
     return set_error(h, RR_EINVAL, "rr_prefilter_gallery_bound: bad argument");
   hipStream_t s = (hipStream_t)stream;
@@ -183,7 +183,7 @@ int rr_cosine_topk_prefilter(rr_handle_t h, const float* queries, int nq, const 
                              const void* gallery_bf16, const double* bound3, long long n, int d, int k,
                              long long idx_offset, float* out_scores, long long* out_idx, void* workspace,
                              size_t workspace_bytes, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (nq < 0 || n < 0 || d <= 0 || (d & 7) || k < 1 || k > 16384)
     return set_error(h, RR_EINVAL, "rr_cosine_topk_prefilter: need nq,n >= 0, d % 8 == 0, 1 <= k <= 16384");
   if (n >= 0xffffffffLL) return set_error(h, RR_EINVAL, "rr_cosine_topk_prefilter: shard must have < 2^32 rows");

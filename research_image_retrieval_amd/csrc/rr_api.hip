@@ -1,6 +1,7 @@
 // rr_api.hip — C-ABI entry points of librr (see include/rr.h).
 #include <algorithm>
 #include <cstring>
+#include <initializer_list>
 
 #include "rr_internal.hpp"
 
@@ -77,14 +78,14 @@ int rr_create(int device, rr_handle_t* out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return RR_EHIP;
   rr_handle_s* h = new (std::nothrow) rr_handle_s();
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   h->device = device;
   *out = h;
   return RR_OK;
 }
 
 int rr_destroy(rr_handle_t h) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   for (int c = 0; c < rr_handle_s::kClasses; ++c)
     for (int i = 0; i < rr_handle_s::kMaxEv; ++i) {
       if (h->ev_start[c][i]) (void)hipEventDestroy(h->ev_start[c][i]);
@@ -97,7 +98,7 @@ int rr_destroy(rr_handle_t h) {
 const char* rr_last_error(rr_handle_t h) { return h ? h->last_error.c_str() : "null handle"; }
 
 int rr_timing_enable(rr_handle_t h, int enable) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   h->timing = enable != 0;
   for (int c = 0; c < rr_handle_s::kClasses; ++c) {
     h->n_ev[c] = 0;
@@ -107,8 +108,45 @@ int rr_timing_enable(rr_handle_t h, int enable) {
   return RR_OK;
 }
 
+int rr_get_device(rr_handle_t h, int* device) {
+  if (!h || !device) return RR_EINVAL;
+  *device = h->device;
+  return RR_OK;
+}
+
+int rr_set_tuning(rr_handle_t h, int key, int value) {
+  if (!h) return RR_EINVAL;
+  auto in = [&](std::initializer_list<int> ok) {
+    for (int v : ok)
+      if (v == value) return true;
+    return false;
+  };
+  switch (key) {
+    case RR_TUNE_GEMM_CFG:
+      if (!in({0, 22, 41, 88})) break;
+      h->tune.gemm_cfg = value;
+      return RR_OK;
+    case RR_TUNE_GEMM_BK:
+      if (!in({0, 16, 32})) break;
+      h->tune.gemm_bk = value;
+      return RR_OK;
+    case RR_TUNE_LP_CFG:
+      if (value < 0 || value > 4) break;
+      h->tune.lp_cfg = value;
+      return RR_OK;
+    case RR_TUNE_S3_CFG:
+      if (value < 0 || value > 6) break;
+      h->tune.s3_cfg = value;
+      return RR_OK;
+    default:
+      return set_error(h, RR_EINVAL, "rr_set_tuning: unknown key");
+  }
+  return set_error(h, RR_EINVAL, "rr_set_tuning: value out of range for this key");
+}
+
 int rr_timing_collect(rr_handle_t h, int cls, double* ms, long long* launches) {
   if (!h || cls < 0 || cls >= rr_handle_s::kClasses) return RR_EINVAL;
+  DeviceGuard dg(h);
   for (int i = 0; i < h->n_ev[cls]; ++i) {
     if (int rc = check_hip(h, hipEventSynchronize(h->ev_stop[cls][i]), "timing sync")) return rc;
     float t = 0.f;
@@ -210,7 +248,7 @@ extern "C" {
 int rr_cosine_topk(rr_handle_t h, const float* queries, int nq, const float* gallery, long long n, int d, int k,
                    long long idx_offset, float* out_scores, long long* out_idx, void* workspace,
                    size_t workspace_bytes, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   return cosine_topk_impl(h, queries, nullptr, nq, gallery, nullptr, n, d, k, idx_offset, out_scores, out_idx,
                           workspace, workspace_bytes, (hipStream_t)stream, DT_F32);
 }
@@ -219,7 +257,7 @@ int rr_cosine_topk_lp(rr_handle_t h, const void* queries, const float* q_scale, 
                       const float* g_scale, long long n, int d, int dtype, int k, long long idx_offset,
                       float* out_scores, long long* out_idx, void* workspace, size_t workspace_bytes,
                       void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (dtype != DT_BF16 && dtype != DT_FP8) return set_error(h, RR_EINVAL, "rr_cosine_topk_lp: dtype must be 1 or 2");
   if (dtype == DT_FP8 && (!q_scale || !g_scale))
     return set_error(h, RR_EINVAL, "rr_cosine_topk_lp: fp8 needs per-row scales");
@@ -231,7 +269,7 @@ int rr_cosine_topk_lp(rr_handle_t h, const void* queries, const float* q_scale, 
 
 int rr_linear_bf16(rr_handle_t h, const void* x, int m, int k, const void* w, const float* bias, int n,
                    const float* residual, int act, int out_bf16, void* y, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !w || !y || m < 0 || k <= 0 || n <= 0 || (k & 7) || act < 0 || act > 2)
     return set_error(h, RR_EINVAL, "rr_linear_bf16: bad argument (k % 8 == 0)");
   if (((uintptr_t)x & 15) || ((uintptr_t)w & 15)) return set_error(h, RR_EINVAL, "rr_linear_bf16: 16-B alignment");
@@ -254,7 +292,7 @@ int rr_linear_bf16(rr_handle_t h, const void* x, int m, int k, const void* w, co
 
 int rr_cosine_scores(rr_handle_t h, const float* queries, int nq, const float* gallery, long long n, int d,
                      float* scores, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (nq < 0 || n < 0 || n > 0x7fffffffLL || d <= 0 || (d & 3))
     return set_error(h, RR_EINVAL, "rr_cosine_scores: bad shape");
   if (nq == 0 || n == 0) return RR_OK;
@@ -274,7 +312,7 @@ int rr_cosine_scores(rr_handle_t h, const float* queries, int nq, const float* g
 
 int rr_topk_merge(rr_handle_t h, const float* ps, const long long* pi, int nparts, int nq, int k_in, int k_out,
                   float* os, long long* oi, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!ps || !pi || !os || !oi) return set_error(h, RR_EINVAL, "rr_topk_merge: null pointer");
   return launch_merge(h, ps, pi, nparts, nq, k_in, k_out, os, oi, (hipStream_t)stream);
 }
@@ -282,7 +320,7 @@ int rr_topk_merge(rr_handle_t h, const float* ps, const long long* pi, int npart
 int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, const float* w, const float* bias,
               int cout, int kh, int kw, int stride, int pad, const float* residual, int relu, float* y,
               void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !w || !y || b < 0 || hgt <= 0 || wid <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 ||
       stride <= 0 || pad < 0)
     return set_error(h, RR_EINVAL, "rr_conv2d: bad argument");
@@ -330,7 +368,7 @@ int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, c
 int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, const void* w3,
                  const float* bias, int cout, int kh, int kw, int stride, int pad, const float* residual, int relu,
                  float* y, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !w3 || !y || b < 0 || hgt <= 0 || wid <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 ||
       stride <= 0 || pad < 0 || relu < 0 || relu > 1)
     return set_error(h, RR_EINVAL, "rr_conv2d_s3: bad argument");
@@ -371,7 +409,7 @@ int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin
 
 int rr_linear_s3(rr_handle_t h, const float* x, int m, int k, const void* w3, const float* bias, int n,
                  const float* residual, int act, float* y, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !w3 || !y || m < 0 || k <= 0 || n <= 0 || act < 0 || act > 2) return set_error(h, RR_EINVAL, "rr_linear_s3: bad argument");
   if (k % 32) return set_error(h, RR_EINVAL, "rr_linear_s3: k must be a multiple of 32");
   GemmArgs g;
@@ -392,7 +430,7 @@ int rr_linear_s3(rr_handle_t h, const float* x, int m, int k, const void* w3, co
 }
 
 int rr_split3_bf16(rr_handle_t h, const float* x, long long n, void* planes, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !planes || n < 0) return set_error(h, RR_EINVAL, "rr_split3_bf16: bad argument");
   TimedLaunch tl(h, kTimeElem, (hipStream_t)stream);
   return launch_split3(h, x, n, reinterpret_cast<uint16_t*>(planes), (hipStream_t)stream);
@@ -405,7 +443,7 @@ int rr_linear(rr_handle_t h, const float* x, int m, int k, const float* w, const
 
 int rr_linear_ex(rr_handle_t h, const float* x, int m, int k, const float* w, const float* bias, int n,
                  const float* residual, int act, float* y, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !w || !y || m < 0 || k <= 0 || n <= 0 || (k & 3)) return set_error(h, RR_EINVAL, "rr_linear: bad argument");
   if (((uintptr_t)x & 15) || ((uintptr_t)w & 15)) return set_error(h, RR_EINVAL, "rr_linear: x/w must be 16-byte aligned");
   GemmArgs g;

@@ -10,6 +10,14 @@
 struct rr_handle_s {
   int device = 0;
   std::string last_error;
+  // kernel-config overrides (rr_set_tuning; 0 = the built-in pick): tests
+  // and tools force each tile config through these, the product path never does
+  struct Tuning {
+    int gemm_cfg = 0;  // fp32 core: 22, 41 or 88
+    int gemm_bk = 0;   // fp32 core k-tile depth: 16 or 32
+    int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps)
+    int s3_cfg = 0;    // split-bf16 core: 1..6 (gemm_s3.hip)
+  } tune;
   // timing (see rr_timing_enable)
   bool timing = false;
   static constexpr int kClasses = 6;
@@ -26,6 +34,36 @@ struct rr_handle_s {
 };
 
 namespace rr {
+
+// Every C-ABI entry runs on its handle's device (rr.h: one handle per
+// device): the calling thread's current device is switched for the call and
+// restored afterwards, so a NULL-stream launch, a memset or an event of a
+// handle created for device d always lands on d.
+struct DeviceGuard {
+  int prev = -1;
+  int rc = 0;
+  explicit DeviceGuard(const rr_handle_s* h) {
+    int cur = -1;
+    if (hipGetDevice(&cur) != hipSuccess) {
+      rc = RR_EHIP;
+      return;
+    }
+    if (cur != h->device) {
+      if (hipSetDevice(h->device) != hipSuccess) {
+        rc = RR_EHIP;
+        return;
+      }
+      prev = cur;
+    }
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+#define RR_ENTRY(h)                                                                 \
+  if (!(h)) return RR_EINVAL;                                                       \
+  rr::DeviceGuard rr_device_guard_(h);                                              \
+  if (rr_device_guard_.rc) return rr::set_error(h, rr_device_guard_.rc, "cannot select the handle's device")
 
 enum TimerClass { kTimeCosine = 0, kTimeGemm = 1, kTimeSelect = 2, kTimeElem = 3, kTimeCosineSeed = 4, kTimeAttn = 5 };
 
@@ -133,11 +171,6 @@ struct GemmArgs {
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,
                 int dt = DT_F32);
-
-// bf16 GEMM on the 256x256 8-phase LDS-DMA pipeline (gemm_8p.hip): dense A/B,
-// K % 128 == 0, no split-K / scales
-bool gemm_8p_eligible(const GemmArgs& g);
-hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s);
 
 // fp32-accurate GEMM on bf16 MFMA (gemm_s3.hip): A fp32 (A_DENSE or A_CONV),
 // B = bf16 planes [3][N][ldb] from launch_split3, E_STORE epilogue

@@ -524,7 +524,7 @@ extern "C" int rr_layernorm(rr_handle_t h, const float* x, long long ldx, int m,
 
 extern "C" int rr_layernorm_ex(rr_handle_t h, const float* x, long long ldx, int m, int d, const float* gamma,
                                const float* beta, float eps, int out_dtype, void* y, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !y || !gamma || !beta || m < 0 || d <= 0 || d > 4096 || ldx < d || (out_dtype != 0 && out_dtype != 1))
     return set_error(h, RR_EINVAL, "rr_layernorm: bad argument (d <= 4096, ldx >= d, out_dtype 0|1)");
   if (m == 0) return RR_OK;
@@ -541,7 +541,7 @@ extern "C" int rr_layernorm_ex(rr_handle_t h, const float* x, long long ldx, int
 
 extern "C" int rr_patchify(rr_handle_t h, const float* x, int b, int hgt, int wid, int c, int patch, float* y,
                            void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!x || !y || b < 0 || c <= 0 || patch <= 0 || hgt % patch || wid % patch)
     return set_error(h, RR_EINVAL, "rr_patchify: bad argument (H, W must be multiples of the patch)");
   const long long total = (long long)b * hgt * wid * c;
@@ -554,7 +554,7 @@ extern "C" int rr_patchify(rr_handle_t h, const float* x, int b, int hgt, int wi
 
 extern "C" int rr_vit_tokens(rr_handle_t h, const float* patches, int b, int npatch, int width, const float* cls,
                              const float* pos, float* y, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!patches || !cls || !pos || !y || b < 0 || npatch <= 0 || width <= 0)
     return set_error(h, RR_EINVAL, "rr_vit_tokens: bad argument");
   const long long total = (long long)b * (npatch + 1) * width;
@@ -573,7 +573,7 @@ extern "C" int rr_attention(rr_handle_t h, const float* qkv, int b, int seq, int
 
 extern "C" int rr_attention_ex(rr_handle_t h, const float* qkv, int b, int seq, int heads, int head_dim,
                                int out_dtype, void* out, void* stream) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!qkv || !out || b < 0 || heads <= 0 || head_dim != 64 || seq <= 0 || seq > 256 ||
       (out_dtype != 0 && out_dtype != 1))
     return set_error(h, RR_EINVAL, "rr_attention: supports head_dim == 64, 1 <= seq <= 256, out_dtype 0|1");
@@ -588,7 +588,7 @@ extern "C" int rr_attention_ex(rr_handle_t h, const float* qkv, int b, int seq, 
 
 static int attention_bf16_any(rr_handle_t h, const void* qkv, int qkv_bf16, int b, int seq, int heads, int head_dim,
                               int out_dtype, void* out, void* stream, const char* what) {
-  if (!h) return RR_EINVAL;
+  RR_ENTRY(h);
   if (!qkv || !out || b < 0 || heads <= 0 || head_dim != 64 || seq <= 0 || seq > 256 ||
       (out_dtype != 0 && out_dtype != 1))
     return set_error(h, RR_EINVAL, std::string(what) + ": supports head_dim == 64, 1 <= seq <= 256, out_dtype 0|1");

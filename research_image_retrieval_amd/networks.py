@@ -25,14 +25,22 @@ class ResNet:
     conv_math: "s3" (default) runs every conv with Cin % 32 == 0 on the
     split-bf16 core (fp32-accurate, weights split once here); "f32" keeps all
     convs on the exact-fp32 MFMA core.  The stem runs on the split-bf16 core
-    too (NHWC4 taps, K padded to 224) unless conv_math == "f32"."""
+    too (NHWC4 taps, K padded to 224) unless conv_math == "f32".
+
+    stride_on: "3x3" (default) = torchvision v1.5 bottlenecks; "1x1" = the
+    reference's own torchvision-free R101, ResNet_DOLG
+    (networks/backbone.py:218-274, BottleneckTransform :305-325: the stride of
+    a stage's first block sits on the 1x1 `a` conv).  A ResNet_DOLG state dict
+    (stem.*, s{K}.b{M}.*) is accepted as is (weights.to_torchvision_keys)."""
 
     outputdim_block5 = 2048
     outputdim_block4 = 1024
 
-    def __init__(self, name="resnet101", state_dict=None, seed=0, device="cuda", conv_math="s3"):
+    def __init__(self, name="resnet101", state_dict=None, seed=0, device="cuda", conv_math="s3", stride_on="3x3"):
         if conv_math not in ("s3", "f32"):
             raise ValueError("conv_math must be 's3' or 'f32'")
+        W.block_strides(1, stride_on)  # validates
+        self.stride_on = stride_on
         if name not in W.RESNET_LAYERS:
             raise ValueError(f"Unsupported or unknown architecture: {name}!")
         self.name = name
@@ -60,21 +68,26 @@ class ResNet:
             return ops.conv2d_s3(x, w3, b, stride, pad, residual, relu)
         return ops.conv2d(x, w, b, stride, pad, residual, relu)
 
-    def forward(self, x):
-        """x: NHWC fp32 with 3 channels or 4 (zero 4th channel, preferred)."""
+    def forward(self, x, return_x3=False):
+        """x: NHWC fp32 with 3 channels or 4 (zero 4th channel, preferred).
+        return_x3: also return layer3's output, as ResNet_DOLG.forward's
+        (x3, x4) (networks/backbone.py:236-242)."""
         if x.shape[-1] == 3:
             x = torch.nn.functional.pad(x, (0, 1))
         x = self._conv(x, "conv1", 2, 3, True)
         x = ops.maxpool2d(x, 3, 2, 1)
+        x3 = None
         for li, nb in enumerate(self.layers):
             for bi in range(nb):
                 p = f"layer{li + 1}.{bi}"
-                s = 2 if (bi == 0 and li > 0) else 1  # torchvision v1.5: stride on the 3x3
-                idn = self._conv(x, f"{p}.downsample.0", s, 0, False) if bi == 0 else x
-                y = self._conv(x, f"{p}.conv1", 1, 0, True)
-                y = self._conv(y, f"{p}.conv2", s, 1, True)
+                s1, s2 = W.block_strides(2 if (bi == 0 and li > 0) else 1, self.stride_on)
+                idn = self._conv(x, f"{p}.downsample.0", s1 * s2, 0, False) if bi == 0 else x
+                y = self._conv(x, f"{p}.conv1", s1, 0, True)
+                y = self._conv(y, f"{p}.conv2", s2, 1, True)
                 x = self._conv(y, f"{p}.conv3", 1, 0, True, residual=idn)
-        return x
+            if li == 2:
+                x3 = x
+        return (x3, x) if return_x3 else x
 
     __call__ = forward
 

@@ -303,6 +303,34 @@ def topk_merge(part_scores, part_idx, k_out):
     return os_, oi
 
 
+_TUNE_KEYS = {"gemm_cfg": _lib.TUNE_GEMM_CFG, "gemm_bk": _lib.TUNE_GEMM_BK, "lp_cfg": _lib.TUNE_LP_CFG,
+              "s3_cfg": _lib.TUNE_S3_CFG}
+
+
+class tuning:
+    """Force kernel tile configs on a device's handle for the duration of a
+    ``with`` block (rr_set_tuning; tests and tuning tools only):
+    ``with ops.tuning(0, s3_cfg=6): ...``.  Values revert to 0 (the library's
+    own pick) on exit."""
+
+    def __init__(self, device_index, **kw):
+        for k in kw:
+            if k not in _TUNE_KEYS:
+                raise ValueError(f"unknown tuning key {k!r}")
+        self.h = _lib.handle(device_index)
+        self.kw = kw
+
+    def __enter__(self):
+        for k, v in self.kw.items():
+            _lib.check(_lib.lib().rr_set_tuning(self.h, _TUNE_KEYS[k], int(v)), self.h, "rr_set_tuning")
+        return self
+
+    def __exit__(self, *exc):
+        for k in self.kw:
+            _lib.lib().rr_set_tuning(self.h, _TUNE_KEYS[k], 0)
+        return False
+
+
 class KernelTimer:
     """HIP-event timing of librr kernel classes on their launch stream."""
 

@@ -17,6 +17,17 @@ import torch
 # torchvision.models.resnet50/101; models/gem_pooling.py:34-38)
 RESNET_LAYERS = {"resnet50": (3, 4, 6, 3), "resnet101": (3, 4, 23, 3), "resnet152": (3, 8, 36, 3)}
 BN_EPS = 1e-5
+# Where a downsampling bottleneck puts its stride: "3x3" = torchvision v1.5
+# (conv2), "1x1" = MSRA / pycls, the reference's own torchvision-free R101
+# (networks/backbone.py:310-312: BottleneckTransform.a carries the stride).
+STRIDE_ON = ("3x3", "1x1")
+
+
+def block_strides(stride, stride_on):
+    """(conv1 stride, conv2 stride) of a bottleneck whose block stride is `stride`."""
+    if stride_on not in STRIDE_ON:
+        raise ValueError(f"stride_on must be one of {STRIDE_ON}")
+    return (1, stride) if stride_on == "3x3" else (stride, 1)
 
 
 def resnet_conv_specs(arch):
@@ -74,6 +85,44 @@ def synthetic_linear(out_dim, in_dim, seed, bias=True, scale=None):
 # GeMModel (models/gem_pooling.py:44) keeps nn.Sequential indices 0..7.
 _SEQ_TO_TV = {"0": "conv1", "1": "bn1", "4": "layer1", "5": "layer2", "6": "layer3", "7": "layer4"}
 _BLOCK_TO_TV = {"block2": "layer1", "block3": "layer2", "block4": "layer3", "block5": "layer4"}
+# ResNet_DOLG (networks/backbone.py:218-274, blocks :305-345): stem.{conv,bn},
+# s{K}.b{M}.{proj,bn} (projection shortcut), s{K}.b{M}.f.{a,a_bn,b,b_bn,c,c_bn}
+_DOLG_F_TO_TV = {"a": "conv1", "a_bn": "bn1", "b": "conv2", "b_bn": "bn2", "c": "conv3", "c_bn": "bn3"}
+_DOLG_SC_TO_TV = {"proj": "downsample.0", "bn": "downsample.1"}
+
+
+def _dolg_to_tv(parts):
+    if parts[0] == "stem" and len(parts) >= 3:
+        return [{"conv": "conv1", "bn": "bn1"}.get(parts[1], "?")] + parts[2:]
+    if len(parts) >= 4 and parts[0][:1] == "s" and parts[0][1:].isdigit() and parts[1][:1] == "b":
+        layer = f"layer{int(parts[0][1:])}"
+        blk = str(int(parts[1][1:]) - 1)
+        if parts[2] == "f" and len(parts) >= 5 and parts[3] in _DOLG_F_TO_TV:
+            return [layer, blk, _DOLG_F_TO_TV[parts[3]]] + parts[4:]
+        if parts[2] in _DOLG_SC_TO_TV:
+            return [layer, blk, _DOLG_SC_TO_TV[parts[2]]] + parts[3:]
+    return None
+
+
+def to_dolg_keys(sd):
+    """torchvision trunk keys -> ResNet_DOLG keys (the inverse of the DOLG
+    branch of to_torchvision_keys); used to load seeded weights into the
+    reference's own R101 when generating the trunk fixture."""
+    inv_f = {v: k for k, v in _DOLG_F_TO_TV.items()}
+    out = collections.OrderedDict()
+    for k, v in sd.items():
+        parts = k.split(".")
+        if parts[0] in ("conv1", "bn1"):
+            nk = ["stem", {"conv1": "conv", "bn1": "bn"}[parts[0]]] + parts[1:]
+        else:
+            li, bi = int(parts[0][5:]), int(parts[1])
+            head = [f"s{li}", f"b{bi + 1}"]
+            if parts[2] == "downsample":
+                nk = head + [{"0": "proj", "1": "bn"}[parts[3]]] + parts[4:]
+            else:
+                nk = head + ["f", inv_f[parts[2]]] + parts[3:]
+        out[".".join(nk)] = v
+    return out
 
 
 def to_torchvision_keys(sd, prefix=""):
@@ -81,8 +130,11 @@ def to_torchvision_keys(sd, prefix=""):
 
     Accepts plain torchvision keys, networks-style ``backbone.block{1..5}.*``
     (e.g. ``globalmodel.backbone.block1.0.weight`` saved by the reference's
-    load_checkpoint, utils/helpfunc.py:342-368) and Table-1
-    ``backbone.backbone.{0..7}.*`` keys.  Non-trunk keys are dropped."""
+    load_checkpoint, utils/helpfunc.py:342-368), Table-1
+    ``backbone.backbone.{0..7}.*`` keys and ResNet_DOLG keys
+    (``stem.conv``, ``s3.b7.f.b_bn``, ``s1.b1.proj``; networks/backbone.py:218-345,
+    whose bottlenecks carry the stride on the 1x1: build the trunk with
+    stride_on="1x1").  Non-trunk keys are dropped."""
     out = collections.OrderedDict()
     for k, v in sd.items():
         if prefix and not k.startswith(prefix):
@@ -92,7 +144,10 @@ def to_torchvision_keys(sd, prefix=""):
             if k2.startswith(lead):
                 k2 = k2[len(lead):]
         parts = k2.split(".")
-        if parts[0] == "block1" and len(parts) >= 3:
+        dolg = _dolg_to_tv(parts)
+        if dolg is not None:
+            parts = dolg
+        elif parts[0] == "block1" and len(parts) >= 3:
             parts = [{"0": "conv1", "1": "bn1"}.get(parts[1], "?")] + parts[2:]
         elif parts[0] in _BLOCK_TO_TV:
             parts = [_BLOCK_TO_TV[parts[0]]] + parts[1:]
@@ -146,7 +201,7 @@ def folded_resnet(sd, arch):
     return out
 
 
-def resnet_conv_flops(arch, h, w):
+def resnet_conv_flops(arch, h, w, stride_on="3x3"):
     """Algorithmic FLOPs (2*M*N*K) of every trunk conv for one h x w image,
     following networks.ResNet.forward's strides/pads."""
     def out(x, k, s, p):
@@ -161,11 +216,13 @@ def resnet_conv_flops(arch, h, w):
         planes = 64 * 2 ** li
         for bi in range(nb):
             s = 2 if (bi == 0 and li > 0) else 1
+            s1, s2 = block_strides(s, stride_on)
             p = f"layer{li + 1}.{bi}"
-            Ho, Wo = out(H, 3, s, 1), out(Wd, 3, s, 1)
+            H1, W1 = out(H, 1, s1, 0), out(Wd, 1, s1, 0)
+            Ho, Wo = out(H1, 3, s2, 1), out(W1, 3, s2, 1)
             if bi == 0:
                 flops[p + ".downsample.0"] = 2 * Ho * Wo * planes * 4 * inplanes
-            flops[p + ".conv1"] = 2 * H * Wd * planes * inplanes
+            flops[p + ".conv1"] = 2 * H1 * W1 * planes * inplanes
             flops[p + ".conv2"] = 2 * Ho * Wo * planes * planes * 9
             flops[p + ".conv3"] = 2 * Ho * Wo * planes * 4 * planes
             H, Wd, inplanes = Ho, Wo, planes * 4

@@ -116,6 +116,18 @@ def vit_state_dict(seed, width, layers, heads, patch, res, out_dim):
     return sd
 
 
+# ResNet_DOLG trunk fixture (networks/backbone.py:218-274): weight seed and
+# (input seed, batch, H, W) of each case
+TRUNK_WEIGHT_SEED = 81
+TRUNK_CASES = {"b2_224": (82, 2, 224, 224), "b1_odd": (83, 1, 100, 132)}
+
+
+def trunk_input(seed, b, h, w):
+    """Normalised-pixel-like NCHW fp32 input for the trunk fixture."""
+    rs = np.random.RandomState(seed)
+    return torch.from_numpy(rs.standard_normal((b, 3, h, w)).astype(np.float32))
+
+
 def loader_images(seed=61):
     """Deterministic RGB images of assorted sizes and aspect ratios (uint8
     HWC): smooth gradients plus noise, so resampling filters matter."""

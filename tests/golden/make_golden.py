@@ -56,13 +56,43 @@ def loader_fixture():
     np.savez_compressed(os.path.join(HERE, "loader.npz"), seed=61, **out)
 
 
+def trunk_fixture():
+    """(ix) The reference's own torchvision-free ResNet-101, ResNet_DOLG
+    (networks/backbone.py:218-274; ResStemIN :261-274, ResStage :244-259,
+    ResBlock :327-346, BottleneckTransform :305-325), eval mode, with seeded
+    torchvision-keyed weights (non-trivial BN statistics) remapped to its keys.
+    Saves its (x3, x4) outputs: x4 for every case, x3 for the odd-size one."""
+    import torch.nn as nn  # noqa: F401
+    from networks.backbone import ResNet_DOLG
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from research_image_retrieval_amd.weights import synthetic_resnet_state_dict, to_dolg_keys
+    torch.set_num_threads(8)
+    net = ResNet_DOLG()
+    sd = to_dolg_keys(synthetic_resnet_state_dict("resnet101", I.TRUNK_WEIGHT_SEED))
+    net.load_state_dict(sd, strict=True)
+    net.eval()
+    out = {"weight_seed": I.TRUNK_WEIGHT_SEED}
+    with torch.no_grad():
+        for tag, (seed, b, h, w) in I.TRUNK_CASES.items():
+            x3, x4 = net(I.trunk_input(seed, b, h, w))
+            out[tag + "_x4"] = x4.numpy()
+            if tag == "b1_odd":
+                out[tag + "_x3"] = x3.numpy()
+            out[tag + "_case"] = np.array([seed, b, h, w])
+    np.savez_compressed(os.path.join(HERE, "resnet_dolg.npz"), **out)
+
+
 def main():
     _stub_torchvision()
     sys.path.insert(0, REF)
     if "--only-loader" in sys.argv:
         loader_fixture()
         return
+    if "--only-trunk" in sys.argv:
+        trunk_fixture()
+        return
     loader_fixture()
+    trunk_fixture()
     from networks.RetrievalNet import gem, GeM
     from networks.backbone import pcawhitenlearn_shrinkage
     from networks.spca import ConvDimReduction

@@ -37,3 +37,15 @@ def test_no_device_calls_error_cleanly_without_gpu():
     assert L.rr_conv2d(None, None, 0, 0, 0, 0, None, None, 0, 0, 0, 0, 0, None, 0, None, None) == _lib.RR_EINVAL
     assert L.rr_timing_enable(None, 1) == _lib.RR_EINVAL
     assert L.rr_cosine_topk_workspace_size(256, 1_600_000, 2048, 100) >= 256 * (1_600_000 - 32768 + 100) * 8
+
+
+def test_handle_entry_points_without_gpu():
+    """Tuning / device queries reject a null handle; rr_create refuses a device
+    that does not exist (here: any, since this container has no GPU)."""
+    L = _lib.lib()
+    dev = ctypes.c_int(-7)
+    assert L.rr_get_device(None, ctypes.byref(dev)) == _lib.RR_EINVAL and dev.value == -7
+    assert L.rr_set_tuning(None, _lib.TUNE_S3_CFG, 1) == _lib.RR_EINVAL
+    out = ctypes.c_void_p()
+    assert L.rr_create(-1, ctypes.byref(out)) != _lib.RR_OK and not out.value
+    assert L.rr_create(1 << 20, ctypes.byref(out)) != _lib.RR_OK and not out.value

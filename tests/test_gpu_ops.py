@@ -101,3 +101,24 @@ def test_maxpool_scalar_path(cuda):
     x = torch.randn(2, 9, 8, 6)  # C % 4 != 0 -> scalar kernel
     ref = F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
     assert torch.equal(ops.maxpool2d(x.to(cuda), 3, 2, 1).cpu(), ref)
+
+
+def test_handle_device_and_tuning_validation(cuda):
+    """rr_get_device reports the handle's device; rr_set_tuning rejects unknown
+    keys and out-of-range values (RR_EINVAL, message set) and accepts 0."""
+    import ctypes
+    from research_image_retrieval_amd import _lib
+    L, h = _lib.lib(), _lib.handle(cuda.index)
+    d = ctypes.c_int(-1)
+    assert L.rr_get_device(h, ctypes.byref(d)) == 0 and d.value == cuda.index
+    assert L.rr_set_tuning(h, 99, 1) == _lib.RR_EINVAL and b"unknown key" in L.rr_last_error(h)
+    assert L.rr_set_tuning(h, _lib.TUNE_GEMM_CFG, 23) == _lib.RR_EINVAL
+    assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG, 7) == _lib.RR_EINVAL
+    for key in (_lib.TUNE_GEMM_CFG, _lib.TUNE_GEMM_BK, _lib.TUNE_LP_CFG, _lib.TUNE_S3_CFG):
+        assert L.rr_set_tuning(h, key, 0) == 0
+    # a call made while another device is current still runs on the handle's device
+    # (one-GPU box: the guard is exercised with the current device equal to the handle's)
+    torch.cuda.set_device(cuda)
+    x = torch.randn(64, 128, device=cuda)
+    y = ops.l2_normalize(x)
+    assert torch.allclose(y.norm(dim=1), torch.ones(64, device=cuda), atol=1e-6)

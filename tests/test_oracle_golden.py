@@ -150,3 +150,31 @@ def test_oracle_vit_vs_reference(tag):
         out = embed_ref.vit_forward(x, sd, patch, width, layers, heads).numpy()
     ref = fx[tag]
     assert np.abs(out - ref).max() < 1e-4 * max(1.0, np.abs(ref).max())
+
+
+@pytest.mark.parametrize("tag", ["b2_224", "b1_odd"])
+def test_oracle_trunk_vs_reference_resnet_dolg(tag):
+    """The oracle's ResNet-101 trunk with the stride on the 1x1 (stride_on="1x1")
+    against the reference's own torchvision-free R101, ResNet_DOLG
+    (networks/backbone.py:218-274, :305-346), run by make_golden.py with the
+    same seeded weights remapped to its keys."""
+    from research_image_retrieval_amd import weights as W
+    fx = load("resnet_dolg")
+    sd = W.synthetic_resnet_state_dict("resnet101", int(fx["weight_seed"]))
+    seed, b, h, w = (int(v) for v in fx[tag + "_case"])
+    with torch.no_grad():
+        x3, x4 = embed_ref.resnet_trunk(I.trunk_input(seed, b, h, w), sd, W.RESNET_LAYERS["resnet101"],
+                                        stride_on="1x1", return_x3=True)
+    np.testing.assert_allclose(x4.numpy(), fx[tag + "_x4"], rtol=0, atol=1e-6)
+    if tag + "_x3" in fx:
+        np.testing.assert_allclose(x3.numpy(), fx[tag + "_x3"], rtol=0, atol=1e-6)
+
+
+def test_dolg_key_layout_round_trip():
+    """ResNet_DOLG keys (stem.*, s{K}.b{M}.{proj,bn,f.*}) <-> torchvision keys."""
+    from research_image_retrieval_amd import weights as W
+    sd = W.synthetic_resnet_state_dict("resnet101", 1)
+    d = W.to_dolg_keys(sd)
+    assert "stem.conv.weight" in d and "s3.b23.f.c_bn.running_var" in d and "s1.b1.proj.weight" in d
+    t = W.to_torchvision_keys({"globalmodel.backbone." + k: v for k, v in d.items()})
+    assert list(t) == list(sd) and all(torch.equal(t[k], sd[k]) for k in sd)

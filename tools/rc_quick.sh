@@ -1,9 +1,12 @@
+#!/bin/bash
+# Quick GPU check: selected test files (default: the whole -m gpu suite), then smoke.
+# usage: bash tools/rc_quick.sh <tag> [pytest paths...]
 set -o pipefail
-O=gpurun_out/r1f
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+TAG=${1:-quick}; shift
+O=$R/gpurun_out/$TAG
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/gpu_tests.log 2>&1 && \
-timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && \
-timeout -k 10 300 python -u bench.py --no-cpu-baseline > $O/bench_c3.json 2> $O/bench_c3.err && \
-timeout -k 10 300 python -u bench.py --workload c4 --no-cpu-baseline > $O/bench_c4.json 2> $O/bench_c4.err && \
-timeout -k 10 300 python -u bench.py --workload c5 --no-cpu-baseline > $O/bench_c5.json 2> $O/bench_c5.err && \
-echo all-done
+cd $R
+T=${@:-tests}
+timeout -k 10 900 python -u -m pytest $T -m gpu -x -v -s --timeout 240 --timeout-method thread > $O/gpu_tests.log 2>&1 && \
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 && echo all-done
