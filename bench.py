@@ -78,7 +78,20 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
     ranker of iris_evaluate.py:383-386 (torch.mm + full np.argsort) against a
     400k-row gallery sample, scaled to the full gallery."""
     from oracle import embed_ref
-    threads = torch.get_num_threads()
+    # BASELINE.md §2: torch.set_num_threads(len(os.sched_getaffinity(0))), capped
+    # by a cgroup CPU quota when one is set (the GPU box grants a share of a
+    # larger machine); both counts are reported
+    affinity = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    threads = min(affinity, quota) if quota else affinity
+    default_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
     n_img, n_q, n_g = 96, 64, 400_000
     sd = W.synthetic_resnet_state_dict(arch, seed)
     ww, wb = W.synthetic_linear(2048, 2048, seed + 1)
@@ -118,7 +131,9 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
                 break
     except OSError:
         pass
+    torch.set_num_threads(default_threads)
     return {"value": 1.0 / (t_embed + t_rank), "unit": "images/s", "cores": threads, "kind": "port",
+            "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "torch_default_threads": default_threads,
             "sample": f"{n_img} images embedded at batch 1 (224x224, {arch}-GeM+PCA-w, fp32) + {n_q} queries "
                       f"ranked against a {n_g}-row x {d} gallery sample (torch.mm + full np.argsort), "
                       f"rank time scaled x{scale:.0f} to {n_total} rows",

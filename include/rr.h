@@ -104,7 +104,8 @@ int rr_cosine_scores(rr_handle_t h, const float* queries, int nq,
 /* Merge nparts partial top-k lists (the per-shard results gathered over RCCL)
  * into one top-k_out list per query, same stable order.  Layout
  * part_scores/part_idx [nparts][nq][k_in]; entries with idx < 0 are padding.
- * Indices must be < 2^32.  No reference counterpart (the reference never
+ * Indices must be < 2^32 - 1 (ShardedGallery refuses larger galleries).
+ * No reference counterpart (the reference never
  * shards); it is the k-way merge of SURVEY.md §8(e).        */
 int rr_topk_merge(rr_handle_t h, const float* part_scores,
                   const long long* part_idx, int nparts, int nq, int k_in,
@@ -133,10 +134,12 @@ int rr_cosine_topk_lp(rr_handle_t h, const void* queries, const float* q_scale,
  * paper models/gem_pooling.py:3 cites):
  *   out[i] = normalize(q[i] + sum_{r<n} max(s[i][r],0)^alpha * g[idx[i][r]-idx_offset])
  * top_idx / top_scores [nq][k] as returned by rr_cosine_topk (idx < 0 =
- * padding, skipped); gallery rows are the local shard.  Re-rank by calling
- * rr_cosine_topk with `out` as the queries.                                */
+ * padding, skipped); gallery [n_rows][d] = the local rows, holding global
+ * indices [idx_offset, idx_offset + n_rows): an index outside that range is
+ * skipped, never read.  Re-rank by calling rr_cosine_topk with `out` as the
+ * queries.                                                                 */
 int rr_alpha_qe(rr_handle_t h, const float* queries, int nq,
-                const float* gallery, int d, const long long* top_idx,
+                const float* gallery, long long n_rows, int d, const long long* top_idx,
                 const float* top_scores, int k, int n, float alpha,
                 long long idx_offset, float* out, void* stream);
 

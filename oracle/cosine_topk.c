@@ -61,10 +61,14 @@ typedef struct {
   long long i;
 } item_t;
 
-/* score desc, index asc; -0.0 == +0.0 */
+/* score desc, index asc; -0.0 == +0.0; NaN after every number (including
+ * -inf), NaNs by index: np.argsort(-similarity, kind="stable") order
+ * (iris_evaluate.py:386; numpy sorts NaN last) */
 static int cmp_item(const void* pa, const void* pb) {
   const item_t* a = (const item_t*)pa;
   const item_t* b = (const item_t*)pb;
+  const int na = isnan(a->s), nb = isnan(b->s);
+  if (na != nb) return na ? 1 : -1;
   if (a->s > b->s) return -1;
   if (a->s < b->s) return 1;
   return (a->i < b->i) ? -1 : (a->i > b->i);

@@ -276,12 +276,14 @@ extern "C" int rr_resize_bilinear(rr_handle_t h, const float* x, int b, int hgt,
 // q'[i] = normalize(q[i] + sum_{r < n} max(s[i][r], 0)^alpha * g[idx[i][r]])
 // One workgroup per query; the n neighbour rows are gathered with coalesced
 // float4 loads and accumulated in registers, then the row is L2-normalised
-// with a block reduction.  Padding entries (idx < 0) are skipped.
+// with a block reduction.  Padding entries (idx < 0) and indices outside the
+// local rows [idx_offset, idx_offset + n_rows) are skipped (never read).
 namespace rr {
 __global__ __launch_bounds__(256) void alpha_qe_kernel(const float* __restrict__ q, const float* __restrict__ g,
                                                        const long long* __restrict__ idx,
                                                        const float* __restrict__ sc, int k, int n, int d,
-                                                       float alpha, long long idx_offset, float* __restrict__ out) {
+                                                       float alpha, long long idx_offset, long long n_rows,
+                                                       float* __restrict__ out) {
   __shared__ float red[256 / 64];
   const int qi = blockIdx.x;
   const int d4 = d >> 2;
@@ -290,7 +292,7 @@ __global__ __launch_bounds__(256) void alpha_qe_kernel(const float* __restrict__
     float4 acc = reinterpret_cast<const float4*>(q + (long long)qi * d)[c];
     for (int r = 0; r < n; ++r) {
       const long long j = idx[(long long)qi * k + r] - idx_offset;
-      if (j < 0) continue;
+      if (j < 0 || j >= n_rows) continue;
       const float s = sc[(long long)qi * k + r];
       const float w = s > 0.f ? powf(s, alpha) : 0.f;
       const float4 v = reinterpret_cast<const float4*>(g + j * d)[c];
@@ -319,17 +321,18 @@ __global__ __launch_bounds__(256) void alpha_qe_kernel(const float* __restrict__
 }
 }  // namespace rr
 
-extern "C" int rr_alpha_qe(rr_handle_t h, const float* queries, int nq, const float* gallery, int d,
-                           const long long* top_idx, const float* top_scores, int k, int n, float alpha,
+extern "C" int rr_alpha_qe(rr_handle_t h, const float* queries, int nq, const float* gallery, long long n_rows,
+                           int d, const long long* top_idx, const float* top_scores, int k, int n, float alpha,
                            long long idx_offset, float* out, void* stream) {
   RR_ENTRY(h);
-  if (!queries || !gallery || !top_idx || !top_scores || !out || nq < 0 || d <= 0 || (d & 3) || k <= 0 || n < 0 ||
+  if (!queries || !top_idx || !top_scores || !out || nq < 0 || n_rows < 0 || (n_rows > 0 && !gallery) || d <= 0 ||
+      (d & 3) || k <= 0 || n < 0 ||
       n > k || ((uintptr_t)queries & 15) || ((uintptr_t)gallery & 15) || ((uintptr_t)out & 15))
     return set_error(h, RR_EINVAL, "rr_alpha_qe: bad argument (d % 4 == 0, 0 <= n <= k, 16-B aligned rows)");
   if (nq == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeElem, s);
   hipLaunchKernelGGL(alpha_qe_kernel, dim3((unsigned)nq), dim3(256), 0, s, queries, gallery, top_idx, top_scores, k,
-                     n, d, alpha, idx_offset, out);
+                     n, d, alpha, idx_offset, n_rows, out);
   return check_hip(h, hipGetLastError(), "alpha_qe launch");
 }

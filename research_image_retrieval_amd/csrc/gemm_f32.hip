@@ -518,7 +518,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
               const int r = 8 * a + 4 * b + e;
               const int m = m0 + wm * WTM + acc_row<true>(i, r, lane);
               const float v = acc[i][j][r];
-              if (v > t && m < g.M) {
+              if (nok && m < g.M && !(v <= t)) {
                 const int pos = atomicAdd(g.cnt + n, 1);
                 if (pos < g.cap) g.cand[(long long)n * g.cap + pos] = make_key(v, (uint32_t)(g.row_offset + m));
               }
@@ -550,6 +550,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
         }
       }
     } else {  // E_FILTER: keep only scores strictly above the query's threshold
+      // (as !(v <= t): a NaN score, or every score under a NaN threshold, is
+      // kept; the NaN keys rank last in select_final, see ord_f32).  Padding
+      // query columns (n >= N) are excluded explicitly: a NaN gallery row gives
+      // NaN there too, and no counter exists for them.
       const float t = nok ? g.tau[n] : __builtin_inff();
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
@@ -557,7 +561,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           const float v = acc[i][j][r];
-          if (v > t && m < g.M) {
+          if (nok && m < g.M && !(v <= t)) {
             const int pos = atomicAdd(g.cnt + n, 1);
             if (pos < g.cap) g.cand[(long long)n * g.cap + pos] = make_key(v, (uint32_t)(g.row_offset + m));
           }

@@ -81,10 +81,15 @@ int set_error(rr_handle_s* h, int code, const std::string& msg);
 int check_hip(rr_handle_s* h, hipError_t e, const char* what);
 
 // ---- ordered 64-bit keys: score descending, then index ascending --------
-// key = (ord(score) << 32) | ~idx ; larger key = better rank.
+// key = (ord(score) << 32) | ~idx ; larger key = better rank.  Every NaN maps
+// to ord 0, below -inf (0x007fffff): NaN scores rank last, among themselves by
+// index, as np.argsort(-similarity) places them (iris_evaluate.py:386).  The
+// all-zero key (ord 0, idx 0xffffffff) is reserved for "no entry"; gallery
+// shards have < 2^32 rows, so a real key is never 0.
 __host__ __device__ inline uint32_t ord_f32(float f) {
   uint32_t u;
   __builtin_memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0u;  // NaN
   if (u == 0x80000000u) u = 0u;  // -0.0 ranks as +0.0 (equal scores tie-break on index)
   return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
 }

@@ -274,7 +274,7 @@ __global__ __launch_bounds__(SEL_NT) void prefilter_rescore_kernel(unsigned long
       if (i < hi) {
         const unsigned long long key = cq[i];
         if (key != 0ull) {
-          if (key_score(key) >= t2) {
+          if (!(key_score(key) < t2)) {  // NaN score or NaN T2: rescore (NaN ranks last)
             const int p = atomicAdd(&lcount, 1);
             lpos[p] = (uint32_t)i;
             lrow[p] = key_idx(key);

@@ -75,6 +75,9 @@ class ShardedGallery:
         result through the bf16-bound prefilter (rr_cosine_topk_prefilter)."""
         self.shard = shard
         self.offset = int(global_offset)
+        # rr_topk_merge keys carry 32-bit row indices (0xffffffff reserved)
+        if self.offset + shard.shape[0] >= 0xffffffff:
+            raise ValueError("ShardedGallery: global row indices must stay below 2^32 - 1")
         self.group = group
         self._local_topk = local_topk
         self._merge = merge
@@ -121,8 +124,9 @@ class ShardedGallery:
 
     def gather_rows(self, idx):
         """Rows g[idx] of the global gallery for this rank's queries: idx
-        [B_r, n] int64 (global rows) -> [B_r, n, D] fp32, each row an exact
-        copy from the shard that owns it (one variable-split all-to-all)."""
+        [B_r, n] int64 (global rows; < 0 = padding -> a zero row) -> [B_r, n, D]
+        fp32, each row an exact copy from the shard that owns it (one
+        variable-split all-to-all)."""
         group = self.group
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
@@ -133,10 +137,13 @@ class ShardedGallery:
         send, send_counts = [], []
         for t in range(world):
             it = ids[t].reshape(-1).to(dev)
-            mine = it[self._owner(it) == rank] - self.offset  # row-major (query, neighbour) order
+            # padding slots (idx < 0: fewer gallery rows than neighbours) have no owner
+            sel = (it >= 0) & (self._owner(it.clamp_min(0)) == rank)
+            mine = it[sel] - self.offset  # row-major (query, neighbour) order
             send.append(self.shard.index_select(0, mine))
             send_counts.append(int(mine.numel()))
-        own = self._owner(idx.reshape(-1).to(dev))
+        flat = idx.reshape(-1).to(dev)
+        own = torch.where(flat >= 0, self._owner(flat.clamp_min(0)), torch.full_like(flat, -1))
         recv_counts = [int((own == r).sum().item()) for r in range(world)]
         sendbuf = torch.cat(send, 0) if send else self.shard.new_empty((0, d))
         recvbuf = self.shard.new_empty((sum(recv_counts), d))
@@ -144,7 +151,7 @@ class ShardedGallery:
             sendbuf, recvbuf = sendbuf.cpu(), recvbuf.cpu()
         dist.all_to_all_single(recvbuf, sendbuf.contiguous(), recv_counts, send_counts, group=group)
         recvbuf = recvbuf.to(dev)
-        out = self.shard.new_empty((b * n, d))
+        out = self.shard.new_zeros((b * n, d))  # padding slots stay zero (and get weight 0)
         start = 0
         for r in range(world):
             pos = torch.nonzero(own == r).reshape(-1)

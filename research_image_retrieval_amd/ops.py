@@ -436,8 +436,29 @@ def quantize_rows(x, dtype):
     return y, sc
 
 
+def _lp_rows(t, sc, dtype, name):
+    """Validate quantised rows as quantize_rows makes them: bf16 [rows, d]
+    (no scales) or fp8-e4m3 bytes uint8 [rows, d] + fp32 scales [rows]."""
+    if t.dim() != 2 or not t.is_contiguous():
+        raise ValueError(f"{name}: expected contiguous [rows, d]")
+    if dtype == "bf16":
+        if t.dtype != torch.bfloat16:
+            raise TypeError(f"{name}: bf16 rows must be torch.bfloat16, got {t.dtype}")
+    else:
+        if t.dtype not in (torch.uint8, torch.float8_e4m3fn):
+            raise TypeError(f"{name}: fp8 rows must be uint8 (e4m3 bytes), got {t.dtype}")
+        if sc is None or sc.dtype != torch.float32 or not sc.is_contiguous() or sc.numel() != t.shape[0]:
+            raise ValueError(f"{name}: fp8 rows need contiguous fp32 scales, one per row")
+
+
 def cosine_topk_lp(q, q_scale, g, g_scale, k, dtype, idx_offset=0, workspace=None):
     """Fused top-k on bf16 / fp8 rows (fp32 accumulate); scores dequantised."""
+    if dtype not in _LP:
+        raise ValueError("cosine_topk_lp: dtype must be 'bf16' or 'fp8'")
+    _lp_rows(q, q_scale, dtype, "cosine_topk_lp queries")
+    _lp_rows(g, g_scale, dtype, "cosine_topk_lp gallery")
+    if q.shape[1] != g.shape[1]:
+        raise ValueError("cosine_topk_lp: descriptor dims differ")
     dev = _dev(q)
     dt = _LP[dtype]
     nq, d = q.shape
@@ -458,9 +479,15 @@ def linear_bf16(x, w, bias=None, residual=None, act=0, out_bf16=False):
     """bf16 x [M,K] . bf16 w [N,K]^T -> fp32 (or bf16) with fused epilogue."""
     if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
         raise TypeError("linear_bf16: x and w must be bfloat16")
+    if x.dim() != 2 or w.dim() != 2 or not x.is_contiguous() or not w.is_contiguous() or x.shape[1] != w.shape[1]:
+        raise ValueError("linear_bf16: contiguous x [M,K] and w [N,K] with matching K")
     dev = _dev(x)
     m, k = x.shape
     n = w.shape[0]
+    if bias is not None and (_f32(bias, "linear_bf16 bias").numel() != n):
+        raise ValueError("linear_bf16: bias must have N entries")
+    if residual is not None and tuple(_f32(residual, "linear_bf16 residual").shape) != (m, n):
+        raise ValueError("linear_bf16: residual shape mismatch")
     y = torch.empty((m, n), dtype=torch.bfloat16 if out_bf16 else torch.float32, device=x.device)
     hd = _lib.handle(dev)
     _lib.check(_lib.lib().rr_linear_bf16(hd, _ptr(x), m, k, _ptr(w), _ptr(bias), n, _ptr(residual), int(act),
@@ -507,7 +534,10 @@ def alpha_qe(queries, gallery, top_idx, top_scores, n=2, alpha=3.0, idx_offset=0
     k = top_idx.shape[1]
     out = torch.empty_like(queries)
     hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_alpha_qe(hd, _ptr(queries), nq, _ptr(gallery), d, _ptr(top_idx.contiguous()),
+    if gallery.shape[1] != d or top_idx.dtype != torch.int64 or top_scores.dtype != torch.float32:
+        raise TypeError("alpha_qe: gallery [N, d] fp32, top_idx int64, top_scores fp32")
+    _lib.check(_lib.lib().rr_alpha_qe(hd, _ptr(queries), nq, _ptr(gallery), gallery.shape[0], d,
+                                      _ptr(top_idx.contiguous()),
                                       _ptr(top_scores.contiguous()), k, int(n), float(alpha), int(idx_offset),
                                       _ptr(out), _stream(dev)), hd, "rr_alpha_qe")
     return out

@@ -83,7 +83,8 @@ def _qe_worker(rank, world, port, q_all, g_all, k, sizes, out):
     sg = ShardedGallery(g_all[lo:hi].contiguous(), lo, local_topk=_local_topk, merge=_merge)
     qlo = sum(sizes[:rank])
     mine = q_all[qlo:qlo + sizes[rank]].contiguous()
-    rows = sg.gather_rows(torch.tensor([[0, g_all.shape[0] - 1]] * sizes[rank], dtype=torch.int64).view(-1, 2))
+    # first row, a padding slot (idx -1: fewer gallery rows than neighbours), last row
+    rows = sg.gather_rows(torch.tensor([[0, -1, g_all.shape[0] - 1]] * sizes[rank], dtype=torch.int64).view(-1, 3))
     s, i, q2 = sg.alpha_qe_search(mine, k, n=3, alpha=3.0, expand=_expand)
     out[rank] = (s.numpy(), i.numpy(), q2.numpy(), rows.numpy())
     dist.barrier()
@@ -114,6 +115,7 @@ def test_sharded_alpha_qe_world3_matches_single():
     np.testing.assert_array_equal(np.concatenate([o[2] for o in got]), q2)
     np.testing.assert_array_equal(np.concatenate([o[1] for o in got]), i2)
     np.testing.assert_array_equal(np.concatenate([o[0] for o in got]), s2)
-    for o in got:  # gather_rows of the first and the last gallery row
+    for o in got:  # gather_rows of the first gallery row, a padding slot, the last row
         assert np.array_equal(o[3][:, 0], np.broadcast_to(g[0], o[3][:, 0].shape))
-        assert np.array_equal(o[3][:, 1], np.broadcast_to(g[-1], o[3][:, 1].shape))
+        assert not o[3][:, 1].any()
+        assert np.array_equal(o[3][:, 2], np.broadcast_to(g[-1], o[3][:, 2].shape))

@@ -23,8 +23,9 @@ sys.path.insert(0, GOLD)
 import inputs as I  # noqa: E402
 
 # descriptor tolerance (unit-norm fp32 vectors, 50-100 conv layers deep):
-# GPU implicit-GEMM vs CPU oneDNN accumulation order + BN folding.
-DESC_TOL = 5e-5
+# GPU implicit-GEMM vs CPU oneDNN accumulation order + BN folding; measured
+# 1.3-1.4e-7 (round 2)
+DESC_TOL = 1e-6
 
 
 def _imgs(seed, b, h, w):
@@ -98,9 +99,11 @@ def test_extract_vectors_multiscale_vs_reference_fixture(cuda):
     imgs = I.tiny_images(int(fx["img_seed"]))
     v1 = extract_vectors(net, imgs, ms=[1], device=cuda, print_freq=0).numpy()
     v3 = extract_vectors(net, imgs, ms=[1, 1 / np.sqrt(2), 1 / 2], device=cuda, print_freq=0).numpy()
-    np.testing.assert_allclose(v1, fx["v1"], rtol=0, atol=2e-5)
     ok = ~np.isnan(fx["v3"]).any(1)
-    np.testing.assert_allclose(v3[ok], fx["v3"][ok], rtol=0, atol=2e-5)
+    print("extract_vectors vs reference fixture: ms=[1] max|err|", np.abs(v1 - fx["v1"]).max(),
+          "3 scales", np.abs(v3[ok] - fx["v3"][ok]).max())
+    np.testing.assert_allclose(v1, fx["v1"], rtol=0, atol=2e-6)
+    np.testing.assert_allclose(v3[ok], fx["v3"][ok], rtol=0, atol=2e-6)
     assert np.isnan(v3[~ok]).all()  # all scales dropped -> NaN, as the reference
 
 

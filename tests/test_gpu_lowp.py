@@ -54,7 +54,7 @@ def test_fp8_quantize_and_scores(cuda):
     torch.testing.assert_close(got, ref, rtol=1e-4, atol=1e-5)
 
 
-@pytest.mark.parametrize("dtype,min_recall", [("bf16", 0.95), ("fp8", 0.80)])
+@pytest.mark.parametrize("dtype,min_recall", [("bf16", 0.99), ("fp8", 0.93)])  # measured 0.997 / 0.95
 def test_lowp_cosine_recall_at_100(cuda, dtype, min_recall):
     q, g = I.rank_inputs(23, 32, 60000, 512)
     _, i_ref = oracle.cosine_topk(q, g, 100)
@@ -105,4 +105,4 @@ def test_vit_b16_bf16_vs_reference(cuda):
     ref = fx["b16"]
     cos = (got * ref).sum(1) / np.linalg.norm(got, axis=1) / np.linalg.norm(ref, axis=1)
     print("bf16 ViT cosine to fp32 reference", cos)
-    assert cos.min() > 0.995
+    assert cos.min() > 0.9999  # measured 0.999988

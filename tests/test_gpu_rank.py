@@ -156,3 +156,55 @@ def test_prefilter_unnormalised_rows(cuda):
     g = (rs.standard_normal((30_000, 64)) * rs.uniform(0.01, 3.0, size=(30_000, 1))).astype(np.float32)
     q = (rs.standard_normal((11, 64)) * 2.5).astype(np.float32)
     _prefilter_vs_exhaustive(cuda, q, g, 50)
+
+
+@pytest.mark.parametrize("ranker", ["exhaustive", "prefilter"])
+def test_nan_rows_and_queries_rank_last(cuda, ranker):
+    """NaN descriptors (extract_vectors yields them when every scale is dropped,
+    utils/helpfunc.py:39-44) rank after every number, by index, as
+    np.argsort(-similarity, kind="stable") places them (iris_evaluate.py:386):
+    NaN gallery rows inside and outside the threshold-seeding sample, a NaN
+    query (all scores NaN: indices 0..k-1), and k > #finite rows."""
+    rs = np.random.RandomState(17)
+    n, d = 20000, 128
+    g = rs.standard_normal((n, d)).astype(np.float32)
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    q = rs.standard_normal((6, d)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    g[5] = np.nan           # inside the seed sample (first 4096 rows)
+    g[15000, 7] = np.nan    # outside it
+    g[16000] = g[5]
+    q[4] = np.nan           # a NaN query
+    for gal, k in ((g, 100), (g[:40].copy(), 60)):
+        sim = oracle.cosine_scores(q, gal)
+        order = oracle.argsort_stable_desc(sim)[:, :k]
+        qd, gd = torch.from_numpy(q).to(cuda), torch.from_numpy(gal).to(cuda)
+        if ranker == "exhaustive":
+            s, i = ops.cosine_topk(qd, gd, k)
+        else:
+            gb, _ = ops.quantize_rows(gd, "bf16")
+            s, i = ops.cosine_topk_prefilter(qd, gd, gb, ops.prefilter_gallery_bound(gd, gb), k)
+        s, i = s.cpu().numpy(), i.cpu().numpy()
+        kk = min(k, gal.shape[0])
+        assert np.array_equal(i[:, :kk], order[:, :kk]), np.argwhere(i[:, :kk] != order[:, :kk])[:5]
+        ref_s = np.take_along_axis(sim, order[:, :kk], 1)
+        assert np.array_equal(np.isnan(s[:, :kk]), np.isnan(ref_s))
+        fin = ~np.isnan(ref_s)
+        assert np.array_equal(s[:, :kk][fin], ref_s[fin])
+        assert (i[:, kk:] == -1).all() and np.isneginf(s[:, kk:]).all()
+        assert list(i[4, :kk]) == list(range(kk))  # the NaN query: every score NaN -> index order
+
+
+def test_alpha_qe_skips_padding_and_foreign_indices(cuda):
+    """rr_alpha_qe reads only local rows [idx_offset, idx_offset + n_rows):
+    padding (-1) and indices of another shard contribute nothing."""
+    rs = np.random.RandomState(5)
+    q = rs.standard_normal((3, 64)).astype(np.float32)
+    g = rs.standard_normal((50, 64)).astype(np.float32)
+    idx = np.array([[100, 101], [100, -1], [100, 150 + 7]], dtype=np.int64)  # local rows 100..149
+    sc = np.array([[0.9, 0.5], [0.7, -np.inf], [0.8, 0.6]], dtype=np.float32)
+    out = ops.alpha_qe(torch.from_numpy(q).to(cuda), torch.from_numpy(g).to(cuda), torch.from_numpy(idx).to(cuda),
+                       torch.from_numpy(sc).to(cuda), n=2, alpha=3.0, idx_offset=100).cpu().numpy()
+    keep = np.where((idx >= 100) & (idx < 150), idx, -1)
+    ref = oracle.alpha_qe(q, g, keep, sc, n=2, alpha=3.0, idx_offset=100)
+    np.testing.assert_allclose(out, ref, rtol=0, atol=2e-6)

@@ -18,7 +18,7 @@ from research_image_retrieval_amd.networks import GeM
 
 pytestmark = pytest.mark.gpu
 
-DESC_TOL = 5e-5  # as tests/test_gpu_embed.py
+DESC_TOL = 1e-6  # as tests/test_gpu_embed.py (measured 1.4e-7)
 
 
 def _planes_to_f32(p):
