@@ -71,6 +71,26 @@ def build_extractor(arch, device, seed=0, conv_math="s3"):
     return GeMPCAw(net, pw)
 
 
+def host_threads():
+    """torch.set_num_threads(len(os.sched_getaffinity(0))) --
+    capped by the CPU share the job is actually granted: a cgroup CPU quota, or
+    the OMP_NUM_THREADS the GPU box exports (its affinity mask shows the whole
+    machine, 256 CPUs, of which the box grants 16; 256 threads on 16 cores ran
+    the batch-1 R50 embed 60x slower).  Returns (affinity, cap, threads)."""
+    affinity = len(os.sched_getaffinity(0))
+    cap = None
+    try:
+        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            cap = max(1, int(int(q) // int(p)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and int(omp) > 0:
+        cap = int(omp) if cap is None else min(cap, int(omp))
+    return affinity, cap, (min(affinity, cap) if cap else affinity)
+
+
 def cpu_baseline(arch, n_total, d, k, seed=0):
     """The reference's CPU path, timed on a bounded sample on this host:
     batch-1 extraction (utils/helpfunc.py:18-48 semantics) through the oracle's
@@ -78,18 +98,7 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
     ranker of iris_evaluate.py:383-386 (torch.mm + full np.argsort) against a
     400k-row gallery sample, scaled to the full gallery."""
     from oracle import embed_ref
-    # BASELINE.md §2: torch.set_num_threads(len(os.sched_getaffinity(0))), capped
-    # by a cgroup CPU quota when one is set (the GPU box grants a share of a
-    # larger machine); both counts are reported
-    affinity = len(os.sched_getaffinity(0))
-    quota = None
-    try:
-        q, p = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
-        if q != "max":
-            quota = max(1, int(int(q) // int(p)))
-    except (OSError, ValueError):
-        pass
-    threads = min(affinity, quota) if quota else affinity
+    affinity, quota, threads = host_threads()
     default_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
     n_img, n_q, n_g = 96, 64, 400_000
@@ -133,12 +142,197 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
         pass
     torch.set_num_threads(default_threads)
     return {"value": 1.0 / (t_embed + t_rank), "unit": "images/s", "cores": threads, "kind": "port",
-            "affinity_cpus": affinity, "cgroup_cpu_quota": quota, "torch_default_threads": default_threads,
+            "affinity_cpus": affinity, "granted_cpus": quota, "torch_default_threads": default_threads,
             "sample": f"{n_img} images embedded at batch 1 (224x224, {arch}-GeM+PCA-w, fp32) + {n_q} queries "
                       f"ranked against a {n_g}-row x {d} gallery sample (torch.mm + full np.argsort), "
                       f"rank time scaled x{scale:.0f} to {n_total} rows",
             "embed_s_per_image": t_embed, "rank_s_per_query_argsort": t_rank, "rank_s_per_query_topk": t_rank_topk,
             "value_with_topk": 1.0 / (t_embed + t_rank_topk), "cpu_model": model}
+
+
+# ---- config C2: ResNet50-GeM 512-d at imsize 1024 over a ROxford5k-shaped set ----
+C2_GALLERY, C2_QUERIES = 4993, 70  # revisitop ROxford5k: 4,993 images, 70 queries
+# (H, W) after thumbnail(1024) and the share of the gallery at that size
+C2_SIZES = ((768, 1024, 0.70), (1024, 768, 0.22), (683, 1024, 0.06), (1024, 683, 0.02))
+C2_BATCH = 16  # same-size gallery images per extractor call (the reference runs batch 1)
+
+
+def c2_layout(n_gallery, n_query, seed=1234):
+    """Sizes of the gallery groups and of the query crops (bbox crops of
+    1024-px images, dataset/ImageFromList.py:40-57: kept at their crop size)."""
+    counts = [int(round(n_gallery * f)) for _, _, f in C2_SIZES]
+    counts[0] += n_gallery - sum(counts)
+    rs = np.random.RandomState(seed)
+    qs = [(int(rs.randint(200, 769)), int(rs.randint(200, 1025))) for _ in range(n_query)]
+    return [(h, w, c) for (h, w, _), c in zip(C2_SIZES, counts)], qs
+
+
+def cpu_baseline_c2(n_gallery, n_query, d=512, seed=0):
+    """The reference CPU path for C2, timed on a bounded sample: batch-1
+    extraction of 2 gallery images at 768x1024 (utils/helpfunc.py:18-48 through
+    the oracle's R50-GeM-512 restatement), and the full ranking of all queries
+    (torch.mm + np.argsort, iris_evaluate.py:383-386) against the whole
+    gallery; the job time = all images x per-image embed + the ranking."""
+    from oracle import embed_ref
+    affinity, granted, threads = host_threads()
+    default_threads = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    sd = W.synthetic_resnet_state_dict("resnet50", seed)
+    pw, pb = W.synthetic_linear(d, 2048, seed + 2)
+    rs = np.random.RandomState(1234)
+    imgs = torch.from_numpy(rs.randint(0, 256, size=(3, 768, 1024, 3), dtype=np.uint8))
+    with torch.no_grad():
+        embed_ref.gem_model_descriptor(embed_ref.normalize_u8(imgs[:1]), sd, W.RESNET_LAYERS["resnet50"], pw, pb)
+        t0 = time.perf_counter()
+        for i in (1, 2):
+            embed_ref.gem_model_descriptor(embed_ref.normalize_u8(imgs[i:i + 1]), sd, W.RESNET_LAYERS["resnet50"],
+                                           pw, pb)
+        t_embed = (time.perf_counter() - t0) / 2
+        gen = torch.Generator().manual_seed(7)
+        g = torch.nn.functional.normalize(torch.randn(n_gallery, d, generator=gen), dim=1)
+        q = torch.nn.functional.normalize(torch.randn(n_query, d, generator=gen), dim=1)
+        t0 = time.perf_counter()
+        np.argsort(-torch.mm(q, g.t()).numpy(), axis=1)
+        t_rank = time.perf_counter() - t0
+    torch.set_num_threads(default_threads)
+    total = (n_gallery + n_query) * t_embed + t_rank
+    return {"value": (n_gallery + n_query) / total, "unit": "images/s", "cores": threads, "kind": "port",
+            "affinity_cpus": affinity, "granted_cpus": granted,
+            "sample": f"2 images embedded at batch 1 (768x1024, resnet50-GeM 512-d, fp32) and the full ranking of "
+                      f"{n_query} queries x {n_gallery} rows (torch.mm + np.argsort); job time = "
+                      f"{n_gallery + n_query} x per-image embed + ranking",
+            "embed_s_per_image": t_embed, "rank_s": t_rank, "torch_default_threads": default_threads}
+
+
+def run_c2(a, world, rank, dev):
+    """C2: ResNet50-GeM 512-d fp32 (Table-1 GeMModel) over a ROxford5k-shaped
+    set at imsize 1024 -- 4,993 gallery images + 70 query crops, every image
+    embedded (gallery images in same-size batches, queries one by one at their
+    own crop size), full ranks of the queries against the gallery and the
+    revisited mAP (utils/evaluate.py:153-194) on the host.  One step = the
+    whole set; N ranks split the images (strong scaling), descriptors are
+    all-gathered over RCCL and rank 0 ranks and scores."""
+    from research_image_retrieval_amd.distributed import _all_gather_var
+    from research_image_retrieval_amd.evaluate import compute_map_and_print
+    from research_image_retrieval_amd.models import get_model
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    n_g, n_q = a.c2_gallery, a.c2_queries
+    groups, qsizes = c2_layout(n_g, n_q)
+    net = get_model("gem_r50", 1000, feature_dim=512, seed=0, device=dev, conv_math=a.conv_math)
+    # this rank's images (contiguous share of the gallery order, and of the queries)
+    glo, ghi = shard_bounds(n_g, world, rank)
+    qlo, qhi = shard_bounds(n_q, world, rank)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1234)
+    batches, start = [], 0
+    for h, w, c in groups:
+        lo, hi = max(start, glo), min(start + c, ghi)
+        for b0 in range(lo, hi, C2_BATCH):
+            nb = min(C2_BATCH, hi - b0)
+            batches.append(torch.randint(0, 256, (nb, h, w, 3), dtype=torch.uint8, device=dev, generator=gen))
+        start += c
+    queries = [torch.randint(0, 256, (1, h, w, 3), dtype=torch.uint8, device=dev, generator=gen)
+               for (h, w) in qsizes[qlo:qhi]]
+    import inputs as I  # noqa: E402  (synthetic ROxford5k-shaped ground truth)
+    gnd, _ = I.map_inputs(31, nq=n_q, n=n_g)
+    torch.cuda.synchronize()
+
+    def step(marks=None):
+        def mark(name):
+            if marks is not None:
+                torch.cuda.synchronize()
+                marks.append((name, time.perf_counter()))
+        mark("start")
+        gd = torch.cat([net.forward_test_u8(b) for b in batches], 0) if batches else \
+            torch.empty((0, 512), device=dev)
+        mark("gallery_embed")
+        qd = torch.cat([net.forward_test_u8(q) for q in queries], 0) if queries else torch.empty((0, 512), device=dev)
+        mark("query_embed")
+        if world > 1:
+            gd = torch.cat(_all_gather_var(gd.contiguous(), None)[0], 0)
+            qd = torch.cat(_all_gather_var(qd.contiguous(), None)[0], 0)
+        mark("all_gather")
+        if rank != 0:
+            return None
+        s, i = ops.cosine_topk(qd.contiguous(), gd.contiguous(), n_g)  # full ranks (k = N)
+        ranks = i.cpu().numpy().T.copy()
+        mark("rank")
+        m = compute_map_and_print("roxford5k", "c2", "global", ranks, gnd)
+        mark("map")
+        return m
+
+    for _ in range(a.warmup):
+        step()
+    marks = []
+    step(marks)  # one more untimed step with a sync at every phase boundary
+    phases = {b[0]: round((b[1] - a_[1]) * 1e3, 2) for a_, b in zip(marks, marks[1:])}
+    log(f"[rank {rank}] c2 phases (ms, synchronised step): {phases}")
+    timer = ops.KernelTimer(dev.index)
+    timer.enable(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        maps = step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    cls = {name: timer.collect(c) for name, c in (("conv_gemm", _lib.TIME_GEMM), ("select", _lib.TIME_SELECT),
+                                                   ("elementwise", _lib.TIME_ELEM),
+                                                   ("cosine_seed", _lib.TIME_COSINE_SEED))}
+    timer.enable(False)
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    units = n_g + n_q
+    value = units * a.steps / elapsed
+    # algorithmic FLOPs of this rank's share: every image's trunk convs + the 2048->512 projection
+    img_flops = sum(c_ * (sum(W.resnet_conv_flops("resnet50", h, w).values()) + 2 * 2048 * 512)
+                    for (h, w, c_) in [(h, w, max(0, min(s0 + c, ghi) - max(s0, glo)))
+                                       for (h, w, c), s0 in zip(groups, np.cumsum([0] + [g[2] for g in groups]))])
+    img_flops += sum(sum(W.resnet_conv_flops("resnet50", h, w).values()) + 2 * 2048 * 512 for (h, w) in qsizes[qlo:qhi])
+    rk = {}
+    ms, n = cls["conv_gemm"]
+    if n:
+        sec = ms / 1e3 / a.steps
+        dt = "s3" if a.conv_math == "s3" else "fp32"
+        ach = img_flops / sec / 1e12
+        rk["conv_gemm"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
+                           "frac": round(ach / PEAK_TFLOPS[dt], 4), "dtype": "fp32", "ms_per_step": round(ms / a.steps, 3),
+                           "launches_per_step": n / a.steps, "algorithmic_flop_per_launch": img_flops / max(1.0, n / a.steps),
+                           "algorithmic_bytes_per_launch": None, "traffic": None}
+        if dt == "s3":
+            rk["conv_gemm"]["math"] = "fp32 via exact 3-way bf16 split (6 bf16 MFMA products per fp32 product); peak = bf16 dense peak / 6"
+    for name in ("select", "elementwise", "cosine_seed"):
+        ms, n = cls[name]
+        rk[name] = {"ms_per_step": round(ms / a.steps, 3), "launches_per_step": n / a.steps}
+    roof = dict(rk.get("conv_gemm", {}))
+    roof["kernel"] = "conv_gemm"
+    res = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps,
+           "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
+           "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
+           "data": "synthetic: uint8 images at ROxford5k's post-thumbnail(1024) sizes (768x1024 / 1024x768 / 683x1024 / "
+                   "1024x683) and random 200-768 x 200-1024 query crops, torch.Generator(1234); synthetic "
+                   "ROxford5k-shaped gnd (mAP is pipeline parity, not accuracy); seeded weights",
+           "config": {"workload": f"C2: resnet50-GeM 512-d fp32 (Table-1 GeMModel), {n_g} gallery + {n_q} query "
+                                  f"images at imsize 1024, full ranks + revisited mAP",
+                      "global_batch": units, "gallery_rows": n_g, "queries": n_q, "dim": 512,
+                      "gallery_batch": C2_BATCH, "parallelism": f"image-dp{world}", "conv_math": a.conv_math},
+           "map_easy_medium_hard": list(maps) if maps is not None else None,
+           "phases_ms_synchronised_step": phases,
+           "roofline": roof, "roofline_by_kernel": rk}
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        t = time.time()
+        res["cpu_baseline"] = cpu_baseline_c2(n_g, n_q)
+        log(f"cpu baseline {time.time() - t:.1f}s")
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
 
 
 def seed_rows(n, k):
@@ -171,8 +365,9 @@ def main():
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--arch", default="resnet101")
-    ap.add_argument("--workload", choices=("c3", "c4", "c5"), default="c3",
-                    help="c3: ResNet101-GeM 2048-d + PCA-w, fp32 (BASELINE metric config); "
+    ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c3",
+                    help="c2: ResNet50-GeM 512-d fp32 over a ROxford5k-shaped set at imsize 1024 (full ranks + mAP); "
+                         "c3: ResNet101-GeM 2048-d + PCA-w, fp32 (BASELINE metric config); "
                          "c4: ViT-B/16 CLS 512-d, bf16 GEMMs + bf16 cosine; "
                          "c5: c3 extractor at 3 scales + fp8 cosine + alpha-QE re-rank (sharded: neighbour rows fetched from their shards)")
     ap.add_argument("--dtype", choices=("fp32", "bf16", "fp8"), default=None,
@@ -184,15 +379,17 @@ def main():
                     help="ResNet trunk convs: s3 = fp32-accurate 3-way bf16 split on the bf16 matrix cores "
                          "(error vs float64 <= the exact-fp32 core's, tests/test_gpu_s3.py); f32 = exact fp32 MFMA")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c2-gallery", type=int, default=C2_GALLERY)
+    ap.add_argument("--c2-queries", type=int, default=C2_QUERIES)
     a = ap.parse_args()
     if a.workload == "c4":
         if a.dim == 2048:
             a.dim = 512
         a.arch = "vit_b16"
     if a.dtype is None:
-        a.dtype = {"c3": "fp32", "c4": "bf16", "c5": "fp8"}[a.workload]
-    if a.workload == "c3" and a.dtype != "fp32":
-        raise SystemExit("c3 is defined in fp32 (the reference's arithmetic)")
+        a.dtype = {"c2": "fp32", "c3": "fp32", "c4": "bf16", "c5": "fp8"}[a.workload]
+    if a.workload in ("c2", "c3") and a.dtype != "fp32":
+        raise SystemExit(f"{a.workload} is defined in fp32 (the reference's arithmetic)")
 
     if a.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # started bare with --gpus N: run ourselves under torch.distributed.run
@@ -221,6 +418,8 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    if a.workload == "c2":
+        return run_c2(a, world, rank, dev)
     t_setup = time.time()
     lo, hi = shard_bounds(a.gallery, world, rank)
     gallery = make_gallery(a.gallery, a.dim, lo, hi, dev)

@@ -20,10 +20,15 @@ int check_hip(rr_handle_s* h, hipError_t e, const char* what) {
 TimedLaunch::TimedLaunch(rr_handle_s* h_, int cls_, hipStream_t s_) : h(h_), cls(cls_), s(s_) {
   if (!h || !h->timing || cls < 0 || cls >= rr_handle_s::kClasses) return;
   const int i = h->n_ev[cls];
-  if (i >= rr_handle_s::kMaxEv) return;
-  if (!h->ev_start[cls][i]) {
-    if (hipEventCreate(&h->ev_start[cls][i]) != hipSuccess) return;
-    if (hipEventCreate(&h->ev_stop[cls][i]) != hipSuccess) return;
+  if (i >= (int)h->ev_start[cls].size()) {
+    hipEvent_t a = nullptr, b = nullptr;
+    if (hipEventCreate(&a) != hipSuccess) return;
+    if (hipEventCreate(&b) != hipSuccess) {
+      (void)hipEventDestroy(a);
+      return;
+    }
+    h->ev_start[cls].push_back(a);
+    h->ev_stop[cls].push_back(b);
   }
   if (hipEventRecord(h->ev_start[cls][i], s) != hipSuccess) return;
   slot = i;
@@ -78,7 +83,7 @@ int rr_create(int device, rr_handle_t* out) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return RR_EHIP;
   rr_handle_s* h = new (std::nothrow) rr_handle_s();
-  RR_ENTRY(h);
+  if (!h) return RR_EINVAL;
   h->device = device;
   *out = h;
   return RR_OK;
@@ -87,9 +92,9 @@ int rr_create(int device, rr_handle_t* out) {
 int rr_destroy(rr_handle_t h) {
   RR_ENTRY(h);
   for (int c = 0; c < rr_handle_s::kClasses; ++c)
-    for (int i = 0; i < rr_handle_s::kMaxEv; ++i) {
-      if (h->ev_start[c][i]) (void)hipEventDestroy(h->ev_start[c][i]);
-      if (h->ev_stop[c][i]) (void)hipEventDestroy(h->ev_stop[c][i]);
+    for (size_t i = 0; i < h->ev_start[c].size(); ++i) {
+      (void)hipEventDestroy(h->ev_start[c][i]);
+      (void)hipEventDestroy(h->ev_stop[c][i]);
     }
   delete h;
   return RR_OK;

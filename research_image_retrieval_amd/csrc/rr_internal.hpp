@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
+#include <vector>
 
 #include "../../include/rr.h"
 
@@ -21,13 +22,10 @@ struct rr_handle_s {
   // timing (see rr_timing_enable)
   bool timing = false;
   static constexpr int kClasses = 6;
-  static constexpr int kMaxEv = 16384;
-  hipEvent_t (*ev_start)[kMaxEv] = new hipEvent_t[kClasses][kMaxEv]();
-  hipEvent_t (*ev_stop)[kMaxEv] = new hipEvent_t[kClasses][kMaxEv]();
-  ~rr_handle_s() {
-    delete[] ev_start;
-    delete[] ev_stop;
-  }
+  // event pairs per class, created on demand and reused across timing
+  // windows; the pool grows with the launches of a window (no cap: a capped
+  // pool silently dropped the launches past it)
+  std::vector<hipEvent_t> ev_start[kClasses], ev_stop[kClasses];
   int n_ev[kClasses] = {};
   double acc_ms[kClasses] = {};
   long long acc_launches[kClasses] = {};

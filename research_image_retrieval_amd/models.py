@@ -34,14 +34,14 @@ class GeMModel(_Extractor):
     in_channels = 4
 
     def __init__(self, backbone="resnet50", pretrained=False, num_classes=1000, feature_dim=2048, gem_p=3.0,
-                 state_dict=None, seed=0, device="cuda"):
+                 state_dict=None, seed=0, device="cuda", conv_math="s3", stride_on="3x3"):
         if pretrained:
             raise ValueError("pretrained weights need a download; pass a local state_dict instead "
                              "(models/gem_pooling.py:35 defaults to pretrained=True)")
         if backbone not in ("resnet50", "resnet101"):
             raise ValueError(f"Unsupported backbone: {backbone}")
         self.device = torch.device(device)
-        self.backbone = ResNet(backbone, state_dict, seed, device)
+        self.backbone = ResNet(backbone, state_dict, seed, device, conv_math=conv_math, stride_on=stride_on)
         self.gem_pool = GeMPooling(p=gem_p)
         backbone_dim = 2048
         pw, pb = _from_sd(state_dict, "feature_proj") or W.synthetic_linear(feature_dim, backbone_dim, seed + 2)

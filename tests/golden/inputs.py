@@ -171,3 +171,32 @@ def write_fake_revisited(root, name="roxford5k"):
     with open(os.path.join(root, name, f"gnd_{name}.pkl"), "wb") as f:
         pickle.dump(cfg, f)
     return cfg
+
+
+# ROxford5k-like full-resolution images (width, height) before the loader's
+# thumbnail(1024): landscape / portrait 4:3, larger photos that get
+# thumbnailed, a 3:2 photo, and a small one that stays as it is
+FULLRES_SIZES = [(1024, 768), (768, 1024), (1280, 960), (1600, 1066), (700, 525), (2048, 1365)]
+FULLRES_BBOXES = [(120.5, 80.25, 900.0, 700.0), (300.0, 10.0, 1500.0, 1000.0)]
+
+
+def write_fake_revisited_fullres(root, name="roxford5k"):
+    """A revisitop-layout dataset at full resolution (config C2: imsize 1024):
+    six gallery images of the sizes above, two bbox queries (images 0 and 3)."""
+    import pickle
+    from PIL import Image
+    d = os.path.join(root, name, "jpg")
+    os.makedirs(d)
+    rs = np.random.RandomState(71)
+    for i, (w, h) in enumerate(FULLRES_SIZES):
+        yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+        base = np.stack([(np.sin(xx / (17 + 5 * c)) + np.cos(yy / (11 + 3 * c))) * 60 + 128 for c in range(3)], -1)
+        img = np.clip(base + rs.randint(-40, 41, size=(h, w, 3)), 0, 255).astype(np.uint8)
+        Image.fromarray(img).save(os.path.join(d, f"im{i}.jpg"), quality=92)
+    e = np.array([], dtype=np.int64)
+    gnd = [{"bbx": np.array(FULLRES_BBOXES[0]), "easy": np.array([1, 4]), "hard": np.array([2]), "junk": e},
+           {"bbx": np.array(FULLRES_BBOXES[1]), "easy": np.array([5]), "hard": e, "junk": np.array([0])}]
+    cfg = {"imlist": [f"im{i}" for i in range(len(FULLRES_SIZES))], "qimlist": ["im0", "im3"], "gnd": gnd}
+    with open(os.path.join(root, name, f"gnd_{name}.pkl"), "wb") as f:
+        pickle.dump(cfg, f)
+    return cfg

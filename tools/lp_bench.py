@@ -1,6 +1,8 @@
 """Low-precision GEMM configs on the shapes that matter (ViT-B/16 linears at
 B=320, the bf16 prefilter sweep, the fp8 C5 sweep).  Run once per forced
-config: RR_GEMM_LPCFG=22|41|big|q320 python tools/lp_bench.py  -> JSON lines."""
+config: LP_CFG=1|2|3|4 python tools/lp_bench.py  -> JSON lines (rr_set_tuning
+RR_TUNE_LP_CFG: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 sweep tile;
+unset = the library's pick)."""
 import json
 import os
 import sys
@@ -25,8 +27,10 @@ def t_ms(fn, iters=10, warm=3):
     return st.elapsed_time(en) / iters
 
 
-cfg = os.environ.get("RR_GEMM_LPCFG", "auto")
+cfg = os.environ.get("LP_CFG", "auto")
 dev = torch.device("cuda:0")
+if cfg != "auto":
+    ops.tuning(0, lp_cfg=int(cfg)).__enter__()
 g = torch.Generator(device=dev).manual_seed(0)
 M = 320 * 197
 for (k, n) in [(768, 2304), (768, 768), (768, 3072), (3072, 768)]:

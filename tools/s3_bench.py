@@ -1,6 +1,6 @@
 """Per-layer timing of the R101 trunk convs at B images: exact-fp32 core vs
-the split-bf16 core (RR_S3_CFG selects the s3 tile config; read once per
-process).  usage: s3_bench.py [B] [reps]"""
+the split-bf16 core.  usage: [S3_CFG=1..6] [S3_ONLY=1] s3_bench.py [B] [reps]
+(S3_CFG forces one s3 tile config through rr_set_tuning; default: the library's pick)"""
 import os
 import sys
 
@@ -21,6 +21,8 @@ SHAPES = [(56, 64, 64, 1, 1, 0, 1), (56, 64, 64, 3, 1, 0, 3), (56, 64, 256, 1, 1
           (14, 1024, 512, 1, 1, 0, 1), (14, 512, 512, 3, 2, 0, 1), (7, 512, 2048, 1, 1, 1, 3),
           (7, 2048, 512, 1, 1, 0, 2), (7, 512, 512, 3, 1, 0, 2), (14, 1024, 2048, 1, 2, 0, 1)]
 dev = torch.device("cuda:0")
+CFG = int(os.environ.get("S3_CFG", "0"))
+ops.tuning(0, s3_cfg=CFG).__enter__()
 tot = {"f32": 0.0, "s3": 0.0}
 flops_tot = 0.0
 for h, cin, cout, k, s, res, cnt in SHAPES:
@@ -58,4 +60,4 @@ for h, cin, cout, k, s, res, cnt in SHAPES:
           f"({fl / out['f32'][0] / 1e9:6.1f} TF/s)  s3 {out['s3'][0]:7.3f} ms ({fl / out['s3'][0] / 1e9:6.1f} TF/s) "
           f"speedup {out['f32'][0] / out['s3'][0]:.2f}  max|diff| {d:.2e}", flush=True)
 print(f"TOTAL trunk convs (weighted): f32 {tot['f32']:.2f} ms ({flops_tot / max(tot['f32'], 1e-9) / 1e9:.1f} TF/s)  "
-      f"s3 {tot['s3']:.2f} ms ({flops_tot / tot['s3'] / 1e9:.1f} TF/s) cfg={os.environ.get('RR_S3_CFG', 'auto')}")
+      f"s3 {tot['s3']:.2f} ms ({flops_tot / tot['s3'] / 1e9:.1f} TF/s) cfg={CFG or 'auto'}")
