@@ -47,16 +47,32 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_gallery(n_total, d, lo, hi, device, seed=0):
-    """Rows [lo, hi) of a seeded Gaussian gallery, L2-normalised, generated on
-    the GPU in 64k-row blocks keyed by global block index (shard-invariant)."""
+GLDV2_CLASSES = 81313  # GLDv2-clean: 1,580,470 images of 81,313 landmarks (dataset/configdataset.py:443)
+
+
+def make_gallery(n_total, d, lo, hi, device, seed=0, kind="gaussian"):
+    """Rows [lo, hi) of a seeded gallery, L2-normalised, generated on the GPU
+    in 64k-row blocks keyed by global block index (shard-invariant).
+    kind "gaussian": isotropic rows.  kind "clustered": landmark-like rows,
+    normalize(centre[c] + noise) with |noise| = |centre| (cosine ~0.7 to the
+    class centre, ~0.5 between members of a class), the class of each row drawn
+    from GLDV2_CLASSES seeded centres: the prefilter's worst case, many rows
+    crowding near a query's top-k threshold."""
     g = torch.empty((hi - lo, d), dtype=torch.float32, device=device)
     blk = 65536
     gen = torch.Generator(device=device)
+    centres = None
+    if kind == "clustered":
+        gen.manual_seed(seed * 1_000_003 + 999_983)
+        centres = torch.randn((GLDV2_CLASSES, d), generator=gen, device=device)
+        centres = ops.l2_normalize(centres, 1e-12, out=centres)
     b0 = lo // blk
     for b in range(b0, (hi + blk - 1) // blk):
         gen.manual_seed(seed * 1_000_003 + b)
         rows = torch.randn((blk, d), generator=gen, device=device)
+        if centres is not None:
+            cls = torch.randint(0, GLDV2_CLASSES, (blk,), generator=gen, device=device)
+            rows = centres[cls] + rows / d ** 0.5
         s, e = max(lo, b * blk), min(hi, (b + 1) * blk)
         g[s - lo:e - lo] = rows[s - b * blk:e - b * blk]
     ops.l2_normalize(g, 1e-12, out=g)
@@ -257,7 +273,9 @@ def run_c2(a, world, rank, dev):
         s, i = ops.cosine_topk(qd.contiguous(), gd.contiguous(), n_g)  # full ranks (k = N)
         ranks = i.cpu().numpy().T.copy()
         mark("rank")
-        m = compute_map_and_print("roxford5k", "c2", "global", ranks, gnd)
+        import contextlib
+        with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
+            m = compute_map_and_print("roxford5k", "c2", "global", ranks, gnd)
         mark("map")
         return m
 
@@ -362,6 +380,9 @@ def main():
                          "640: 8985, 960: 9109, 1280: 9206 -- larger batches amortise the gallery sweep and fill "
                          "the conv grids' last rounds better)")
     ap.add_argument("--gallery", type=int, default=1_600_000)
+    ap.add_argument("--gallery-kind", choices=("gaussian", "clustered"), default="gaussian",
+                    help="gaussian: isotropic rows; clustered: 81,313 landmark-like classes (the prefilter's "
+                         "harder case: many rows near each query's top-k threshold)")
     ap.add_argument("--dim", type=int, default=2048)
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--arch", default="resnet101")
@@ -422,7 +443,7 @@ def main():
         return run_c2(a, world, rank, dev)
     t_setup = time.time()
     lo, hi = shard_bounds(a.gallery, world, rank)
-    gallery = make_gallery(a.gallery, a.dim, lo, hi, dev)
+    gallery = make_gallery(a.gallery, a.dim, lo, hi, dev, kind=a.gallery_kind)
     if a.workload == "c4":
         net = VisionTransformer(224, 16, 768, 12, 12, a.dim, dtype="bf16" if a.dtype != "fp32" else "fp32",
                                 state_dict=W.synthetic_vit_state_dict(out_dim=a.dim, seed=0), device=dev)
@@ -482,6 +503,7 @@ def main():
     for _ in range(a.warmup):
         out = step()
     torch.cuda.synchronize()
+    prefilter_stats = None
     if gal_bf is not None:  # the prefilter must reproduce the exhaustive fp32 ranking bit for bit
         d0 = embed()
         s_p, i_p = ops.cosine_topk_prefilter(d0, gallery, gal_bf, gal_bound, a.k, idx_offset=lo, workspace=ws)
@@ -490,6 +512,11 @@ def main():
         assert torch.equal(i_p, i_x) and torch.equal(s_p.view(torch.int32), s_x.view(torch.int32)), \
             "prefilter ranking differs from the exhaustive fp32 ranking"
         log("[rank 0] prefilter == exhaustive fp32 ranking on this batch (bit-exact)")
+        ops.cosine_topk_prefilter(d0, gallery, gal_bf, gal_bound, a.k, idx_offset=lo, workspace=ws)
+        surv = ops.prefilter_survivors(ws, q_total, hi - lo, a.dim, a.k).float()
+        prefilter_stats = {"bf16_filter_survivors_per_query": {"mean": round(surv.mean().item(), 1),
+                                                               "min": int(surv.min().item()),
+                                                               "max": int(surv.max().item())}}
     # sanity: a gallery row used as a query must come back first
     chk_s, chk_i = ops.cosine_topk(gallery[:2].contiguous(), gallery, 1, idx_offset=lo, workspace=ws)
     assert chk_i[:, 0].tolist() == [lo, lo + 1], chk_i
@@ -617,8 +644,9 @@ def main():
     res = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
            "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-           "data": "synthetic: uint8 224x224x3 images RandomState(1234+rank); seeded Gaussian L2-normalised "
-                   "gallery; seeded ResNet/whiten/PCA-w weights (no pretrained weights offline)",
+           "data": "synthetic: uint8 224x224x3 images RandomState(1234+rank); seeded "
+                   + ("Gaussian" if a.gallery_kind == "gaussian" else "clustered (81,313 classes)")
+                   + " L2-normalised gallery; seeded ResNet/whiten/PCA-w weights (no pretrained weights offline)",
            "config": {"workload": {"c3": f"C3: {a.arch}-GeM 2048-d + PCA-whiten",
                                    "c4": f"C4: ViT-B/16 CLS {a.dim}-d ({a.dtype} GEMMs + {a.dtype} cosine)",
                                    "c5": f"C5: {a.arch}-GeM+PCA-w at 3 scales, {a.dtype} cosine + alpha-QE "
@@ -634,7 +662,10 @@ def main():
     if exhaustive is not None:
         res["ranker"] = {"kind": "prefilter", "detail": "bf16-bound prefilter + exact fp32 rescoring; results "
                          "asserted bit-identical to the exhaustive fp32 ranker on a measured batch",
-                         "exhaustive_fp32": exhaustive}
+                         "gallery_kind": a.gallery_kind, "exhaustive_fp32": exhaustive,
+                         "sweep_ms_per_step": rk.get("cosine_filter", {}).get("ms_per_step"),
+                         "select_and_rescore_ms_per_step": rk.get("select", {}).get("ms_per_step"),
+                         **(prefilter_stats or {})}
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "c3":
         t = time.time()
         res["cpu_baseline"] = cpu_baseline(a.arch, a.gallery, a.dim, a.k)

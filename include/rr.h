@@ -154,6 +154,11 @@ int rr_prefilter_gallery_bound(rr_handle_t h, const float* gallery,
                                const void* gallery_bf16, long long n, int d,
                                double* bound3, void* stream);
 size_t rr_cosine_topk_prefilter_workspace_size(int nq, long long n, int d, int k);
+/* Byte offset, inside that workspace, of the int32 [nq] count of rows each
+ * query kept through the bf16 filter pass (the rows then bounded and, where
+ * they can still reach the top-k, rescored exactly); valid after a call with
+ * the same (nq, n, d, k) until the workspace is reused.  Diagnostics only. */
+size_t rr_cosine_topk_prefilter_counts_offset(int nq, long long n, int d, int k);
 int rr_cosine_topk_prefilter(rr_handle_t h, const float* queries, int nq,
                              const float* gallery, const void* gallery_bf16,
                              const double* bound3, long long n, int d, int k,

@@ -71,6 +71,7 @@ SIGNATURES = {
     "rr_alpha_qe": (_i, [_vp, _vp, _i, _vp, _ll, _i, _vp, _vp, _i, _i, _f, _ll, _vp, _vp]),
     "rr_prefilter_gallery_bound": (_i, [_vp, _vp, _vp, _ll, _i, _vp, _vp]),
     "rr_cosine_topk_prefilter_workspace_size": (_sz, [_i, _ll, _i, _i]),
+    "rr_cosine_topk_prefilter_counts_offset": (_sz, [_i, _ll, _i, _i]),
     "rr_cosine_topk_prefilter": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _ll, _i, _i, _ll, _vp, _vp, _vp, _sz, _vp]),
     "rr_pcaw_gram_workspace_size": (_sz, [_ll, _i]),
     "rr_pcaw_gram": (_i, [_vp, _vp, _ll, _i, _vp, _sz, _vp, _vp, _vp]),

@@ -179,6 +179,11 @@ size_t rr_cosine_topk_prefilter_workspace_size(int nq, long long n, int d, int k
   return prefilter_layout(nq, n > 0 ? n : 1, d, k).total;
 }
 
+size_t rr_cosine_topk_prefilter_counts_offset(int nq, long long n, int d, int k) {
+  if (nq < 0 || n < 0 || d <= 0 || k < 1) return 0;
+  return prefilter_layout(nq, n > 0 ? n : 1, d, k).off_cnt;
+}
+
 int rr_cosine_topk_prefilter(rr_handle_t h, const float* queries, int nq, const float* gallery,
                              const void* gallery_bf16, const double* bound3, long long n, int d, int k,
                              long long idx_offset, float* out_scores, long long* out_idx, void* workspace,

@@ -578,6 +578,13 @@ def cosine_topk_prefilter_workspace_size(nq, n, d, k):
     return int(_lib.lib().rr_cosine_topk_prefilter_workspace_size(nq, n, d, k))
 
 
+def prefilter_survivors(workspace, nq, n, d, k):
+    """Per-query count of rows that passed the bf16 filter in the last
+    cosine_topk_prefilter call on this workspace (int32 [nq], device)."""
+    off = int(_lib.lib().rr_cosine_topk_prefilter_counts_offset(int(nq), int(n), int(d), int(k)))
+    return workspace[off:off + 4 * int(nq)].view(torch.int32)
+
+
 def cosine_topk_prefilter(q, g, g_bf16, bound3, k, idx_offset=0, workspace=None):
     """Exact top-k (bit-identical to cosine_topk) via the bf16 prefilter."""
     _f32(q, "cosine_topk_prefilter q")
