@@ -67,17 +67,11 @@ int rr_get_device(rr_handle_t h, int* device);
  *   RR_TUNE_LP_CFG:   bf16/fp8 core, 1 (128x128), 2 (256x64), 3 (256x256),
  *                     4 (256x320 for filter / score sweeps, 256x256 otherwise)
  *   RR_TUNE_S3_CFG:   split-bf16 core, 1..6 (gemm_s3.hip tile table)
- *   RR_TUNE_S3_RESIDUAL: split-bf16 dense GEMMs with a residual: 1 = add it in
- *                     the epilogue, 2 = load it into the accumulators up front
- *   RR_TUNE_S3_VARIANT: split-bf16 k-loop variant bits (1: next k-tile's B
- *                     DMA spread between the MFMA groups)
  * Any other key or value: RR_EINVAL. */
 #define RR_TUNE_GEMM_CFG 1
 #define RR_TUNE_GEMM_BK 2
 #define RR_TUNE_LP_CFG 3
 #define RR_TUNE_S3_CFG 4
-#define RR_TUNE_S3_RESIDUAL 5
-#define RR_TUNE_S3_VARIANT 6
 int rr_set_tuning(rr_handle_t h, int key, int value);
 
 /* ---- search (ranker) ----------------------------------------------------

@@ -104,14 +104,7 @@ __device__ __forceinline__ void s3_launder(f32x4& v) { asm volatile("" : "+v"(v)
 // 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
 // 'DVFS give-back' item 7).  The k-tile's MFMAs go in two parts around the A
 // split: a0b0 + a1b1 + a0b1 + a1b0 (planes 0-1), then a0b2 + a2b0 (plane 2).
-// RESI: the residual is loaded into the large-term accumulator at the tile's
-// start (acc_hi = residual, then += a0b0 ...) instead of being read in the
-// epilogue: its HBM read overlaps the k-loop prologue and the epilogue is a
-// pure store.
-// SPREAD (MF16 only): the B LDS-DMA of the next k-tile is issued in pieces
-// between the first part's MFMA groups (each piece pinned by sched_barrier),
-// and the A loads of k-tile kt+2 after that part, instead of all up front.
-template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0, int RESI = 0, int SPREAD = 0>
+template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
   static_assert(!MF16 || BK == 32, "MF16: BK 32");
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
@@ -290,18 +283,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     const int n = min(n0 + r, g.N - 1);  // rows past N feed only unstored columns
     b_src[i] = Bp + p * g.b_plane + (long long)n * g.ldb + pswz<BK>(r, lane % SL) * 8;
   }
-  auto glds_b1 = [&](int kt, int buf, int i) {
-    uint16_t* lb = lds + buf * BUF + A_EL;
-    __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + (long long)kt * BK),
-                                     (__attribute__((address_space(3))) void*)(lb + min(i * NW + wave, B_TI - 1) * B_RPI * BK),
-                                     16, 0, 0);
-  };
   auto glds_b = [&](int kt, int buf) {
+    uint16_t* lb = lds + buf * BUF + A_EL;
     // every wave issues B_INS (the counted vmcnt assumes it): in a partial
     // last round the surplus waves repeat the last row group (same source,
     // same LDS destination)
 #pragma unroll
-    for (int i = 0; i < B_INS; ++i) glds_b1(kt, buf, i);
+    for (int i = 0; i < B_INS; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + (long long)kt * BK),
+                                       (__attribute__((address_space(3))) void*)(lb + min(i * NW + wave, B_TI - 1) * B_RPI * BK),
+                                       16, 0, 0);
   };
 
   f32x16 hi[FM][FN];
@@ -315,20 +306,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         hi[i][j][r] = 0.f;
         lo[i][j][r] = 0.f;
       }
-  // residual into the large-term accumulator (plain loads; the first counted
-  // vmcnt wait of the prologue covers them, being the oldest)
-  auto res_at = [&](int row, int col) -> float {
-    const int m = m0 + wm * WTM + row, n = n0 + wn * WTN + col;
-    return (m < g.M && n < g.N) ? g.residual[(long long)m * g.ldc + n] : 0.f;
-  };
-  if constexpr (RESI && !MF16) {
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) hi[i][j][r] = res_at(acc_row<false>(i, r, lane), acc_col<false>(j, r, lane));
-  }
 
   auto compute_st = [&](int cur, int st) {
     const uint16_t* la = lds + cur * BUF;
@@ -375,13 +352,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          if constexpr (RESI) {
-#pragma unroll
-            for (int e = 0; e < 4; ++e)
-              hi4[i][j][t][e] = res_at(acc_row<true>(i, 4 * t + e, lane), acc_col<true>(j, 4 * t + e, lane));
-          } else {
-            hi4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
+          hi4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
           lo4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
   }
@@ -407,23 +378,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       }
   };
 #define RR_MF16(a, b, c) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
-  // dma_kt >= 0 (SPREAD): the B pieces of k-tile dma_kt go out between the
-  // MFMA groups, B_INS spread over the FM*FN + 1 group boundaries
-  auto mf_part0 = [&](int cur, int dma_kt = -1, int dma_buf = 0) {
+  auto mf_part0 = [&](int cur) {
     if constexpr (MF16) {
-      constexpr int NG = FM * FN + 1;
-      int issued = 0;
-      auto dma_upto = [&](int slot) __attribute__((always_inline)) {
-        if constexpr (SPREAD) {
-          const int want = (B_INS * (slot + 1) + NG - 1) / NG;
-          while (issued < want && issued < B_INS) {
-            __builtin_amdgcn_sched_barrier(0);
-            glds_b1(dma_kt, dma_buf, issued);
-            __builtin_amdgcn_sched_barrier(0);
-            ++issued;
-          }
-        }
-      };
       rd_mf(cur, 0);
       rd_mf(cur, 1);
 #pragma unroll
@@ -432,19 +388,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int t = 0; t < 4; ++t) RR_MF16(fa[0][i][t >> 1], fb[0][j][t & 1], hi4[i][j][t]);
-      dma_upto(0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) {
+        for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
             RR_MF16(fa[1][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
             RR_MF16(fa[0][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
             RR_MF16(fa[1][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
           }
-          dma_upto(1 + i * FN + j);
-        }
     }
   };
   // with two A chunks per thread the plane-0 fragments are re-read in part 1
@@ -496,15 +449,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     auto iter = [&](int kt, int cur) __attribute__((always_inline)) {
-      if constexpr (SPREAD && MF16) {
-        mf_part0(cur, min(kt + 1, nk - 1), cur ^ 1);  // B DMA of kt+1 between the MFMA groups
-        load_a(min(kt + 2, nk - 1), cur);             // then the A loads of kt+2 (youngest)
-      } else {
-        glds_b(min(kt + 1, nk - 1), cur ^ 1);
-        load_a(min(kt + 2, nk - 1), cur);
-        if constexpr (MF16) mf_part0(cur);
-        else compute_st(cur, 0);
-      }
+      glds_b(min(kt + 1, nk - 1), cur ^ 1);
+      load_a(min(kt + 2, nk - 1), cur);
+      if constexpr (MF16) mf_part0(cur);
+      else compute_st(cur, 0);
       // A(kt+1) landed (the B DMA of kt+1 and the A loads of kt+2 may not
       // have): its split overlaps the remaining MFMAs of tile kt
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
@@ -550,23 +498,17 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 #pragma unroll
       for (int j = 0; j < FN; ++j) hi[i][j] += lo[i][j];
   }
-  if constexpr (RESI) {
-    GemmArgs ge = g;
-    ge.residual = nullptr;  // already in the accumulators
-    epilogue_store<WM, WN, FM, FN, BUF, (bool)MF16>(ge, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
-  } else {
-    epilogue_store<WM, WN, FM, FN, BUF, (bool)MF16>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
-  }
+  epilogue_store<WM, WN, FM, FN, BUF, (bool)MF16>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
 }
 
-template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int RESI = 0, int SPREAD = 0>
+template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0>
 static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16, RESI, SPREAD>), dim3((unsigned)nblk), dim3(64 * WM * WN),
+  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16>), dim3((unsigned)nblk), dim3(64 * WM * WN),
                      0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
@@ -605,24 +547,7 @@ static int pick_s3(const GemmArgs& g, int forced) {
 }
 
 template <int AM>
-static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int resi, int var) {
-  if ((var & 1) && pick_s3(g, forced) == 4) {
-    if (AM == A_DENSE && g.residual != nullptr && resi != 1) return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1, AM == A_DENSE, 1>(g, s);
-    return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1, 0, 1>(g, s);
-  }
-  if constexpr (AM == A_DENSE) {
-    // residual 1x1 convs: residual in the accumulators (resi 0 = default on, 1 = off, 2 = on)
-    if (g.residual != nullptr && resi != 1) {
-      switch (pick_s3(g, forced)) {
-        case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1, 0, 1>(g, s);
-        case 3: return launch_s3_t<4, 2, 2, 2, 32, AM, 1, 0, 1>(g, s);
-        case 4: return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1, 1>(g, s);
-        case 5: return launch_s3_t<4, 1, 2, 2, 32, AM, 1, 0, 1>(g, s);
-        case 6: return launch_s3_t<4, 1, 2, 2, 16, AM, 2, 0, 1>(g, s);
-        default: return launch_s3_t<2, 2, 2, 2, 16, AM, 2, 0, 1>(g, s);
-      }
-    }
-  }
+static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced) {
   switch (pick_s3(g, forced)) {
     case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1>(g, s);
     case 3: return launch_s3_t<4, 2, 2, 2, 32, AM, 1>(g, s);
@@ -649,10 +574,10 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
   hipError_t e;
   {
     TimedLaunch tl(h, timer_cls, s);
-    const int f = h->tune.s3_cfg, r = h->tune.s3_resi, v = h->tune.s3_var;
-    e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s, f, r, v)
-        : amode == A_CONV ? launch_s3_am<A_CONV>(g, s, f, r, v)
-                          : launch_s3_am<A_CONV_C4>(g, s, f, r, v);
+    const int f = h->tune.s3_cfg;
+    e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s, f)
+        : amode == A_CONV ? launch_s3_am<A_CONV>(g, s, f)
+                          : launch_s3_am<A_CONV_C4>(g, s, f);
   }
   return check_hip(h, e, "gemm_s3 launch");
 }

@@ -143,14 +143,6 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       if (value < 0 || value > 6) break;
       h->tune.s3_cfg = value;
       return RR_OK;
-    case RR_TUNE_S3_RESIDUAL:
-      if (value < 0 || value > 2) break;
-      h->tune.s3_resi = value;
-      return RR_OK;
-    case RR_TUNE_S3_VARIANT:
-      if (value < 0 || value > 1) break;
-      h->tune.s3_var = value;
-      return RR_OK;
     default:
       return set_error(h, RR_EINVAL, "rr_set_tuning: unknown key");
   }

@@ -18,8 +18,6 @@ struct rr_handle_s {
     int gemm_bk = 0;   // fp32 core k-tile depth: 16 or 32
     int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps)
     int s3_cfg = 0;    // split-bf16 core: 1..6 (gemm_s3.hip)
-    int s3_resi = 0;   // split-bf16 residual 1x1 convs: 0 default, 1 residual in the epilogue, 2 in the accumulators
-    int s3_var = 0;    // split-bf16 k-loop variants (bit 0: spread the B DMA between MFMA groups)
   } tune;
   // timing (see rr_timing_enable)
   bool timing = false;

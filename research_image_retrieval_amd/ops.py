@@ -304,8 +304,7 @@ def topk_merge(part_scores, part_idx, k_out):
 
 
 _TUNE_KEYS = {"gemm_cfg": _lib.TUNE_GEMM_CFG, "gemm_bk": _lib.TUNE_GEMM_BK, "lp_cfg": _lib.TUNE_LP_CFG,
-              "s3_cfg": _lib.TUNE_S3_CFG, "s3_residual": _lib.TUNE_S3_RESIDUAL,
-              "s3_variant": _lib.TUNE_S3_VARIANT}
+              "s3_cfg": _lib.TUNE_S3_CFG}
 
 
 class tuning:

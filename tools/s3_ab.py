@@ -1,7 +1,7 @@
 """Interleaved A/B of two rr_set_tuning settings on the split-bf16 convs that
 a setting affects: per shape, alternate the two settings REPS times each and
 report the median ms and the max |difference| of the outputs.
-usage: s3_ab.py KEY VA VB [B]   e.g. s3_ab.py s3_residual 1 2 1280"""
+usage: s3_ab.py KEY VA VB [B]   e.g. s3_ab.py s3_cfg 3 4 1280"""
 import os
 import statistics
 import sys
@@ -13,10 +13,8 @@ from research_image_retrieval_amd import ops  # noqa: E402
 
 key, va, vb = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
 B = int(sys.argv[4]) if len(sys.argv) > 4 else 1280
-SHAPES = {  # (h, cin, cout, k, stride, residual)
-    "s3_residual": [(14, 256, 1024, 1, 1, 1), (28, 128, 512, 1, 1, 1), (56, 64, 256, 1, 1, 1), (7, 512, 2048, 1, 1, 1)],
-}.get(key, [(14, 256, 1024, 1, 1, 1), (14, 1024, 256, 1, 1, 0), (14, 256, 256, 3, 1, 0), (56, 64, 64, 3, 1, 0),
-            (28, 128, 128, 3, 1, 0), (7, 512, 512, 3, 1, 0)])
+SHAPES = [(14, 256, 1024, 1, 1, 1), (14, 1024, 256, 1, 1, 0), (14, 256, 256, 3, 1, 0), (56, 64, 64, 3, 1, 0),
+          (28, 128, 128, 3, 1, 0), (7, 512, 512, 3, 1, 0)]  # (h, cin, cout, k, stride, residual)
 dev = torch.device("cuda:0")
 for h, cin, cout, k, s, res in SHAPES:
     p = k // 2
