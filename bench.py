@@ -399,6 +399,9 @@ def main():
     ap.add_argument("--conv-math", choices=("s3", "f32"), default="s3",
                     help="ResNet trunk convs: s3 = fp32-accurate 3-way bf16 split on the bf16 matrix cores "
                          "(error vs float64 <= the exact-fp32 core's, tests/test_gpu_s3.py); f32 = exact fp32 MFMA")
+    ap.add_argument("--ws-budget-gb", type=float, default=4.0,
+                    help="ranker workspace budget per rank (bounded candidate buffers, overflowed queries re-run; "
+                         "0 = the worst-case size, ~Q*N*8 bytes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c2-gallery", type=int, default=C2_GALLERY)
     ap.add_argument("--c2-queries", type=int, default=C2_QUERIES)
@@ -453,9 +456,14 @@ def main():
     imgs = torch.from_numpy(rs.randint(0, 256, size=(a.batch, 224, 224, 3), dtype=np.uint8)).to(dev)
     q_total = a.batch * world
     pre = a.ranker == "prefilter" and a.dtype == "fp32"
-    wsize = ops.cosine_topk_prefilter_workspace_size if pre else ops.cosine_topk_workspace_size
-    ws = torch.empty(wsize(q_total, hi - lo, a.dim, a.k), dtype=torch.uint8, device=dev)
-    sharded = ShardedGallery(gallery, lo, workspace=ws, dtype=a.dtype, prefilter=pre) if world > 1 else None
+    # ranker workspace: the worst case (every row a candidate, ~Q*N*8 bytes), or
+    # --ws-budget-gb of bounded candidate buffers (overflowed queries re-run)
+    ws_max = int(a.ws_budget_gb * (1 << 30)) if a.ws_budget_gb > 0 else None
+    ws_lo, ws_full = ops.ranker_workspace_bounds("prefilter" if pre else "exact", q_total, hi - lo, a.dim, a.k)
+    ws = torch.empty(ws_full if ws_max is None else max(ws_lo, min(ws_full, ws_max)), dtype=torch.uint8, device=dev)
+    counts = [a.batch] * world  # every rank's query count: the sharded search needs no size exchange
+    sharded = ShardedGallery(gallery, lo, workspace=ws, dtype=a.dtype, prefilter=pre,
+                             max_workspace_bytes=ws_max) if world > 1 else None
     gal_bf, gal_bound = (None, None)
     if pre and world == 1:
         gal_bf, _ = ops.quantize_rows(gallery, "bf16")
@@ -483,22 +491,26 @@ def main():
         desc = embed()
         if a.workload == "c5" and sharded is not None:
             # sharded alpha-QE: neighbour rows fetched from their owning shards (bit-identical to 1 GPU)
-            s2, i2, _ = sharded.alpha_qe_search(desc, a.k, n=2, alpha=3.0)
+            s2, i2, _ = sharded.alpha_qe_search(desc, a.k, n=2, alpha=3.0, counts=counts)
             return s2, i2
         if a.workload == "c5":
             q_lp, q_sc = ops.quantize_rows(desc, a.dtype)
-            s1, i1 = ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws)
+            s1, i1 = ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws,
+                                        max_workspace_bytes=ws_max)
             q2 = ops.alpha_qe(desc, gallery, i1, s1, n=2, alpha=3.0, idx_offset=lo)
             q_lp, q_sc = ops.quantize_rows(q2, a.dtype)
-            return ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws)
+            return ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws,
+                                      max_workspace_bytes=ws_max)
         if sharded is not None:
-            return sharded.search(desc, a.k)
+            return sharded.search(desc, a.k, counts)
         if gal_lp is not None:
             q_lp, q_sc = ops.quantize_rows(desc, a.dtype)
-            return ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws)
+            return ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws,
+                                      max_workspace_bytes=ws_max)
         if gal_bf is not None:
-            return ops.cosine_topk_prefilter(desc, gallery, gal_bf, gal_bound, a.k, idx_offset=lo, workspace=ws)
-        return ops.cosine_topk(desc, gallery, a.k, idx_offset=lo, workspace=ws)
+            return ops.cosine_topk_prefilter(desc, gallery, gal_bf, gal_bound, a.k, idx_offset=lo, workspace=ws,
+                                             max_workspace_bytes=ws_max)
+        return ops.cosine_topk(desc, gallery, a.k, idx_offset=lo, workspace=ws, max_workspace_bytes=ws_max)
 
     for _ in range(a.warmup):
         out = step()
@@ -521,7 +533,7 @@ def main():
     chk_s, chk_i = ops.cosine_topk(gallery[:2].contiguous(), gallery, 1, idx_offset=lo, workspace=ws)
     assert chk_i[:, 0].tolist() == [lo, lo + 1], chk_i
     if sharded is not None:  # the full sharded path: all-gather -> shard top-k -> all-to-all -> merge
-        ss, si = sharded.search(gallery[:2].contiguous(), a.k)
+        ss, si = sharded.search(gallery[:2].contiguous(), a.k, [2] * world)
         assert si[:, 0].tolist() == [lo, lo + 1], si[:, :3]
 
     timer = ops.KernelTimer(dev.index)
@@ -585,6 +597,24 @@ def main():
         flop_seed *= 2
     else:
         conv_flops_img = sum(W.resnet_conv_flops(a.arch, 224, 224).values()) + 2 * 2 * 2048 * 2048  # + whiten, PCA-w
+    conv_bytes_step, conv_floor_ms = None, None
+    if a.workload in ("c3", "c5"):
+        # per-layer algorithmic bytes (weights.resnet_conv_bytes) and the layer-wise
+        # roofline floor sum_l max(FLOP_l / peak, bytes_l / HBM peak) of the conv class
+        s3 = a.conv_math == "s3"
+        pk = PEAK_TFLOPS["s3" if s3 else "fp32"] * 1e12
+        conv_bytes_step, floor = 0.0, 0.0
+        for sc in (scales if a.workload == "c5" else (1.0,)):
+            hh = int(224.0 * sc)
+            fl_l = W.resnet_conv_flops(a.arch, hh, hh)
+            by_l = W.resnet_conv_bytes(a.arch, hh, hh, a.batch, weight_bytes=6 if s3 else 4)
+            for name in fl_l:
+                conv_bytes_step += by_l[name]
+                floor += max(fl_l[name] * a.batch / pk, by_l[name] / (PEAK_HBM_GBS * 1e9))
+            lin_by = 2 * (2 * a.batch * 2048 * 4 + 2048 * 2048 * 4)  # whiten + PCA-w (exact-fp32 core)
+            conv_bytes_step += lin_by
+            floor += max(2 * 2 * 2048 * 2048 * a.batch / (PEAK_TFLOPS["fp32"] * 1e12), lin_by / (PEAK_HBM_GBS * 1e9))
+        conv_floor_ms = floor * 1e3
     traffic = load_traffic()
     rk = {}
     rank_dt = "bf16" if pre else a.dtype  # the dtype the gallery sweep runs in
@@ -603,7 +633,7 @@ def main():
     attn_bytes = (12.0 * a.batch * 197 * 768 * (3 + 1) * (2 if attn_dt == "bf16" else 4)
                   if a.workload == "c4" else None)
     entries = (("cosine_filter", flop_filter, searches * float(rows_filter) * a.dim * esz, rank_dt),
-               ("conv_gemm", conv_flops_img * a.batch, None, conv_dt),
+               ("conv_gemm", conv_flops_img * a.batch, conv_bytes_step, conv_dt),
                ("cosine_seed", flop_seed, searches * float(s_rows) * a.dim * esz, rank_dt),
                ("attention", attn_flops_img * a.batch, attn_bytes, attn_dt))
     for name, fl_step, by_step, dt in entries:
@@ -633,6 +663,9 @@ def main():
                   "traffic": ((traffic or {}).get(name) or {}).get("hbm_bytes_per_launch")
                   if (traffic and traffic.get("workload") == a.workload and a.gallery == 1_600_000
                       and a.batch == traffic.get("batch", 320) and pre and a.conv_math == "s3") else None})
+        if name == "conv_gemm" and conv_floor_ms is not None:
+            e["layer_roofline_floor_ms_per_step"] = round(conv_floor_ms, 3)
+            e["frac_of_layer_floor"] = round(conv_floor_ms / (ms / a.steps), 4)
         rk[name] = e
     for name in ("select", "elementwise"):
         ms, n = cls[name]
@@ -657,7 +690,9 @@ def main():
                       "global_batch": q_total,
                       "images_per_gpu_per_step": a.batch, "gallery_rows": a.gallery, "dim": a.dim, "k": a.k,
                       "parallelism": f"query-dp{world} + gallery-shard{world}",
-                      "conv_math": a.conv_math if a.workload != "c4" else None},
+                      "conv_math": a.conv_math if a.workload != "c4" else None,
+                      "ranker_workspace_bytes_per_rank": int(ws.numel()),
+                      "ranker_workspace_worst_case_bytes": int(ws_full)},
            "roofline": roof, "roofline_by_kernel": rk}
     if exhaustive is not None:
         res["ranker"] = {"kind": "prefilter", "detail": "bf16-bound prefilter + exact fp32 rescoring; results "

@@ -65,7 +65,9 @@ int rr_get_device(rr_handle_t h, int* device);
  *   RR_TUNE_GEMM_CFG: exact-fp32 core tile, 22 (128x128), 41 (256x64), 88 (256x256)
  *   RR_TUNE_GEMM_BK:  exact-fp32 core k-tile depth, 16 or 32
  *   RR_TUNE_LP_CFG:   bf16/fp8 core, 1 (128x128), 2 (256x64), 3 (256x256),
- *                     4 (256x320 for filter / score sweeps, 256x256 otherwise)
+ *                     4 (256x320 for filter / score sweeps, 256x256 otherwise),
+ *                     5 (bf16 sweeps with K % 128 == 0: 256x256 8-phase pipeline;
+ *                     otherwise as 3)
  *   RR_TUNE_S3_CFG:   split-bf16 core, 1..6 (gemm_s3.hip tile table)
  * Any other key or value: RR_EINVAL. */
 #define RR_TUNE_GEMM_CFG 1
@@ -87,9 +89,30 @@ int rr_set_tuning(rr_handle_t h, int key, int value);
  *   If n < k the tail is filled with (-inf, -1).
  *   1 <= k <= 16384, d % 4 == 0, 16-byte aligned rows.
  * Workspace: rr_cosine_topk_workspace_size(nq, n, d, k) bytes of device
- * memory, any alignment >= 256.  The candidate buffer is sized for the worst
- * case, so RR_EOVERFLOW cannot occur with that size.                        */
+ * memory, any alignment >= 256.  That size holds a worst-case candidate
+ * buffer (every row of the gallery, per query: ~nq * n * 8 bytes), which can
+ * never overflow.
+ *
+ * Bounded workspaces (all three rankers: rr_cosine_topk, rr_cosine_topk_lp,
+ * rr_cosine_topk_prefilter with its _prefilter_ functions).  Any workspace of
+ * at least rr_cosine_topk_workspace_size_cap(nq, n, d, k, k) bytes is
+ * accepted; the ranker then keeps cap = rr_cosine_topk_cap_for(nq, n, d, k,
+ * workspace_bytes) candidates per query (cap >= k; workspace_size_cap(...,
+ * cap) gives the bytes for a chosen cap).  A query whose threshold filter
+ * passes more than cap rows gets an incomplete candidate set: its output row
+ * is NOT its exact top-k.  Every call zeroes and then sets the int32 at
+ * rr_cosine_topk_overflow_offset (device, inside the workspace) to the number
+ * of such queries; the int32 [nq] at rr_cosine_topk_counts_offset holds each
+ * query's count (> cap = overflowed).  The caller re-runs those queries, e.g.
+ * with a worst-case workspace for just them (ops.cosine_topk* with
+ * max_workspace_bytes do this).  The status cannot be returned synchronously:
+ * the counts exist only once the stream has run.  Offsets are valid for the
+ * same (nq, n, d, k) until the workspace is reused.                         */
 size_t rr_cosine_topk_workspace_size(int nq, long long n, int d, int k);
+size_t rr_cosine_topk_workspace_size_cap(int nq, long long n, int d, int k, long long cap);
+long long rr_cosine_topk_cap_for(int nq, long long n, int d, int k, size_t workspace_bytes);
+size_t rr_cosine_topk_counts_offset(int nq, long long n, int d, int k);
+size_t rr_cosine_topk_overflow_offset(int nq, long long n, int d, int k);
 int rr_cosine_topk(rr_handle_t h, const float* queries, int nq,
                    const float* gallery, long long n, int d, int k,
                    long long idx_offset, float* out_scores, long long* out_idx,
@@ -157,8 +180,13 @@ size_t rr_cosine_topk_prefilter_workspace_size(int nq, long long n, int d, int k
 /* Byte offset, inside that workspace, of the int32 [nq] count of rows each
  * query kept through the bf16 filter pass (the rows then bounded and, where
  * they can still reach the top-k, rescored exactly); valid after a call with
- * the same (nq, n, d, k) until the workspace is reused.  Diagnostics only. */
+ * the same (nq, n, d, k) until the workspace is reused. */
 size_t rr_cosine_topk_prefilter_counts_offset(int nq, long long n, int d, int k);
+/* Bounded workspaces, as for rr_cosine_topk (the count above > cap marks an
+ * overflowed query). */
+size_t rr_cosine_topk_prefilter_overflow_offset(int nq, long long n, int d, int k);
+size_t rr_cosine_topk_prefilter_workspace_size_cap(int nq, long long n, int d, int k, long long cap);
+long long rr_cosine_topk_prefilter_cap_for(int nq, long long n, int d, int k, size_t workspace_bytes);
 int rr_cosine_topk_prefilter(rr_handle_t h, const float* queries, int nq,
                              const float* gallery, const void* gallery_bf16,
                              const double* bound3, long long n, int d, int k,

@@ -42,6 +42,10 @@ SIGNATURES = {
     "rr_get_device": (_i, [_vp, ctypes.POINTER(_i)]),
     "rr_set_tuning": (_i, [_vp, _i, _i]),
     "rr_cosine_topk_workspace_size": (_sz, [_i, _ll, _i, _i]),
+    "rr_cosine_topk_workspace_size_cap": (_sz, [_i, _ll, _i, _i, _ll]),
+    "rr_cosine_topk_cap_for": (_ll, [_i, _ll, _i, _i, _sz]),
+    "rr_cosine_topk_counts_offset": (_sz, [_i, _ll, _i, _i]),
+    "rr_cosine_topk_overflow_offset": (_sz, [_i, _ll, _i, _i]),
     "rr_cosine_topk": (_i, [_vp, _vp, _i, _vp, _ll, _i, _i, _ll, _vp, _vp, _vp, _sz, _vp]),
     "rr_cosine_scores": (_i, [_vp, _vp, _i, _vp, _ll, _i, _vp, _vp]),
     "rr_topk_merge": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
@@ -72,6 +76,9 @@ SIGNATURES = {
     "rr_prefilter_gallery_bound": (_i, [_vp, _vp, _vp, _ll, _i, _vp, _vp]),
     "rr_cosine_topk_prefilter_workspace_size": (_sz, [_i, _ll, _i, _i]),
     "rr_cosine_topk_prefilter_counts_offset": (_sz, [_i, _ll, _i, _i]),
+    "rr_cosine_topk_prefilter_overflow_offset": (_sz, [_i, _ll, _i, _i]),
+    "rr_cosine_topk_prefilter_workspace_size_cap": (_sz, [_i, _ll, _i, _i, _ll]),
+    "rr_cosine_topk_prefilter_cap_for": (_ll, [_i, _ll, _i, _i, _sz]),
     "rr_cosine_topk_prefilter": (_i, [_vp, _vp, _i, _vp, _vp, _vp, _ll, _i, _i, _ll, _vp, _vp, _vp, _sz, _vp]),
     "rr_pcaw_gram_workspace_size": (_sz, [_ll, _i]),
     "rr_pcaw_gram": (_i, [_vp, _vp, _ll, _i, _vp, _sz, _vp, _vp, _vp]),

@@ -1,0 +1,262 @@
+// gemm_8p.hip — bf16 GEMM on a 256x256 tile with an 8-phase LDS-DMA pipeline
+// (cdna_hip_programming.md §5 'The 256² 8-phase template') for the long-K
+// cosine sweeps (iris_evaluate.py:383): the filter epilogue (survivors above
+// each query's threshold) and the transposed score store of the seed pass.
+// Measured (tools/sweep_ab.py, profiles/r02c_sweep_ab.txt): 1.22-1.25x the
+// 256x320 sweep tile at 256 / 512 / 768 queries x 1.6 M x 2048, 1.03x at 1280;
+// on the ViT linears (K = 768, stored C) it was 2-4 % slower than gemm_f32.hip's
+// 256x256 tile, so stored-C GEMMs do not come here.
+//
+// C[M,N] = A[M,K] . B[N,K]^T, bf16 in, fp32 accumulate, K % 128 == 0.
+// LDS: two k-tile buffers, each four 16 KB half-tiles (A rows 0-127, A rows
+// 128-255, B rows 0-127, B rows 128-255) of 128-B rows (64 bf16 = one k-tile),
+// 16-B slots XOR-swizzled by (row >> 1) & 7.  A k-tile is computed in four
+// phases, one 128x128 block quadrant each, in the order (A0,B0), (A0,B1),
+// (A1,B1), (A1,B0): every phase reads one A half and/or one B half from LDS
+// into registers, so each half-tile's last read is at a known phase and it can
+// be restaged two phases later.  8 waves (2 x 4) each own a 64x32 piece of
+// every quadrant (16 MFMAs of 16x16x32 per phase).
+//
+// Two k-tiles per iteration (phases P1..P8; even buffer in P1-P4, odd in
+// P5-P8).  Each phase issues exactly one half-tile (two global_load_lds per
+// thread):  P1: A1 of tile 2j+1, P2: B0 of 2j+1, P3: A0 of 2j+2, P4: B1 of
+// 2j+2, P5: A1 of 2j+2, P6: B0 of 2j+2, P7: A0 of 2j+3, P8: B1 of 2j+3 (tile
+// indices clamped to nk-1; a clamped copy lands in a half nobody reads again).
+// Every restage is >= 2 phases after that half's last ds_read (WAR).  RAW:
+// P4 waits vmcnt(4) (everything up to P2's loads landed: tile 2j+1 complete),
+// read from P5 on; P8 waits vmcnt(4) (up to P6: tile 2j+2 complete), read from
+// the next P1.  The counted waits never drain to 0 inside the loop, so the
+// DMA stays in flight across the raw barriers.
+#include "gemm_epilogue.hpp"
+#include "rr_internal.hpp"
+
+namespace rr {
+
+namespace {
+
+constexpr int P8_HALF = 128 * 128;  // bytes per half-tile (128 rows x 128 B)
+
+__device__ __forceinline__ int swz8(int row, int slot) { return slot ^ ((row >> 1) & 7); }
+
+template <int EM>
+__global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g, int tiles_n) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[8 * P8_HALF];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave & 1, wc = wave >> 1;  // 2 x 4 waves: 64 rows x 32 cols per quadrant
+  const int l16 = lane & 15, lg = lane >> 4;
+
+  // XCD-aware bijective block remap (blocks b, b+8, ... share an XCD)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tn = wgid % tiles_n, tm = wgid / tiles_n;
+  const int m0 = tm * 256, n0 = tn * 256;
+  const int nk = g.K / 64;  // even (K % 128 == 0, checked on the host)
+
+  // LDS-DMA sources: instruction i of wave w fills rows (i*8 + w)*8 .. +7 of a
+  // half, lane l -> row + l/8, physical slot l%8 (logical slot swz8 of it)
+  const uint16_t* src[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r = (i * 8 + wave) * 8 + (lane >> 3);
+      const bool isa = h < 2;
+      const int row = (isa ? m0 : n0) + (h & 1) * 128 + r;
+      const int lim = (isa ? g.M : g.N) - 1;
+      const uint16_t* base = reinterpret_cast<const uint16_t*>(isa ? g.A : g.B);
+      src[h][i] = base + (long long)min(row, lim) * (isa ? g.lda : g.ldb) + swz8(r, lane & 7) * 8;
+    }
+  auto stage = [&](int h, int kt, int buf) {
+    const int t = min(kt, nk - 1);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(src[h][i] + (long long)t * 64),
+          (__attribute__((address_space(3))) void*)(lds + (buf * 4 + h) * P8_HALF + (i * 8 + wave) * 8 * 128), 16, 0, 0);
+  };
+
+  f32x4 acc[4][4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b) acc[q][a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[4][2], fb[2][2];
+
+  auto read_a = [&](int buf, int ha) {
+    const unsigned char* base = lds + (buf * 4 + ha) * P8_HALF;
+#pragma unroll
+    for (int mg = 0; mg < 4; ++mg) {
+      const int row = wr * 64 + mg * 16 + l16;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fa[mg][s] = *reinterpret_cast<const bf16x8*>(base + row * 128 + swz8(row, 4 * s + lg) * 16);
+    }
+  };
+  auto read_b = [&](int buf, int hb) {
+    const unsigned char* base = lds + (buf * 4 + 2 + hb) * P8_HALF;
+#pragma unroll
+    for (int ng = 0; ng < 2; ++ng) {
+      const int row = wc * 32 + ng * 16 + l16;
+#pragma unroll
+      for (int s = 0; s < 2; ++s)
+        fb[ng][s] = *reinterpret_cast<const bf16x8*>(base + row * 128 + swz8(row, 4 * s + lg) * 16);
+    }
+  };
+  auto mfma_q = [&](int q) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mg = 0; mg < 4; ++mg)
+#pragma unroll
+        for (int ng = 0; ng < 2; ++ng)
+          acc[q][mg][ng] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mg][s], fb[ng][s], acc[q][mg][ng], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  auto sync_mid = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  };
+  auto sync_end = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // prologue: tile 0 (even) whole, then A0 and B1 of tile 1 (as P7/P8 would)
+  stage(0, 0, 0);
+  stage(1, 0, 0);
+  stage(2, 0, 0);
+  stage(3, 0, 0);
+  stage(0, 1, 1);
+  stage(3, 1, 1);
+  asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile 0 landed
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  for (int kt = 0; kt < nk; kt += 2) {
+    // P1: (A0,B0) of the even tile
+    read_a(0, 0);
+    read_b(0, 0);
+    stage(1, kt + 1, 1);
+    sync_mid();
+    mfma_q(0);
+    sync_end();
+    // P2: (A0,B1)
+    read_b(0, 1);
+    stage(2, kt + 1, 1);
+    sync_mid();
+    mfma_q(1);
+    sync_end();
+    // P3: (A1,B1)
+    read_a(0, 1);
+    stage(0, kt + 2, 0);
+    sync_mid();
+    mfma_q(2);
+    sync_end();
+    // P4: (A1,B0); the odd tile kt+1 has landed once P2's loads have
+    read_b(0, 0);
+    stage(3, kt + 2, 0);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    sync_mid();
+    mfma_q(3);
+    sync_end();
+    // P5-P8: the odd tile
+    read_a(1, 0);
+    read_b(1, 0);
+    stage(1, kt + 2, 0);
+    sync_mid();
+    mfma_q(0);
+    sync_end();
+    read_b(1, 1);
+    stage(2, kt + 2, 0);
+    sync_mid();
+    mfma_q(1);
+    sync_end();
+    read_a(1, 1);
+    stage(0, kt + 3, 1);
+    sync_mid();
+    mfma_q(2);
+    sync_end();
+    read_b(1, 0);
+    stage(3, kt + 3, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");  // tile kt+2 landed (P6's loads)
+    sync_mid();
+    mfma_q(3);
+    sync_end();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();  // the epilogue reuses the LDS
+
+  // acc[q][mg][ng][e]: row = qa*128 + wr*64 + mg*16 + 4*lg + e, col = qb*128 + wc*32 + ng*16 + l16
+  constexpr int QA[4] = {0, 0, 1, 1}, QB[4] = {0, 1, 1, 0};
+  if constexpr (EM == E_FILTER) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int ng = 0; ng < 2; ++ng) {
+        const int n = n0 + QB[q] * 128 + wc * 32 + ng * 16 + l16;
+        const bool nok = n < g.N;
+        const float t = nok ? g.tau[n] : __builtin_inff();
+#pragma unroll
+        for (int mg = 0; mg < 4; ++mg)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int m = m0 + QA[q] * 128 + wr * 64 + mg * 16 + 4 * lg + e;
+            const float v = acc[q][mg][ng][e];
+            if (nok && m < g.M && !(v <= t)) {
+              const int pos = atomicAdd(g.cnt + n, 1);
+              if (pos < g.cap) g.cand[(long long)n * g.cap + pos] = make_key(v, (uint32_t)(g.row_offset + m));
+            }
+          }
+      }
+  } else if constexpr (EM == E_SCORES_T) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int ng = 0; ng < 2; ++ng) {
+        const int n = n0 + QB[q] * 128 + wc * 32 + ng * 16 + l16;
+        if (n >= g.N) continue;
+#pragma unroll
+        for (int mg = 0; mg < 4; ++mg) {
+          const int mb = m0 + QA[q] * 128 + wr * 64 + mg * 16 + 4 * lg;
+          float* dst = g.C + (long long)n * g.ldc + mb;
+          if (mb + 3 < g.M) {
+            *reinterpret_cast<f32x4*>(dst) = acc[q][mg][ng];
+          } else {
+#pragma unroll
+            for (int e = 0; e < 4; ++e)
+              if (mb + e < g.M) dst[e] = acc[q][mg][ng][e];
+          }
+        }
+      }
+  }
+}
+
+}  // namespace
+
+// Host side: dense bf16 A and B, K % 128 == 0 (whole k-tile pairs), 16-B
+// aligned rows (checked by launch_gemm), no split-K / symmetric / scales.
+bool gemm_8p_eligible(const GemmArgs& g) {
+  return (g.K % 128) == 0 && g.k_split == 0 && !g.sym && g.scale_a == nullptr && g.scale_b == nullptr &&
+         (((uintptr_t)g.A | (uintptr_t)g.B) & 15) == 0;
+}
+
+hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s) {
+  const long long tiles_m = (g.M + 255) / 256, tiles_n = (g.N + 255) / 256;
+  const long long nblk = tiles_m * tiles_n;
+  if (nblk <= 0) return hipSuccess;
+  if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (emode == E_FILTER)
+    hipLaunchKernelGGL(gemm_8p_kernel<E_FILTER>, dim3((unsigned)nblk), dim3(512), 0, s, g, (int)tiles_n);
+  else if (emode == E_SCORES_T)
+    hipLaunchKernelGGL(gemm_8p_kernel<E_SCORES_T>, dim3((unsigned)nblk), dim3(512), 0, s, g, (int)tiles_n);
+  else
+    return hipErrorInvalidValue;  // stored C: the 256x256 tile of gemm_f32.hip (config 3)
+  return hipGetLastError();
+}
+
+}  // namespace rr

@@ -643,12 +643,16 @@ static hipError_t launch_cfg(const GemmArgs& g, hipStream_t s, const rr_handle_s
 //   4: 256x320, 8 waves of 64x160, 1/CU (144 KB) — a 320-query batch in
 //      one tile column: the streamed gallery is read exactly once (filter
 //      and score sweeps only)
+//   5: 256x256 on the 8-phase LDS-DMA pipeline of gemm_8p.hip (bf16, K %
+//      128 == 0; picked for long-K filter sweeps whose query count 256-wide
+//      panels tile better than 320-wide ones)
 // picked by estimated rounds x tile area (rr_set_tuning(RR_TUNE_LP_CFG) forces).
-// Not kept: an 8-phase 256x256 pipeline (2-4 % slower on the ViT
-// linears) and the 256x320 tile on a 4-stage 64-B-row LDS-DMA ring (7.59 vs
-// 6.94 ms per C3 sweep).
-static int pick_lp(const GemmArgs& g, int emode, const rr_handle_s::Tuning& tu) {
+// Not kept: the 8-phase pipeline for the ViT linears (2-4 %
+// slower: short K) and the 256x320 tile on a 4-stage 64-B-row LDS-DMA ring
+// (7.59 vs 6.94 ms per C3 sweep).
+static int pick_lp(const GemmArgs& g, int emode, bool dt_bf16, const rr_handle_s::Tuning& tu) {
   if (tu.lp_cfg >= 1 && tu.lp_cfg <= 3) return tu.lp_cfg;
+  if (tu.lp_cfg == 5) return emode == E_STORE ? 3 : 5;
   if (tu.lp_cfg == 4) return emode == E_STORE ? 3 : 4;
   // rounds x tile area / relative per-FLOP speed (measured, tools/lp_bench.py:
   // the 8-wave tiles run ViT linears 1.2-1.3x faster than 128x128; the
@@ -671,6 +675,12 @@ static int pick_lp(const GemmArgs& g, int emode, const rr_handle_s::Tuning& tu) 
     best = cost(256, 256, 256, 1.25), cfg = 3;
   if (emode != E_STORE && g.K >= 1024 && g.scale_a == nullptr && cost(256, 320, 256, 1.35) < best)
     best = cost(256, 320, 256, 1.35), cfg = 4;
+  // the 8-phase 256x256 pipeline (gemm_8p.hip) on the long-K bf16 sweeps:
+  // measured (tools/sweep_ab.py, random queries x 1.6 M x 2048) 1.22-1.25x the
+  // 256x320 tile at 256 / 512 / 768 queries (no padded query columns), 1.03x
+  // at 1280 and slower at 320 (256 + 64 padded); so it must win by padding
+  if (emode != E_STORE && dt_bf16 && g.K >= 1024 && (g.K % 128) == 0 && cost(256, 256, 256, 1.35 * 1.03) < best * 0.97)
+    best = cost(256, 256, 256, 1.35 * 1.03), cfg = 5;
   return cfg;
 }
 
@@ -681,8 +691,14 @@ template <int EM, int DT>
 static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s::Tuning& tu) {
   constexpr int EPR = DT == DT_BF16 ? 64 : 128;  // elements per 128-B k-tile row
   constexpr int MF = DT == DT_BF16 ? 1 : 0;
-  int cfg = pick_lp(g, EM, tu);
+  int cfg = pick_lp(g, EM, DT == DT_BF16, tu);
   if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles
+  if (cfg == 5) {
+    if constexpr (DT == DT_BF16) {
+      if (gemm_8p_eligible(g)) return launch_gemm_8p(g, EM, s);
+    }
+    cfg = 3;
+  }
   switch (cfg) {
     case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF>(g, s);
     case 3: return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);

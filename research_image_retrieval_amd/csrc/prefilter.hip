@@ -129,11 +129,12 @@ struct PrefilterWs {
 
 static inline size_t al256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-static PrefilterWs prefilter_layout(int nq, long long n, int d, int k) {
+static PrefilterWs prefilter_layout(int nq, long long n, int d, int k, long long cap = -1) {
   PrefilterWs w{};
   w.s = seed_sample_rows(n, k);
   w.ld = (w.s + 3) & ~3LL;
   w.cap = std::max<long long>(n, k);  // worst case: every row passes pass 1
+  if (cap >= 0 && cap < w.cap) w.cap = cap;  // bounded candidate buffer (rr.h)
   size_t o = 0;
   w.off_scores = o;
   o = al256(o + (size_t)nq * w.ld * 4);
@@ -184,6 +185,22 @@ size_t rr_cosine_topk_prefilter_counts_offset(int nq, long long n, int d, int k)
   return prefilter_layout(nq, n > 0 ? n : 1, d, k).off_cnt;
 }
 
+size_t rr_cosine_topk_prefilter_overflow_offset(int nq, long long n, int d, int k) {
+  if (nq < 0 || n < 0 || d <= 0 || k < 1) return 0;
+  return prefilter_layout(nq, n > 0 ? n : 1, d, k).off_ovf;
+}
+
+size_t rr_cosine_topk_prefilter_workspace_size_cap(int nq, long long n, int d, int k, long long cap) {
+  if (nq < 0 || n < 0 || d <= 0 || k < 1 || cap < k) return 0;
+  return prefilter_layout(nq, n > 0 ? n : 1, d, k, cap).total;
+}
+
+long long rr_cosine_topk_prefilter_cap_for(int nq, long long n, int d, int k, size_t workspace_bytes) {
+  if (nq <= 0 || n < 0 || d <= 0 || k < 1) return 0;
+  const PrefilterWs L = prefilter_layout(nq, n > 0 ? n : 1, d, k);
+  return workspace_bytes >= L.total ? L.cap : cap_that_fits(L.off_cand, nq, workspace_bytes, L.cap);
+}
+
 int rr_cosine_topk_prefilter(rr_handle_t h, const float* queries, int nq, const float* gallery,
                              const void* gallery_bf16, const double* bound3, long long n, int d, int k,
                              long long idx_offset, float* out_scores, long long* out_idx, void* workspace,
@@ -197,10 +214,14 @@ int rr_cosine_topk_prefilter(rr_handle_t h, const float* queries, int nq, const 
     return set_error(h, RR_EINVAL, "rr_cosine_topk_prefilter: null pointer");
   if (((uintptr_t)queries & 15) || ((uintptr_t)gallery & 15) || ((uintptr_t)gallery_bf16 & 15))
     return set_error(h, RR_EINVAL, "rr_cosine_topk_prefilter: buffers must be 16-byte aligned");
-  const PrefilterWs L = prefilter_layout(nq, n > 0 ? n : 1, d, k);
+  PrefilterWs L = prefilter_layout(nq, n > 0 ? n : 1, d, k);
+  if (workspace && workspace_bytes < L.total) {  // bounded candidate buffer
+    const long long cap = cap_that_fits(L.off_cand, nq, workspace_bytes, L.cap);
+    if (cap >= k) L = prefilter_layout(nq, n > 0 ? n : 1, d, k, cap);
+  }
   if (!workspace || workspace_bytes < L.total)
-    return set_error(h, RR_EWORKSPACE,
-                     "rr_cosine_topk_prefilter: workspace too small (query rr_cosine_topk_prefilter_workspace_size)");
+    return set_error(h, RR_EWORKSPACE, "rr_cosine_topk_prefilter: workspace too small (at least "
+                                       "rr_cosine_topk_prefilter_workspace_size_cap(..., k))");
   hipStream_t s = (hipStream_t)stream;
   char* ws = (char*)workspace;
   float* scores_t = (float*)(ws + L.off_scores);

@@ -49,11 +49,12 @@ struct TopkWs {
   size_t off_scores, off_tau, off_cnt, off_ovf, off_cand, total;
 };
 
-static TopkWs topk_layout(int nq, long long n, int k) {
+static TopkWs topk_layout(int nq, long long n, int k, long long cap = -1) {
   TopkWs w{};
   w.s = seed_rows(n, k);
   w.ld = (w.s + 3) & ~3LL;
   w.cap = k + (n - w.s);  // worst case: every non-seed row passes its threshold
+  if (cap >= 0 && cap < w.cap) w.cap = cap;  // bounded candidate buffer (rr.h)
   size_t o = 0;
   w.off_scores = o;
   o = align256(o + (size_t)nq * w.ld * 4);
@@ -136,7 +137,7 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.gemm_bk = value;
       return RR_OK;
     case RR_TUNE_LP_CFG:
-      if (value < 0 || value > 4) break;
+      if (value < 0 || value > 5) break;
       h->tune.lp_cfg = value;
       return RR_OK;
     case RR_TUNE_S3_CFG:
@@ -174,6 +175,31 @@ size_t rr_cosine_topk_workspace_size(int nq, long long n, int d, int k) {
   return topk_layout(nq, n > 0 ? n : 1, k).total;
 }
 
+size_t rr_cosine_topk_workspace_size_cap(int nq, long long n, int d, int k, long long cap) {
+  (void)d;
+  if (nq <= 0 || k <= 0 || cap < k) return 0;
+  return topk_layout(nq, n > 0 ? n : 1, k, cap).total;
+}
+
+long long rr_cosine_topk_cap_for(int nq, long long n, int d, int k, size_t workspace_bytes) {
+  (void)d;
+  if (nq <= 0 || k <= 0) return 0;
+  const TopkWs L = topk_layout(nq, n > 0 ? n : 1, k);
+  return workspace_bytes >= L.total ? L.cap : cap_that_fits(L.off_cand, nq, workspace_bytes, L.cap);
+}
+
+size_t rr_cosine_topk_counts_offset(int nq, long long n, int d, int k) {
+  (void)d;
+  if (nq <= 0 || k <= 0) return 0;
+  return topk_layout(nq, n > 0 ? n : 1, k).off_cnt;
+}
+
+size_t rr_cosine_topk_overflow_offset(int nq, long long n, int d, int k) {
+  (void)d;
+  if (nq <= 0 || k <= 0) return 0;
+  return topk_layout(nq, n > 0 ? n : 1, k).off_ovf;
+}
+
 }  // extern "C"
 
 namespace rr {
@@ -191,9 +217,14 @@ static int cosine_topk_impl(rr_handle_t h, const void* queries, const float* q_s
   if (((uintptr_t)queries & 15) || ((uintptr_t)gallery & 15))
     return set_error(h, RR_EINVAL, "rr_cosine_topk: queries/gallery must be 16-byte aligned");
   const int es = dt == DT_F32 ? 4 : (dt == DT_BF16 ? 2 : 1);
-  const TopkWs L = topk_layout(nq, n > 0 ? n : 1, k);
+  TopkWs L = topk_layout(nq, n > 0 ? n : 1, k);
+  if (workspace && workspace_bytes < L.total) {  // bounded candidate buffer
+    const long long cap = cap_that_fits(L.off_cand, nq, workspace_bytes, L.cap);
+    if (cap >= k) L = topk_layout(nq, n > 0 ? n : 1, k, cap);
+  }
   if (!workspace || workspace_bytes < L.total)
-    return set_error(h, RR_EWORKSPACE, "rr_cosine_topk: workspace too small (query rr_cosine_topk_workspace_size)");
+    return set_error(h, RR_EWORKSPACE,
+                     "rr_cosine_topk: workspace too small (at least rr_cosine_topk_workspace_size_cap(..., k))");
   char* ws = (char*)workspace;
   float* scores_t = (float*)(ws + L.off_scores);
   float* tau = (float*)(ws + L.off_tau);

@@ -16,7 +16,7 @@ struct rr_handle_s {
   struct Tuning {
     int gemm_cfg = 0;  // fp32 core: 22, 41 or 88
     int gemm_bk = 0;   // fp32 core k-tile depth: 16 or 32
-    int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps)
+    int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 sweeps)
     int s3_cfg = 0;    // split-bf16 core: 1..6 (gemm_s3.hip)
   } tune;
   // timing (see rr_timing_enable)
@@ -133,6 +133,16 @@ inline long long seed_sample_rows(long long n, int k) {
   return n < s ? n : s;
 }
 
+// Candidate capacity per query that a workspace of `bytes` holds when the
+// candidate buffer [nq][cap] of 8-byte keys starts at `off_cand` (256-aligned)
+// and the layout's total is rounded up to 256 B; at most `worst`.
+inline long long cap_that_fits(size_t off_cand, int nq, size_t bytes, long long worst) {
+  const size_t usable = bytes & ~(size_t)255;
+  if (nq <= 0 || usable <= off_cand) return 0;
+  const long long cap = (long long)((usable - off_cand) / ((size_t)nq * 8));
+  return cap < worst ? cap : worst;
+}
+
 enum AMode { A_DENSE = 0, A_CONV = 1, A_CONV_GENERIC = 2, A_CONV_C4 = 3 };
 enum EMode { E_STORE = 0, E_SCORES_T = 1, E_FILTER = 2 };
 enum DType { DT_F32 = 0, DT_BF16 = 1, DT_FP8 = 2 };
@@ -178,6 +188,10 @@ int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStre
 // fp32-accurate GEMM on bf16 MFMA (gemm_s3.hip): A fp32 (A_DENSE or A_CONV),
 // B = bf16 planes [3][N][ldb] from launch_split3, E_STORE epilogue
 int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls);
+
+// bf16 256x256 8-phase pipeline (gemm_8p.hip): dense A/B, K % 128 == 0
+bool gemm_8p_eligible(const GemmArgs& g);
+hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s);
 int launch_split3(rr_handle_s* h, const float* x, long long n, uint16_t* planes, hipStream_t s);
 
 // ---- top-k kernels (topk.hip) -------------------------------------------

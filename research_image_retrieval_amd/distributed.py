@@ -48,16 +48,24 @@ def _host_staged(group):
     return dist.get_backend(group) == "gloo"
 
 
-def _all_gather_var(t, group):
-    """all_gather of tensors whose first dim may differ across ranks."""
+def _all_gather_var(t, group, sizes=None):
+    """all_gather of tensors whose first dim may differ across ranks.  With
+    `sizes` (every rank's first dim, known to all ranks, e.g. a fixed batch)
+    no size exchange and no host sync happen; otherwise one small all-gather
+    and one device->host read."""
     world = dist.get_world_size(group)
     dev = t.device
     if _host_staged(group):
         t = t.cpu()
-    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
-    sizes = [torch.zeros_like(n) for _ in range(world)]
-    dist.all_gather(sizes, n, group=group)
-    sizes = [int(s.item()) for s in sizes]
+    if sizes is None:
+        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+        parts = [torch.zeros_like(n) for _ in range(world)]
+        dist.all_gather(parts, n, group=group)
+        sizes = torch.cat(parts).tolist()
+    else:
+        sizes = [int(x) for x in sizes]
+        if len(sizes) != world or sizes[dist.get_rank(group)] != t.shape[0]:
+            raise ValueError(f"_all_gather_var: sizes {sizes} do not match this rank's {t.shape[0]} rows")
     mx = max(sizes)
     pad = t.new_zeros((mx,) + tuple(t.shape[1:]))
     pad[: t.shape[0]] = t
@@ -70,9 +78,12 @@ class ShardedGallery:
     """This rank's shard of a gallery that is row-partitioned over the group."""
 
     def __init__(self, shard, global_offset, group=None, local_topk=None, merge=None, workspace=None, dtype="fp32",
-                 prefilter=False):
+                 prefilter=False, max_workspace_bytes=None):
         """dtype "fp32" ranks exactly; prefilter=True gives the same exact
-        result through the bf16-bound prefilter (rr_cosine_topk_prefilter)."""
+        result through the bf16-bound prefilter (rr_cosine_topk_prefilter).
+        max_workspace_bytes bounds the ranker workspace (rr.h "Bounded
+        workspaces"; overflowed queries are re-run, results unchanged)."""
+        self.max_ws = max_workspace_bytes
         self.shard = shard
         self.offset = int(global_offset)
         # rr_topk_merge keys carry 32-bit row indices (0xffffffff reserved)
@@ -94,18 +105,15 @@ class ShardedGallery:
         if self._local_topk is not None:
             return self._local_topk(q, self.shard, k, self.offset)
         n, d = self.shard.shape[0], q.shape[1]
-        need = (ops.cosine_topk_prefilter_workspace_size if self.prefilter else ops.cosine_topk_workspace_size)(
-            q.shape[0], n, d, k)
-        if self._ws is None or self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=q.device)
+        self._ws, _ = ops._ranker_workspace("prefilter" if self.prefilter else "exact", q.shape[0], n, d, k,
+                                            self._ws, self.max_ws, q.device)
+        kw = dict(idx_offset=self.offset, workspace=self._ws, max_workspace_bytes=self.max_ws)
         if self.prefilter:
-            return ops.cosine_topk_prefilter(q, self.shard, self.shard_lp, self.bound, k, idx_offset=self.offset,
-                                             workspace=self._ws)
+            return ops.cosine_topk_prefilter(q, self.shard, self.shard_lp, self.bound, k, **kw)
         if self.dtype != "fp32":
             q_lp, q_sc = ops.quantize_rows(q, self.dtype)
-            return ops.cosine_topk_lp(q_lp, q_sc, self.shard_lp, self.shard_scale, k, self.dtype,
-                                      idx_offset=self.offset, workspace=self._ws)
-        return ops.cosine_topk(q, self.shard, k, idx_offset=self.offset, workspace=self._ws)
+            return ops.cosine_topk_lp(q_lp, q_sc, self.shard_lp, self.shard_scale, k, self.dtype, **kw)
+        return ops.cosine_topk(q, self.shard, k, **kw)
 
     def _bounds(self):
         """[lo_r, hi_r) of every rank's shard (all-gathered once)."""
@@ -122,49 +130,51 @@ class ShardedGallery:
         """Rank whose shard holds each global row index (shards are contiguous, in rank order)."""
         return torch.bucketize(idx, self._bounds(), right=True)
 
-    def gather_rows(self, idx):
+    def gather_rows(self, idx, counts=None):
         """Rows g[idx] of the global gallery for this rank's queries: idx
         [B_r, n] int64 (global rows; < 0 = padding -> a zero row) -> [B_r, n, D]
         fp32, each row an exact copy from the shard that owns it (one
-        variable-split all-to-all)."""
+        variable-split all-to-all).  counts: every rank's B_r when known (no
+        size exchange); the split sizes then cost one device->host read."""
         group = self.group
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
         dev = self.shard.device
         b, n = idx.shape
         d = self.shard.shape[1]
-        ids, sizes = _all_gather_var(idx.contiguous(), group)
-        send, send_counts = [], []
-        for t in range(world):
-            it = ids[t].reshape(-1).to(dev)
-            # padding slots (idx < 0: fewer gallery rows than neighbours) have no owner
-            sel = (it >= 0) & (self._owner(it.clamp_min(0)) == rank)
-            mine = it[sel] - self.offset  # row-major (query, neighbour) order
-            send.append(self.shard.index_select(0, mine))
-            send_counts.append(int(mine.numel()))
+        ids, sizes = _all_gather_var(idx.contiguous(), group, counts)
+        # every rank's requests, requesting-rank-major, (query, neighbour) order within
+        req = torch.cat([x.reshape(-1).to(dev) for x in ids]) if ids else idx.new_empty((0,)).to(dev)
+        seg = torch.cat([torch.full((sz * n,), r, dtype=torch.int64, device=dev) for r, sz in enumerate(sizes)])
+        # padding slots (idx < 0: fewer gallery rows than neighbours) have no owner
+        mine = (req >= 0) & (self._owner(req.clamp_min(0)) == rank)
+        skey = torch.where(mine, seg, torch.full_like(seg, world))  # rows to send, grouped by requester
+        send_order = torch.argsort(skey, stable=True)
         flat = idx.reshape(-1).to(dev)
-        own = torch.where(flat >= 0, self._owner(flat.clamp_min(0)), torch.full_like(flat, -1))
-        recv_counts = [int((own == r).sum().item()) for r in range(world)]
-        sendbuf = torch.cat(send, 0) if send else self.shard.new_empty((0, d))
-        recvbuf = self.shard.new_empty((sum(recv_counts), d))
+        own = torch.where(flat >= 0, self._owner(flat.clamp_min(0)), torch.full_like(flat, world))
+        recv_order = torch.argsort(own, stable=True)  # own slots grouped by owner rank
+        ones = torch.ones_like(skey)
+        counts2 = torch.stack([torch.zeros(world + 1, dtype=torch.int64, device=dev).scatter_add_(0, skey, ones),
+                               torch.zeros(world + 1, dtype=torch.int64, device=dev).scatter_add_(
+                                   0, own, torch.ones_like(own))]).cpu()  # the one host sync
+        send_counts, recv_counts = counts2[0, :world].tolist(), counts2[1, :world].tolist()
+        n_send, n_recv = sum(send_counts), sum(recv_counts)
+        sendbuf = self.shard.index_select(0, req[send_order[:n_send]] - self.offset)
+        recvbuf = self.shard.new_empty((n_recv, d))
         if _host_staged(group):
             sendbuf, recvbuf = sendbuf.cpu(), recvbuf.cpu()
         dist.all_to_all_single(recvbuf, sendbuf.contiguous(), recv_counts, send_counts, group=group)
-        recvbuf = recvbuf.to(dev)
         out = self.shard.new_zeros((b * n, d))  # padding slots stay zero (and get weight 0)
-        start = 0
-        for r in range(world):
-            pos = torch.nonzero(own == r).reshape(-1)
-            out[pos] = recvbuf[start:start + recv_counts[r]]
-            start += recv_counts[r]
+        out.index_copy_(0, recv_order[:n_recv], recvbuf.to(dev))
         return out.view(b, n, d)
 
-    def alpha_qe_search(self, queries, k=100, n=2, alpha=3.0, expand=None):
+    def alpha_qe_search(self, queries, k=100, n=2, alpha=3.0, expand=None, counts=None):
         """Search, alpha-QE this rank's queries with their top-n neighbours
         (rows fetched from their owning shards), search again (config C5).
-        Returns (scores [B_r,k], global idx [B_r,k], expanded queries)."""
-        s, i = self.search(queries, max(k, n))
-        rows = self.gather_rows(i[:, :n].contiguous())
+        Returns (scores [B_r,k], global idx [B_r,k], expanded queries).
+        counts: every rank's query count when known (see search)."""
+        s, i = self.search(queries, max(k, n), counts)
+        rows = self.gather_rows(i[:, :n].contiguous(), counts)
         top_s = s[:, :n].contiguous()
         b = queries.shape[0]
         if b == 0:  # no queries on this rank: still take part in the collectives
@@ -174,7 +184,7 @@ class ShardedGallery:
         else:
             local = torch.arange(b * n, dtype=torch.int64, device=queries.device).view(b, n)
             q2 = ops.alpha_qe(queries.contiguous(), rows.view(b * n, rows.shape[-1]), local, top_s, n=n, alpha=alpha)
-        s2, i2 = self.search(q2, k)
+        s2, i2 = self.search(q2, k, counts)
         return s2, i2, q2
 
     def _merge_parts(self, ps, pi, k):
@@ -182,12 +192,15 @@ class ShardedGallery:
             return self._merge(ps, pi, k)
         return ops.topk_merge(ps, pi, k)
 
-    def search(self, queries, k):
-        """queries [B_r, D] (this rank's) -> (scores [B_r,k], global idx [B_r,k])."""
+    def search(self, queries, k, counts=None):
+        """queries [B_r, D] (this rank's) -> (scores [B_r,k], global idx [B_r,k]).
+        counts: every rank's B_r, when all ranks know them (a fixed batch):
+        then the search has no host sync (the merge and the collectives stay
+        on the stream); without, one size all-gather + one host read."""
         group = self.group
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
-        qs, sizes = _all_gather_var(queries.contiguous(), group)
+        qs, sizes = _all_gather_var(queries.contiguous(), group, counts)
         allq = torch.cat(qs, 0).contiguous()
         s, i = self._local(allq, k)
         # each rank needs only its own queries' partial lists: all-to-all

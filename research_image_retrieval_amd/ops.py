@@ -253,8 +253,71 @@ def cosine_topk_workspace_size(nq, n, d, k):
     return int(_lib.lib().rr_cosine_topk_workspace_size(int(nq), int(n), int(d), int(k)))
 
 
-def cosine_topk(queries, gallery, k, idx_offset=0, workspace=None):
-    """Exact stable top-k of queries [nq,D] against gallery [N,D] -> (scores [nq,k] fp32, idx [nq,k] int64)."""
+# ---- bounded ranker workspaces (rr.h "Bounded workspaces") ----------------
+# kind -> C functions: worst-case size, size for a cap, cap for a size,
+# per-query counts offset, overflow-count offset
+_WS_FUNCS = {
+    "exact": ("rr_cosine_topk_workspace_size", "rr_cosine_topk_workspace_size_cap", "rr_cosine_topk_cap_for",
+              "rr_cosine_topk_counts_offset", "rr_cosine_topk_overflow_offset"),
+    "prefilter": ("rr_cosine_topk_prefilter_workspace_size", "rr_cosine_topk_prefilter_workspace_size_cap",
+                  "rr_cosine_topk_prefilter_cap_for", "rr_cosine_topk_prefilter_counts_offset",
+                  "rr_cosine_topk_prefilter_overflow_offset"),
+}
+
+
+def _wsf(kind, i):
+    return getattr(_lib.lib(), _WS_FUNCS[kind][i])
+
+
+def ranker_workspace_bounds(kind, nq, n, d, k):
+    """(minimum bytes = a cap of k candidates per query, worst-case bytes) of
+    a ranker workspace; kind 'exact' (cosine_topk / cosine_topk_lp) or
+    'prefilter'."""
+    a = (int(nq), int(n), int(d), int(k))
+    return int(_wsf(kind, 1)(*a, int(k))), int(_wsf(kind, 0)(*a))
+
+
+def _ranker_workspace(kind, nq, n, d, k, workspace, max_workspace_bytes, device):
+    """The workspace a ranker call runs with: the caller's if large enough,
+    else a new one of the worst-case size or, with max_workspace_bytes, of at
+    most that many bytes (never below the k-candidate minimum).  Returns
+    (workspace, bounded)."""
+    lo, full = ranker_workspace_bounds(kind, nq, n, d, k)
+    budget = full if max_workspace_bytes is None else max(lo, min(full, int(max_workspace_bytes)))
+    if workspace is None or workspace.numel() < budget:
+        workspace = torch.empty(budget, dtype=torch.uint8, device=device)
+    return workspace, workspace.numel() < full
+
+
+def _recover_overflow(kind, nq, n, d, k, workspace, rerun, os_, oi):
+    """After a bounded-workspace call: re-run every query whose candidates
+    overflowed the buffer (rr.h) with a worst-case workspace for just those
+    queries, in chunks that fit the same workspace, and write their rows.
+    rerun(query_index_tensor, workspace) -> (scores, idx).  One device->host
+    read of the overflow count (a stream sync); returns the re-run count."""
+    a = (int(nq), int(n), int(d), int(k))
+    ovf_off = int(_wsf(kind, 4)(*a))
+    if int(workspace[ovf_off:ovf_off + 4].view(torch.int32).item()) == 0:
+        return 0
+    cap = int(_wsf(kind, 2)(*a, workspace.numel()))
+    cnt_off = int(_wsf(kind, 3)(*a))
+    bad = torch.nonzero(workspace[cnt_off:cnt_off + 4 * int(nq)].view(torch.int32) > cap).flatten()
+    c = max(1, bad.numel())
+    while c > 1 and int(_wsf(kind, 0)(c, int(n), int(d), int(k))) > workspace.numel():
+        c = (c + 1) // 2
+    need = int(_wsf(kind, 0)(c, int(n), int(d), int(k)))
+    ws = workspace if need <= workspace.numel() else torch.empty(need, dtype=torch.uint8, device=workspace.device)
+    for part in bad.split(c):
+        s_, i_ = rerun(part, ws)
+        os_[part] = s_
+        oi[part] = i_
+    return int(bad.numel())
+
+
+def cosine_topk(queries, gallery, k, idx_offset=0, workspace=None, max_workspace_bytes=None):
+    """Exact stable top-k of queries [nq,D] against gallery [N,D] -> (scores [nq,k] fp32, idx [nq,k] int64).
+    max_workspace_bytes: run with a bounded candidate buffer (rr.h) and re-run
+    overflowed queries; results are identical either way."""
     _f32(queries, "cosine_topk queries")
     _f32(gallery, "cosine_topk gallery")
     dev = _dev(queries)
@@ -262,15 +325,16 @@ def cosine_topk(queries, gallery, k, idx_offset=0, workspace=None):
     n = gallery.shape[0]
     if gallery.shape[1] != d:
         raise ValueError("cosine_topk: descriptor dims differ")
-    need = cosine_topk_workspace_size(nq, n, d, k)
-    if workspace is None or workspace.numel() < need:
-        workspace = torch.empty(need, dtype=torch.uint8, device=queries.device)
+    workspace, bounded = _ranker_workspace("exact", nq, n, d, k, workspace, max_workspace_bytes, queries.device)
     os_ = torch.empty((nq, k), dtype=torch.float32, device=queries.device)
     oi = torch.empty((nq, k), dtype=torch.int64, device=queries.device)
     hd = _lib.handle(dev)
     _lib.check(_lib.lib().rr_cosine_topk(hd, _ptr(queries), nq, _ptr(gallery), n, d, k, int(idx_offset), _ptr(os_),
                                          _ptr(oi), _ptr(workspace), workspace.numel(), _stream(dev)), hd,
                "rr_cosine_topk")
+    if bounded and nq > 0:
+        _recover_overflow("exact", nq, n, d, k, workspace,
+                          lambda r, ws: cosine_topk(queries[r].contiguous(), gallery, k, idx_offset, ws), os_, oi)
     return os_, oi
 
 
@@ -451,8 +515,9 @@ def _lp_rows(t, sc, dtype, name):
             raise ValueError(f"{name}: fp8 rows need contiguous fp32 scales, one per row")
 
 
-def cosine_topk_lp(q, q_scale, g, g_scale, k, dtype, idx_offset=0, workspace=None):
-    """Fused top-k on bf16 / fp8 rows (fp32 accumulate); scores dequantised."""
+def cosine_topk_lp(q, q_scale, g, g_scale, k, dtype, idx_offset=0, workspace=None, max_workspace_bytes=None):
+    """Fused top-k on bf16 / fp8 rows (fp32 accumulate); scores dequantised.
+    max_workspace_bytes: bounded candidate buffer, as in cosine_topk."""
     if dtype not in _LP:
         raise ValueError("cosine_topk_lp: dtype must be 'bf16' or 'fp8'")
     _lp_rows(q, q_scale, dtype, "cosine_topk_lp queries")
@@ -463,15 +528,18 @@ def cosine_topk_lp(q, q_scale, g, g_scale, k, dtype, idx_offset=0, workspace=Non
     dt = _LP[dtype]
     nq, d = q.shape
     n = g.shape[0]
-    need = cosine_topk_workspace_size(nq, n, d, k)
-    if workspace is None or workspace.numel() < need:
-        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    workspace, bounded = _ranker_workspace("exact", nq, n, d, k, workspace, max_workspace_bytes, q.device)
     os_ = torch.empty((nq, k), dtype=torch.float32, device=q.device)
     oi = torch.empty((nq, k), dtype=torch.int64, device=q.device)
     hd = _lib.handle(dev)
     _lib.check(_lib.lib().rr_cosine_topk_lp(hd, _ptr(q), _ptr(q_scale), nq, _ptr(g), _ptr(g_scale), n, d, dt, k,
                                             int(idx_offset), _ptr(os_), _ptr(oi), _ptr(workspace), workspace.numel(),
                                             _stream(dev)), hd, "rr_cosine_topk_lp")
+    if bounded and nq > 0:
+        _recover_overflow("exact", nq, n, d, k, workspace,
+                          lambda r, ws: cosine_topk_lp(q[r].contiguous(), None if q_scale is None else
+                                                       q_scale[r].contiguous(), g, g_scale, k, dtype, idx_offset, ws),
+                          os_, oi)
     return os_, oi
 
 
@@ -585,20 +653,24 @@ def prefilter_survivors(workspace, nq, n, d, k):
     return workspace[off:off + 4 * int(nq)].view(torch.int32)
 
 
-def cosine_topk_prefilter(q, g, g_bf16, bound3, k, idx_offset=0, workspace=None):
-    """Exact top-k (bit-identical to cosine_topk) via the bf16 prefilter."""
+def cosine_topk_prefilter(q, g, g_bf16, bound3, k, idx_offset=0, workspace=None, max_workspace_bytes=None):
+    """Exact top-k (bit-identical to cosine_topk) via the bf16 prefilter.
+    max_workspace_bytes: bounded candidate buffer + re-run of overflowed
+    queries, as in cosine_topk."""
     _f32(q, "cosine_topk_prefilter q")
     _f32(g, "cosine_topk_prefilter g")
     dev = _dev(q)
     nq, d = q.shape
     n = g.shape[0]
-    need = cosine_topk_prefilter_workspace_size(nq, n, d, k)
-    if workspace is None or workspace.numel() < need:
-        workspace = torch.empty(need, dtype=torch.uint8, device=q.device)
+    workspace, bounded = _ranker_workspace("prefilter", nq, n, d, k, workspace, max_workspace_bytes, q.device)
     s = torch.empty((nq, k), dtype=torch.float32, device=q.device)
     i = torch.empty((nq, k), dtype=torch.int64, device=q.device)
     hd = _lib.handle(dev)
     _lib.check(_lib.lib().rr_cosine_topk_prefilter(hd, _ptr(q), nq, _ptr(g), _ptr(g_bf16), _ptr(bound3), n, d, k,
                                                    int(idx_offset), _ptr(s), _ptr(i), _ptr(workspace),
                                                    workspace.numel(), _stream(dev)), hd, "rr_cosine_topk_prefilter")
+    if bounded and nq > 0:
+        _recover_overflow("prefilter", nq, n, d, k, workspace,
+                          lambda r, ws: cosine_topk_prefilter(q[r].contiguous(), g, g_bf16, bound3, k, idx_offset, ws),
+                          s, i)
     return s, i

@@ -229,6 +229,40 @@ def resnet_conv_flops(arch, h, w, stride_on="3x3"):
     return flops
 
 
+def resnet_conv_bytes(arch, h, w, batch, stride_on="3x3", weight_bytes=6):
+    """Algorithmic HBM bytes of every trunk conv launch for `batch` h x w
+    images (the same layer walk as resnet_conv_flops): the fp32 NHWC input map
+    read once (the stem's NHWC4 image: 4 channels), the fp32 output written
+    once, the block's fp32 identity read once by the residual conv3, and the
+    weights once per launch (`weight_bytes` per parameter: 6 = the split-bf16
+    core's three bf16 planes, 4 = fp32)."""
+    def out(x, k, s, p):
+        return (x + 2 * p - k) // s + 1
+
+    by = {}
+    H, Wd = out(h, 7, 2, 3), out(w, 7, 2, 3)
+    by["conv1"] = batch * (h * w * 4 + H * Wd * 64) * 4 + 64 * 7 * 7 * 4 * weight_bytes
+    H, Wd = out(H, 3, 2, 1), out(Wd, 3, 2, 1)
+    inplanes = 64
+    for li, nb in enumerate(RESNET_LAYERS[arch]):
+        planes = 64 * 2 ** li
+        for bi in range(nb):
+            s = 2 if (bi == 0 and li > 0) else 1
+            s1, s2 = block_strides(s, stride_on)
+            p = f"layer{li + 1}.{bi}"
+            H1, W1 = out(H, 1, s1, 0), out(Wd, 1, s1, 0)
+            Ho, Wo = out(H1, 3, s2, 1), out(W1, 3, s2, 1)
+            x_in = H * Wd * inplanes
+            if bi == 0:
+                by[p + ".downsample.0"] = batch * (x_in + Ho * Wo * planes * 4) * 4 + planes * 4 * inplanes * weight_bytes
+            by[p + ".conv1"] = batch * (x_in + H1 * W1 * planes) * 4 + planes * inplanes * weight_bytes
+            by[p + ".conv2"] = batch * (H1 * W1 * planes + Ho * Wo * planes) * 4 + planes * planes * 9 * weight_bytes
+            by[p + ".conv3"] = batch * (Ho * Wo * planes + 2 * Ho * Wo * planes * 4) * 4 + \
+                planes * 4 * planes * weight_bytes
+            H, Wd, inplanes = Ho, Wo, planes * 4
+    return by
+
+
 def synthetic_vit_state_dict(width=768, layers=12, heads=12, patch=16, res=224, out_dim=512, seed=0):
     """Seeded CLIP-layout ViT weights (networks/model.py:206-243 key names)."""
     rs = np.random.RandomState(seed)

@@ -135,7 +135,9 @@ static void gpu_checks() {
   EXPECT(rr_cosine_topk(h, q, nq, g, n, 6, k, 0, os, oi, ws, ws_n, nullptr) == RR_EINVAL);      // d % 4
   EXPECT(rr_cosine_topk(h, q, nq, g, n, d, 0, 0, os, oi, ws, ws_n, nullptr) == RR_EINVAL);      // k
   EXPECT(rr_cosine_topk(h, q, nq, g, n, d, 20000, 0, os, oi, ws, ws_n, nullptr) == RR_EINVAL);  // k > 16384
-  EXPECT(rr_cosine_topk(h, q, nq, g, n, d, k, 0, os, oi, ws, ws_n - 1, nullptr) == RR_EWORKSPACE);
+  const size_t ws_min = rr_cosine_topk_workspace_size_cap(nq, n, d, k, k);  // bounded: k candidates per query
+  EXPECT(ws_min > 0 && ws_min < ws_n && rr_cosine_topk_cap_for(nq, n, d, k, ws_n) > k);
+  EXPECT(rr_cosine_topk(h, q, nq, g, n, d, k, 0, os, oi, ws, ws_min - 1, nullptr) == RR_EWORKSPACE);
   EXPECT(rr_cosine_topk(h, q, nq, nullptr, n, d, k, 0, os, oi, ws, ws_n, nullptr) == RR_EINVAL);
   EXPECT(rr_cosine_topk(h, q + 1, nq, g, n, d, k, 0, os, oi, ws, ws_n, nullptr) == RR_EINVAL);  // misaligned
   EXPECT(rr_cosine_topk(h, q, nq, g, 0x100000000LL, d, k, 0, os, oi, ws, ws_n, nullptr) == RR_EINVAL);
@@ -156,6 +158,24 @@ static void gpu_checks() {
   HIPCHK(hipMemcpy(hs.data(), os, hs.size() * 4, hipMemcpyDeviceToHost));
   for (int i = 0; i < nq; ++i)
     for (int r = 0; r + 1 < k; ++r) EXPECT(hs[i * k + r] >= hs[i * k + r + 1] && hi[i * k + r] >= 100);
+  // bounded workspaces: room for 400 candidates per query is plenty here (no
+  // overflow, same result); room for k is not (the overflow int counts it)
+  {
+    int ovf = -1;
+    const size_t b400 = rr_cosine_topk_workspace_size_cap(nq, n, d, k, 400);
+    // (the 256-B rounding of the workspace may leave room for a few more)
+    const long long c400 = rr_cosine_topk_cap_for(nq, n, d, k, b400);
+    EXPECT(c400 >= 400 && rr_cosine_topk_workspace_size_cap(nq, n, d, k, c400) == b400);
+    EXPECT(rr_cosine_topk(h, q, nq, g, n, d, k, 100, os, oi, ws, b400, nullptr) == RR_OK);
+    HIPCHK(hipMemcpy(&ovf, ws + rr_cosine_topk_overflow_offset(nq, n, d, k), 4, hipMemcpyDeviceToHost));
+    std::vector<long long> hb(nq * k);
+    HIPCHK(hipMemcpy(hb.data(), oi, hb.size() * 8, hipMemcpyDeviceToHost));
+    EXPECT(ovf == 0 && hb == hi);
+    EXPECT(rr_cosine_topk(h, q, nq, g, n, d, k, 100, os, oi, ws, ws_min, nullptr) == RR_OK);
+    HIPCHK(hipMemcpy(&ovf, ws + rr_cosine_topk_overflow_offset(nq, n, d, k), 4, hipMemcpyDeviceToHost));
+    EXPECT(ovf > 0 && ovf <= nq);
+    EXPECT(rr_cosine_topk(h, q, nq, g, n, d, k, 100, os, oi, ws, ws_n, nullptr) == RR_OK);  // restore os / oi
+  }
   uint16_t* gb = dmalloc<uint16_t>((size_t)n * d);
   double* b3 = dmalloc<double>(3);
   EXPECT(rr_quantize_rows(h, g, n, d, 1, gb, nullptr, nullptr) == RR_OK);
@@ -164,7 +184,8 @@ static void gpu_checks() {
   char* pws = dmalloc<char>(pw_n);
   float* os2 = dmalloc<float>(nq * k);
   long long* oi2 = dmalloc<long long>(nq * k);
-  EXPECT(rr_cosine_topk_prefilter(h, q, nq, g, gb, b3, n, d, k, 100, os2, oi2, pws, pw_n - 8, nullptr) ==
+  const size_t pw_min = rr_cosine_topk_prefilter_workspace_size_cap(nq, n, d, k, k);
+  EXPECT(rr_cosine_topk_prefilter(h, q, nq, g, gb, b3, n, d, k, 100, os2, oi2, pws, pw_min - 8, nullptr) ==
          RR_EWORKSPACE);
   EXPECT(rr_cosine_topk_prefilter(h, q, nq, g, gb, b3, n, d, k, 100, os2, oi2, pws, pw_n, nullptr) == RR_OK);
   std::vector<long long> hi2(nq * k);

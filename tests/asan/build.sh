@@ -10,7 +10,7 @@ HERE=$(cd "$(dirname "$0")" && pwd)
 ROOT=$(cd "$HERE/../.." && pwd)
 OUT=$HERE/out
 mkdir -p "$OUT"
-SRC="rr_api.hip gemm_f32.hip topk.hip embed_ops.hip vit_ops.hip lowp_ops.hip pcaw_ops.hip prefilter.hip gemm_s3.hip"
+SRC=$(sed -n 's/^SRCS := //p' "$ROOT/research_image_retrieval_amd/csrc/Makefile")  # the product library's sources
 SAN="-Xarch_host -fsanitize=address -Xarch_host -fno-omit-frame-pointer"
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 gcc -O1 -g -fsanitize=address,undefined -fno-omit-frame-pointer -ffp-contract=off -std=c11 \

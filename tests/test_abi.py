@@ -49,3 +49,35 @@ def test_handle_entry_points_without_gpu():
     out = ctypes.c_void_p()
     assert L.rr_create(-1, ctypes.byref(out)) != _lib.RR_OK and not out.value
     assert L.rr_create(1 << 20, ctypes.byref(out)) != _lib.RR_OK and not out.value
+
+
+def test_bounded_workspace_arithmetic():
+    """Bounded ranker workspaces (rr.h): sizes grow with the candidate cap,
+    the cap a workspace affords round-trips, the worst case caps at every row,
+    and below k candidates per query nothing fits (0)."""
+    L = _lib.lib()
+    for kind, pre in (("exact", "rr_cosine_topk"), ("prefilter", "rr_cosine_topk_prefilter")):
+        size = getattr(L, pre + "_workspace_size")
+        size_cap = getattr(L, pre + "_workspace_size_cap")
+        cap_for = getattr(L, pre + "_cap_for")
+        cnt_off = getattr(L, pre + "_counts_offset")
+        ovf_off = getattr(L, pre + "_overflow_offset")
+        nq, n, d, k = 1280, 1_600_000, 2048, 100
+        full = size(nq, n, d, k)
+        lo = size_cap(nq, n, d, k, k)
+        assert 0 < lo < full and size_cap(nq, n, d, k, k - 1) == 0
+        worst = cap_for(nq, n, d, k, full)
+        assert worst >= n - 32768 and size_cap(nq, n, d, k, worst) == full
+        for cap in (k, 4096, 65_536, 1_000_000):
+            b = size_cap(nq, n, d, k, cap)
+            assert cap_for(nq, n, d, k, b) == cap and cap_for(nq, n, d, k, b + 255) == cap
+            assert cap_for(nq, n, d, k, b - 1) < cap
+            # nq * 8 not a divisor of 256: the rounding may leave room for a few more
+            c5 = cap_for(5, n, d, k, size_cap(5, n, d, k, cap))
+            assert cap <= c5 < cap + 7 and size_cap(5, n, d, k, c5) == size_cap(5, n, d, k, cap)
+        assert cap_for(nq, n, d, k, lo - 1) < k
+        # counts and the overflow flag sit before the candidate buffer: the same
+        # offsets for every cap
+        assert 0 < cnt_off(nq, n, d, k) < lo and 0 < ovf_off(nq, n, d, k) < lo
+        # 2 GB instead of the ~16 GB worst case at the C3 shape
+        assert cap_for(nq, n, d, k, 2 << 30) > 100_000

@@ -41,6 +41,14 @@ def _worker(rank, world, port, q_all, g_all, k, sizes, out):
     sg = ShardedGallery(g_all[lo:hi].contiguous(), lo, local_topk=_local_topk, merge=_merge)
     qlo = sum(sizes[:rank])
     s, i = sg.search(q_all[qlo:qlo + sizes[rank]].contiguous(), k)
+    # every rank's query count known up front: no size exchange, same result
+    s_c, i_c = sg.search(q_all[qlo:qlo + sizes[rank]].contiguous(), k, counts=sizes)
+    assert torch.equal(s, s_c) and torch.equal(i, i_c)
+    try:
+        sg.search(q_all[qlo:qlo + sizes[rank]].contiguous(), k, counts=sizes[::-1])
+        raise AssertionError("mismatched counts accepted")
+    except ValueError:
+        pass
     out[rank] = (s.numpy(), i.numpy())
     dist.barrier()
     dist.destroy_process_group()
@@ -86,6 +94,8 @@ def _qe_worker(rank, world, port, q_all, g_all, k, sizes, out):
     # first row, a padding slot (idx -1: fewer gallery rows than neighbours), last row
     rows = sg.gather_rows(torch.tensor([[0, -1, g_all.shape[0] - 1]] * sizes[rank], dtype=torch.int64).view(-1, 3))
     s, i, q2 = sg.alpha_qe_search(mine, k, n=3, alpha=3.0, expand=_expand)
+    s_c, i_c, q2_c = sg.alpha_qe_search(mine, k, n=3, alpha=3.0, expand=_expand, counts=sizes)
+    assert torch.equal(s, s_c) and torch.equal(i, i_c) and torch.equal(q2, q2_c)
     out[rank] = (s.numpy(), i.numpy(), q2.numpy(), rows.numpy())
     dist.barrier()
     dist.destroy_process_group()

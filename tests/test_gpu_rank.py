@@ -129,6 +129,22 @@ def test_prefilter_bitexact_random(cuda, nq, n, d, k):
     assert np.array_equal(i, i_o) and np.array_equal(s, s_o)
 
 
+@pytest.mark.parametrize("nq", [256, 768])
+def test_prefilter_query_panels_of_256(cuda, nq):
+    """Query counts that tile into 256-wide panels send the bf16 sweep to the
+    8-phase 256x256 pipeline (gemm_8p.hip) by default: still bit-identical to
+    the exhaustive fp32 ranker (itself oracle-pinned above)."""
+    rs = np.random.RandomState(nq)
+    d = 2048
+    g = rs.standard_normal((120_000, d)).astype(np.float32)
+    q = rs.standard_normal((nq, d)).astype(np.float32)
+    g[77_777] = q[3]  # a planted exact match
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    s, i = _prefilter_vs_exhaustive(cuda, q, g, 100)
+    assert i[3, 0] == 77_777
+
+
 def test_prefilter_bitexact_ties_and_clusters(cuda):
     """Exact ties (duplicate rows on both sides of the seed boundary), planted
     near-duplicates, and a dense cluster where thousands of rows score within
@@ -208,3 +224,56 @@ def test_alpha_qe_skips_padding_and_foreign_indices(cuda):
     keep = np.where((idx >= 100) & (idx < 150), idx, -1)
     ref = oracle.alpha_qe(q, g, keep, sc, n=2, alpha=3.0, idx_offset=100)
     np.testing.assert_allclose(out, ref, rtol=0, atol=2e-6)
+
+
+def test_bounded_workspace_overflow_recovery(cuda):
+    """Bounded candidate buffers (rr.h): with room for 2000 candidates per
+    query, a query facing a 30k-row cluster overflows (counted in the
+    workspace's overflow int, its raw row wrong); the ops wrappers re-run it
+    and every ranker's output equals the worst-case-workspace run bit for bit."""
+    from research_image_retrieval_amd import _lib
+    rs = np.random.RandomState(3)
+    n, d, k = 60_000, 256, 100
+    g = rs.standard_normal((n, d)).astype(np.float32)
+    base = rs.standard_normal(d).astype(np.float32)
+    g[20_000:50_000] = base + 0.05 * rs.standard_normal((30_000, d)).astype(np.float32)  # past the seed rows
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    rq = rs.standard_normal((5, d)).astype(np.float32)
+    bh = base / np.linalg.norm(base)
+    rq -= (rq @ bh)[:, None] * bh[None]  # orthogonal to the cluster: these queries never overflow
+    q = np.concatenate([base[None], rq])
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    qd, gd = torch.from_numpy(q).to(cuda), torch.from_numpy(g).to(cuda)
+    nq = q.shape[0]
+    L = _lib.lib()
+    budget = L.rr_cosine_topk_workspace_size_cap(nq, n, d, k, 2000)
+    assert budget < L.rr_cosine_topk_workspace_size(nq, n, d, k) // 10
+    # raw C call on the bounded workspace: the overflow is reported, not hidden
+    ws = torch.empty(budget, dtype=torch.uint8, device=cuda)
+    s_raw = torch.empty((nq, k), dtype=torch.float32, device=cuda)
+    i_raw = torch.empty((nq, k), dtype=torch.int64, device=cuda)
+    hd = _lib.handle(cuda.index)
+    _lib.check(L.rr_cosine_topk(hd, qd.data_ptr(), nq, gd.data_ptr(), n, d, k, 0, s_raw.data_ptr(), i_raw.data_ptr(),
+                                ws.data_ptr(), budget, torch.cuda.current_stream(cuda).cuda_stream), hd, "topk")
+    off = L.rr_cosine_topk_overflow_offset(nq, n, d, k)
+    assert ws[off:off + 4].view(torch.int32).item() == 1
+    cnt = ws[L.rr_cosine_topk_counts_offset(nq, n, d, k):][:4 * nq].view(torch.int32).cpu()
+    assert cnt[0] > 2000 and (cnt[1:] <= 2000).all()
+
+    s0, i0 = ops.cosine_topk(qd, gd, k)
+    assert not torch.equal(i_raw[0], i0[0]) and torch.equal(i_raw[1:], i0[1:])
+    s1, i1 = ops.cosine_topk(qd, gd, k, max_workspace_bytes=budget)
+    assert torch.equal(i1, i0) and torch.equal(s1.view(torch.int32), s0.view(torch.int32))
+    s_o, i_o = oracle.cosine_topk(q, g, k)
+    assert np.array_equal(i0.cpu().numpy(), i_o) and np.array_equal(s0.cpu().numpy(), s_o)
+
+    gb, _ = ops.quantize_rows(gd, "bf16")
+    bound = ops.prefilter_gallery_bound(gd, gb)
+    pbudget = L.rr_cosine_topk_prefilter_workspace_size_cap(nq, n, d, k, 2000)
+    s2, i2 = ops.cosine_topk_prefilter(qd, gd, gb, bound, k, max_workspace_bytes=pbudget)
+    assert torch.equal(i2, i0) and torch.equal(s2.view(torch.int32), s0.view(torch.int32))
+
+    qb, _ = ops.quantize_rows(qd, "bf16")
+    s3, i3 = ops.cosine_topk_lp(qb, None, gb, None, k, "bf16")
+    s4, i4 = ops.cosine_topk_lp(qb, None, gb, None, k, "bf16", max_workspace_bytes=budget)
+    assert torch.equal(i3, i4) and torch.equal(s3, s4)
