@@ -236,21 +236,15 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     for (int i = 0; i < A_CH; ++i) {
       uint32_t h[8], m[8], l[8];
 #pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        // split3 on a pair: the subtractions as one v_pk_add_f32 each
-        const f32x2 x = {ra[i][e >> 2][e & 3], ra[i][e >> 2][(e & 3) + 1]};
-        const f32x2 xh = {__uint_as_float(__float_as_uint(x[0]) & 0xffff0000u),
-                          __uint_as_float(__float_as_uint(x[1]) & 0xffff0000u)};
-        const f32x2 r1 = x - xh;
-        const f32x2 r1h = {__uint_as_float(__float_as_uint(r1[0]) & 0xffff0000u),
-                           __uint_as_float(__float_as_uint(r1[1]) & 0xffff0000u)};
-        const f32x2 r2 = r1 - r1h;
-        h[e] = __float_as_uint(x[0]);  // pack2 keeps only the high halves
-        h[e + 1] = __float_as_uint(x[1]);
-        m[e] = __float_as_uint(r1[0]);
-        m[e + 1] = __float_as_uint(r1[1]);
-        l[e] = __float_as_uint(r2[0]);
-        l[e + 1] = __float_as_uint(r2[1]);
+      for (int e = 0; e < 8; ++e) {
+        // scalar f32 subtractions: packed v_pk_add_f32 beside MFMAs costs
+        // more issue time than two v_sub_f32 (MI355X_MICROARCH.md constants)
+        const float x = ra[i][e >> 2][e & 3];
+        const float r1 = x - __uint_as_float(__float_as_uint(x) & 0xffff0000u);
+        const float r2 = r1 - __uint_as_float(__float_as_uint(r1) & 0xffff0000u);
+        h[e] = __float_as_uint(x);  // pack2 keeps only the high halves
+        m[e] = __float_as_uint(r1);
+        l[e] = __float_as_uint(r2);
       }
       pk[i][0] = u32x4{pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
       pk[i][1] = u32x4{pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7])};
@@ -378,7 +372,33 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       }
   };
 #define RR_MF16(a, b, c) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
-  auto mf_part0 = [&](int cur) {
+  // k-tile of MFMAs in two parts.  lo1: the plane-1 products (a1b1, a0b1,
+  // a1b0) into lo; rest: a0b0 into hi, then the plane-2 products (a0b2,
+  // a2b0) into lo — the same per-accumulator order as one pass — with the A
+  // split + LDS store of the next stage interleaved one VALU per MFMA (the
+  // plane-1 fragments are dead by then, which leaves the registers for it).
+  auto mf_lo1 = [&](int cur) {
+    if constexpr (MF16) {
+      rd_mf(cur, 0);
+      rd_mf(cur, 1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            RR_MF16(fa[1][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
+            RR_MF16(fa[0][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
+            RR_MF16(fa[1][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
+          }
+    }
+  };
+  // with two A chunks per thread the plane-0 fragments are re-read for the
+  // plane-2 products rather than held across the A split (holding them spills)
+  constexpr bool MF_REREAD = A_CH >= 2;
+  // dense A (1x1 convs, linears): a0b0 + the plane-1 products, then the
+  // split, then the plane-2 products (the order above measured slower there)
+  auto mf_dense0 = [&](int cur) {
     if constexpr (MF16) {
       rd_mf(cur, 0);
       rd_mf(cur, 1);
@@ -400,10 +420,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
           }
     }
   };
-  // with two A chunks per thread the plane-0 fragments are re-read in part 1
-  // rather than held across the A split (holding them spills)
-  constexpr bool MF_REREAD = A_CH >= 2;
-  auto mf_part1 = [&](int cur) {
+  auto mf_dense1 = [&](int cur) {
     if constexpr (MF16) {
       if constexpr (MF_REREAD) rd_mf(cur, 0);
       rd_mf(cur, 2);
@@ -416,6 +433,34 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
             RR_MF16(fa[0][i][t >> 1], fb[2][j][t & 1], lo4[i][j][t]);
             RR_MF16(fa[2][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
           }
+    }
+  };
+  auto mf_rest = [&](int cur, int nxt) {
+    if constexpr (MF16) {
+      split_a(nxt);
+      write_a(nxt);  // the other stage is free since the last barrier
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) RR_MF16(fa[0][i][t >> 1], fb[0][j][t & 1], hi4[i][j][t]);
+      if constexpr (MF_REREAD) rd_mf(cur, 0);
+      rd_mf(cur, 2);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            RR_MF16(fa[0][i][t >> 1], fb[2][j][t & 1], lo4[i][j][t]);
+            RR_MF16(fa[2][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
+          }
+#pragma unroll
+      for (int x = 0; x < 3 * FM * FN * 4; ++x) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // 1 VALU
+      }
     }
   };
 #undef RR_MF16
@@ -451,20 +496,32 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     auto iter = [&](int kt, int cur) __attribute__((always_inline)) {
       glds_b(min(kt + 1, nk - 1), cur ^ 1);
       load_a(min(kt + 2, nk - 1), cur);
-      if constexpr (MF16) mf_part0(cur);
-      else compute_st(cur, 0);
-      // A(kt+1) landed (the B DMA of kt+1 and the A loads of kt+2 may not
-      // have): its split overlaps the remaining MFMAs of tile kt
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
-      launder_a(cur ^ 1);
-      split_a(cur ^ 1);
-      if constexpr (MF16) {
-        mf_part1(cur);
+      if constexpr (MF16 && AMODE == A_DENSE) {
+        mf_dense0(cur);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
+        launder_a(cur ^ 1);
+        split_a(cur ^ 1);
+        mf_dense1(cur);
+        write_a(cur ^ 1);
+      } else if constexpr (MF16) {
+        mf_lo1(cur);
+        // A(kt+1) landed (the B DMA of kt+1 and the A loads of kt+2 may not
+        // have): split and stored among the remaining MFMAs of tile kt
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
+        launder_a(cur ^ 1);
+        mf_rest(cur, cur ^ 1);
       } else {
+        compute_st(cur, 0);
+        // A(kt+1) landed: its split overlaps the remaining MFMAs of tile kt
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
+        launder_a(cur ^ 1);
+        split_a(cur ^ 1);
+      }
+      if constexpr (!MF16) {
 #pragma unroll
         for (int st = 1; st < BK / 16; ++st) compute_st(cur, st);
+        write_a(cur ^ 1);
       }
-      write_a(cur ^ 1);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of kt+1 landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
