@@ -10,9 +10,11 @@ for r in 1 2; do
     n=$(basename $L .so)
     if [ "$L" = main ]; then
       S3_ONLY=1 timeout -k 10 200 python -u tools/s3_bench.py 1280 8 > gpurun_out/$TAG/${n}_$r.txt 2>&1 || exit 1
+      timeout -k 10 100 python -u tools/stem_ab.py 1280 >> gpurun_out/$TAG/${n}_$r.txt 2>&1 || exit 1
     else
       S3_ONLY=1 RR_LIB_PATH=$L timeout -k 10 200 python -u tools/s3_bench.py 1280 8 > gpurun_out/$TAG/${n}_$r.txt 2>&1 || exit 1
+      RR_LIB_PATH=$L timeout -k 10 100 python -u tools/stem_ab.py 1280 >> gpurun_out/$TAG/${n}_$r.txt 2>&1 || exit 1
     fi
   done
 done
-grep TOTAL gpurun_out/$TAG/*.txt
+grep -E "TOTAL|s3" gpurun_out/$TAG/*.txt | grep -v "^.*:h "

@@ -24,6 +24,9 @@ def cls_of(name):
     seed scores, 0 = stored C: convs / linears); gemm_s3_kernel = convs."""
     if "gemm_s3_kernel" in name:
         return "conv_gemm"
+    m = re.search(r"gemm_8p_kernel<(\d)>", name)
+    if m:  # the 8-phase bf16 sweep (filter / seed scores only)
+        return {2: "cosine_filter", 1: "cosine_seed"}.get(int(m.group(1)), "other")
     m = re.search(r"gemm_kernel<([^>]*)>", name)
     if m:
         args = [int(x) for x in m.group(1).split(",")]
@@ -84,7 +87,8 @@ def main(src, tag):
             # arg: 1 = bf16 prefilter sweep, 0 = exhaustive fp32); the bench's
             # side calls (exhaustive comparison, sanity search) are excluded
             dt = os.environ.get("RR_PROFILE_RANK_DT", "1")
-            rs = [r for r in rs if r["kernel"].split(",")[7].strip() == dt] or rs
+            # (the 8-phase kernel is bf16 only: gemm_8p_kernel<EM>)
+            rs = [r for r in rs if (r["kernel"].split(",")[7].strip() if r["kernel"].count(",") >= 7 else "1") == dt] or rs
             rs = [max(rs, key=lambda r: r["total_ms"])]
         if rs:
             tot_calls = sum(r["calls"] for r in rs)
