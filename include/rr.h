@@ -69,11 +69,14 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     5 (bf16 sweeps with K % 128 == 0: 256x256 8-phase pipeline;
  *                     otherwise as 3)
  *   RR_TUNE_S3_CFG:   split-bf16 core, 1..6 (gemm_s3.hip tile table)
+ *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of
+ *                     ~1 us for every other resident block (-1 = the library's pick)
  * Any other key or value: RR_EINVAL. */
 #define RR_TUNE_GEMM_CFG 1
 #define RR_TUNE_GEMM_BK 2
 #define RR_TUNE_LP_CFG 3
 #define RR_TUNE_S3_CFG 4
+#define RR_TUNE_S3_STAGGER 5
 int rr_set_tuning(rr_handle_t h, int key, int value);
 
 /* ---- search (ranker) ----------------------------------------------------

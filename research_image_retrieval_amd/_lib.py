@@ -20,7 +20,7 @@ RR_OK, RR_EINVAL, RR_EHIP, RR_EWORKSPACE, RR_EOVERFLOW = 0, -1, -2, -3, -4
 # timing classes (rr_timing_enable / rr_timing_collect)
 TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM, TIME_COSINE_SEED, TIME_ATTN = 0, 1, 2, 3, 4, 5
 # rr_set_tuning keys
-TUNE_GEMM_CFG, TUNE_GEMM_BK, TUNE_LP_CFG, TUNE_S3_CFG = 1, 2, 3, 4
+TUNE_GEMM_CFG, TUNE_GEMM_BK, TUNE_LP_CFG, TUNE_S3_CFG, TUNE_S3_STAGGER = 1, 2, 3, 4, 5
 
 _lib = None
 _lock = threading.RLock()

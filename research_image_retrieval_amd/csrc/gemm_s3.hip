@@ -122,6 +122,13 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   static_assert(BK == 16 || BK == 32, "BK");
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
 
+  // round stagger (GemmArgs): half of the first round's blocks start later,
+  // so in every later round half the CUs run their k-loop while the other
+  // half run their HBM-heavy epilogue (blocks b, b+8, ... share an XCD, so
+  // (b >> 3) & 1 halves every XCD)
+  if (g.stagger_sleeps > 0 && (int)blockIdx.x < g.stagger_blocks && ((blockIdx.x >> 3) & 1))
+    for (int i = 0; i < g.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(32);
+
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const int lr = lane & 31, lh = lane >> 5;
@@ -559,12 +566,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 }
 
 template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0>
-static hipError_t launch_s3_t(const GemmArgs& g, hipStream_t s) {
+static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
+  g.stagger_blocks = n_cu * MINB;
+  g.stagger_sleeps = nblk > 2LL * n_cu * MINB ? stagger : 0;  // only grids of several rounds
   hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16>), dim3((unsigned)nblk), dim3(64 * WM * WN),
                      0, s, g, (int)tiles_n);
   return hipGetLastError();
@@ -604,14 +613,14 @@ static int pick_s3(const GemmArgs& g, int forced) {
 }
 
 template <int AM>
-static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced) {
+static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
   switch (pick_s3(g, forced)) {
-    case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1>(g, s);
-    case 3: return launch_s3_t<4, 2, 2, 2, 32, AM, 1>(g, s);
-    case 4: return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1>(g, s);
-    case 5: return launch_s3_t<4, 1, 2, 2, 32, AM, 1>(g, s);
-    case 6: return launch_s3_t<4, 1, 2, 2, 16, AM, 2>(g, s);
-    default: return launch_s3_t<2, 2, 2, 2, 16, AM, 2>(g, s);
+    case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1>(g, s, n_cu, st);
+    case 3: return launch_s3_t<4, 2, 2, 2, 32, AM, 1>(g, s, n_cu, st);
+    case 4: return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1>(g, s, n_cu, st);
+    case 5: return launch_s3_t<4, 1, 2, 2, 32, AM, 1>(g, s, n_cu, st);
+    case 6: return launch_s3_t<4, 1, 2, 2, 16, AM, 2>(g, s, n_cu, st);
+    default: return launch_s3_t<2, 2, 2, 2, 16, AM, 2>(g, s, n_cu, st);
   }
 }
 
@@ -628,13 +637,17 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
   if ((g.ldb & 7) || (g.b_plane & 7) || ((uintptr_t)g.B & 15))
     return set_error(h, RR_EINVAL, "gemm_s3: B planes need ldb % 8 == 0, plane stride % 8 == 0, 16-B alignment");
   if (g.M == 0) return RR_OK;
+  // default stagger: the residual layers only (their 256 KB-per-tile epilogue
+  // is the HBM-heavy phase): 256->1024 x23 -5 %, the other residual layers
+  // -1 %, the rest neutral to +2 % (tools/stagger_ab.sh, profiles/r02f_s3_stagger.txt)
+  const int st = h->tune.s3_stagger >= 0 ? h->tune.s3_stagger : (g.residual != nullptr ? 8 : 0);
   hipError_t e;
   {
     TimedLaunch tl(h, timer_cls, s);
     const int f = h->tune.s3_cfg;
-    e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s, f)
-        : amode == A_CONV ? launch_s3_am<A_CONV>(g, s, f)
-                          : launch_s3_am<A_CONV_C4>(g, s, f);
+    e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s, f, device_cu_count(h), st)
+        : amode == A_CONV ? launch_s3_am<A_CONV>(g, s, f, device_cu_count(h), st)
+                          : launch_s3_am<A_CONV_C4>(g, s, f, device_cu_count(h), st);
   }
   return check_hip(h, e, "gemm_s3 launch");
 }

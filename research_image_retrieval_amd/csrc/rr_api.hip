@@ -144,6 +144,10 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       if (value < 0 || value > 6) break;
       h->tune.s3_cfg = value;
       return RR_OK;
+    case RR_TUNE_S3_STAGGER:
+      if (value < -1 || value > 200) break;
+      h->tune.s3_stagger = value;
+      return RR_OK;
     default:
       return set_error(h, RR_EINVAL, "rr_set_tuning: unknown key");
   }

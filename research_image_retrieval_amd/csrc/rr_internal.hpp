@@ -18,7 +18,9 @@ struct rr_handle_s {
     int gemm_bk = 0;   // fp32 core k-tile depth: 16 or 32
     int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 sweeps)
     int s3_cfg = 0;    // split-bf16 core: 1..6 (gemm_s3.hip)
+    int s3_stagger = -1;  // split-bf16 core round stagger in ~1 us sleeps (-1: the library's pick)
   } tune;
+  int n_cu = 0;  // compute units of the handle's device (device_cu_count)
   // timing (see rr_timing_enable)
   bool timing = false;
   static constexpr int kClasses = 6;
@@ -133,6 +135,16 @@ inline long long seed_sample_rows(long long n, int k) {
   return n < s ? n : s;
 }
 
+// compute units of the handle's device (queried once)
+inline int device_cu_count(rr_handle_s* h) {
+  if (h->n_cu <= 0) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, h->device) != hipSuccess || v <= 0) v = 256;
+    h->n_cu = v;
+  }
+  return h->n_cu;
+}
+
 // Candidate capacity per query that a workspace of `bytes` holds when the
 // candidate buffer [nq][cap] of 8-byte keys starts at `off_cand` (256-aligned)
 // and the layout's total is rounded up to 256 B; at most `worst`.
@@ -180,6 +192,10 @@ struct GemmArgs {
   int sym = 0;  // E_STORE of a symmetric product: skip tiles strictly below the diagonal
   // split-bf16 GEMM (gemm_s3.hip): B = three bf16 planes, b_plane elements apart
   long long b_plane = 0;
+  // round stagger: of the first stagger_blocks blocks (one full round of
+  // resident blocks), every other XCD-slot one sleeps stagger_sleeps x ~2k
+  // cycles before starting, so later rounds run half the CUs out of phase
+  int stagger_blocks = 0, stagger_sleeps = 0;
 };
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,

@@ -368,14 +368,15 @@ def topk_merge(part_scores, part_idx, k_out):
 
 
 _TUNE_KEYS = {"gemm_cfg": _lib.TUNE_GEMM_CFG, "gemm_bk": _lib.TUNE_GEMM_BK, "lp_cfg": _lib.TUNE_LP_CFG,
-              "s3_cfg": _lib.TUNE_S3_CFG}
+              "s3_cfg": _lib.TUNE_S3_CFG, "s3_stagger": _lib.TUNE_S3_STAGGER}
+_TUNE_DEFAULT = {"s3_stagger": -1}  # the library's own pick (0 elsewhere)
 
 
 class tuning:
     """Force kernel tile configs on a device's handle for the duration of a
     ``with`` block (rr_set_tuning; tests and tuning tools only):
-    ``with ops.tuning(0, s3_cfg=6): ...``.  Values revert to 0 (the library's
-    own pick) on exit."""
+    ``with ops.tuning(0, s3_cfg=6): ...``.  Values revert to the library's
+    own pick on exit."""
 
     def __init__(self, device_index, **kw):
         for k in kw:
@@ -391,7 +392,7 @@ class tuning:
 
     def __exit__(self, *exc):
         for k in self.kw:
-            _lib.lib().rr_set_tuning(self.h, _TUNE_KEYS[k], 0)
+            _lib.lib().rr_set_tuning(self.h, _TUNE_KEYS[k], _TUNE_DEFAULT.get(k, 0))
         return False
 
 

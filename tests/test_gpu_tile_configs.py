@@ -134,3 +134,20 @@ def test_lowp_every_tile_config(cuda, cfg, dtype):
     assert (s - torch.gather(ref, 1, i)).abs().max().item() < 1e-5
     kth = ref.topk(50, dim=1).values[:, -1:]
     assert bool((s[:, -1:] >= kth - 1e-5).all())
+
+
+def test_s3_round_stagger_changes_nothing_but_timing(cuda):
+    """The first-round stagger (RR_TUNE_S3_STAGGER; default on for residual
+    layers) only delays blocks: outputs are bit-identical for every value, on a
+    grid of several rounds."""
+    g = torch.Generator().manual_seed(5)
+    x = torch.relu(torch.randn(8, 28, 28, 256, generator=g)).to(cuda)
+    wt = (torch.randn(1024, 1, 1, 256, generator=g) * (2.0 / 256) ** 0.5).to(cuda)
+    bias = (torch.randn(1024, generator=g) * 0.1).to(cuda)
+    r = torch.randn(8, 28, 28, 1024, generator=g).to(cuda)
+    w3 = ops.split3_bf16(wt)
+    outs = []
+    for st in (0, 3, 20, -1):
+        with ops.tuning(cuda.index, s3_stagger=st):
+            outs.append(ops.conv2d_s3(x, w3, bias, 1, 0, r, True).cpu())
+    assert all(torch.equal(outs[0], o) for o in outs[1:])

@@ -32,20 +32,22 @@ dev = torch.device("cuda:0")
 if cfg != "auto":
     ops.tuning(0, lp_cfg=int(cfg)).__enter__()
 g = torch.Generator(device=dev).manual_seed(0)
-M = 320 * 197
+M = int(os.environ.get("LP_B", "320")) * 197
+SWEEPS = os.environ.get("LP_SWEEPS", "1") == "1"
 for (k, n) in [(768, 2304), (768, 768), (768, 3072), (3072, 768)]:
+    res = torch.randn(M, n, device=dev, generator=g) if os.environ.get("LP_RESIDUAL") == "1" else None
     x = (torch.randn(M, k, device=dev, generator=g) * 0.5).to(torch.bfloat16)
     w = (torch.randn(n, k, device=dev, generator=g) / k ** 0.5).to(torch.bfloat16)
     b = torch.randn(n, device=dev, generator=g)
-    y = ops.linear_bf16(x, w, b)
-    ref = torch.addmm(b, x[:4096].float(), w.float().t())
+    y = ops.linear_bf16(x, w, b, residual=res)
+    ref = torch.addmm(b, x[:4096].float(), w.float().t()) + (0 if res is None else res[:4096])
     err = ((y[:4096] - ref).abs().max() / ref.abs().max()).item()
-    ms = t_ms(lambda: ops.linear_bf16(x, w, b))
-    print(json.dumps({"cfg": cfg, "op": f"linear_bf16 {M}x{k}->{n}", "ms": round(ms, 4),
+    ms = t_ms(lambda: ops.linear_bf16(x, w, b, residual=res))
+    print(json.dumps({"cfg": cfg, "op": f"linear_bf16 {M}x{k}->{n}" + (" +res" if res is not None else ""), "ms": round(ms, 4),
                       "tflops": round(2.0 * M * k * n / ms / 1e9, 1), "rel_err": err}), flush=True)
 # cosine sweeps: bf16 d=2048 (prefilter), bf16 d=512 (C4), fp8 d=2048 (C5)
 N = 1_600_000
-for dt, d in [("bf16", 2048), ("bf16", 512), ("fp8", 2048)]:
+for dt, d in ([("bf16", 2048), ("bf16", 512), ("fp8", 2048)] if SWEEPS else []):
     gal = torch.nn.functional.normalize(torch.randn(N, d, device=dev, generator=g), dim=1)
     q = torch.nn.functional.normalize(torch.randn(320, d, device=dev, generator=g), dim=1)
     gl, gs = ops.quantize_rows(gal, dt)

@@ -1,6 +1,7 @@
 """Per-layer timing of the R101 trunk convs at B images: exact-fp32 core vs
 the split-bf16 core.  usage: [S3_CFG=1..6] [S3_ONLY=1] s3_bench.py [B] [reps]
-(S3_CFG forces one s3 tile config through rr_set_tuning; default: the library's pick)"""
+(S3_CFG forces one s3 tile config through rr_set_tuning, S3_STAGGER the
+first-round stagger in ~1 us sleeps; default: the library's picks)"""
 import os
 import sys
 
@@ -22,7 +23,8 @@ SHAPES = [(56, 64, 64, 1, 1, 0, 1), (56, 64, 64, 3, 1, 0, 3), (56, 64, 256, 1, 1
           (7, 2048, 512, 1, 1, 0, 2), (7, 512, 512, 3, 1, 0, 2), (14, 1024, 2048, 1, 2, 0, 1)]
 dev = torch.device("cuda:0")
 CFG = int(os.environ.get("S3_CFG", "0"))
-ops.tuning(0, s3_cfg=CFG).__enter__()
+STAGGER = int(os.environ.get("S3_STAGGER", "-1"))  # rr_set_tuning(RR_TUNE_S3_STAGGER); -1 = the library's pick
+ops.tuning(0, s3_cfg=CFG, s3_stagger=STAGGER).__enter__()
 tot = {"f32": 0.0, "s3": 0.0}
 flops_tot = 0.0
 for h, cin, cout, k, s, res, cnt in SHAPES:
