@@ -572,8 +572,10 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  g.stagger_blocks = n_cu * MINB;
-  g.stagger_sleeps = nblk > 2LL * n_cu * MINB ? stagger : 0;  // only grids of several rounds
+  // resident blocks per CU: MINB is the launch bound's minimum waves per SIMD
+  constexpr int PER_CU = (MINB * 4) / (WM * WN) > 1 ? (MINB * 4) / (WM * WN) : 1;
+  g.stagger_blocks = n_cu * PER_CU;
+  g.stagger_sleeps = nblk > 2LL * n_cu * PER_CU ? stagger : 0;  // only grids of several rounds
   hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16>), dim3((unsigned)nblk), dim3(64 * WM * WN),
                      0, s, g, (int)tiles_n);
   return hipGetLastError();
@@ -586,6 +588,9 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //   4: 128x256, 8 waves of 64x64, BK 32, 1/CU (144 KB), v_mfma_f32_16x16x32_bf16
 //   5: 256x64,  4 waves of 64x64, BK 32, 1/CU (120 KB)
 //   6: 256x64,  4 waves of 64x64, BK 16, 2/CU (60 KB)
+//   7: 256x64,  8 waves of 32x64, BK 16, 2/CU (60 KB), 4 waves per SIMD
+//      (<= 128 registers): the picked 256x64 tile (the N = 64 layers and the
+//      stem 2-7 % faster than 6, profiles/r02f_s3_cfg7.txt)
 // (all others on v_mfma_f32_32x32x16_bf16).  Measured per R101 layer at 320
 // images (tools/s3_bench.py): 3 is the fastest wherever N >= 128 (1.1-1.3x
 // config 1 per FLOP); 4 on 16x16x32 runs every N % 256 == 0 layer 3-14 %
@@ -597,7 +602,7 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 // all six terms (less accurate than exact fp32).  rr_set_tuning(RR_TUNE_S3_CFG)
 // forces a config (tests, tools).
 static int pick_s3(const GemmArgs& g, int forced) {
-  if (forced >= 1 && forced <= 6) return forced;
+  if (forced >= 1 && forced <= 7) return forced;
   if ((g.N % 256) == 0) return 4;
   // rounds of resident blocks x tile area per CU / relative per-FLOP speed
   auto cost = [&](long long bm, long long bn, long long per_cu, double speed) {
@@ -608,7 +613,7 @@ static int pick_s3(const GemmArgs& g, int forced) {
   double best = cost(128, 128, 2, 1.0);
   int cfg = 1;
   if (cost(256, 128, 1, 1.15) < best) best = cost(256, 128, 1, 1.15), cfg = 3;
-  if (cost(256, 64, 2, 1.0) < best) best = cost(256, 64, 2, 1.0), cfg = 6;
+  if (cost(256, 64, 2, 1.0) < best) best = cost(256, 64, 2, 1.0), cfg = 7;
   return cfg;
 }
 
@@ -620,6 +625,7 @@ static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int
     case 4: return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1>(g, s, n_cu, st);
     case 5: return launch_s3_t<4, 1, 2, 2, 32, AM, 1>(g, s, n_cu, st);
     case 6: return launch_s3_t<4, 1, 2, 2, 16, AM, 2>(g, s, n_cu, st);
+    case 7: return launch_s3_t<8, 1, 1, 2, 16, AM, 4>(g, s, n_cu, st);
     default: return launch_s3_t<2, 2, 2, 2, 16, AM, 2>(g, s, n_cu, st);
   }
 }

@@ -35,7 +35,7 @@ S3_CONVS = [(3, 13, 11, 64, 96, 1, 1, 0, True), (2, 15, 13, 32, 160, 3, 2, 1, Fa
             (2, 14, 14, 64, 256, 1, 2, 0, False), (2, 9, 11, 128, 512, 3, 1, 1, True)]
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("shape", S3_CONVS)
 def test_s3_conv_every_tile_config(cuda, cfg, shape):
     b, h, w, cin, cout, k, s, p, res = shape
@@ -52,7 +52,7 @@ def test_s3_conv_every_tile_config(cuda, cfg, shape):
     _check(y, ref, scale, 4e-7)
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("b,h,w", [(2, 224, 224), (1, 37, 53)])
 def test_s3_stem_every_tile_config(cuda, cfg, b, h, w):
     """The NHWC4 stem (7x7/2, K = 196 padded to 224): BK = 16 tiles (configs 1
@@ -68,7 +68,7 @@ def test_s3_stem_every_tile_config(cuda, cfg, b, h, w):
     _check(y, ref, scale, 4e-7)
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7])
 def test_s3_linear_every_tile_config(cuda, cfg):
     g = torch.Generator().manual_seed(cfg)
     m, k, n = 517, 320, 320

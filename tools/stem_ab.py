@@ -11,6 +11,8 @@ from research_image_retrieval_amd import ops  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 320
 dev = torch.device("cuda:0")
+if os.environ.get("S3_CFG"):  # force one split-bf16 tile config (rr_set_tuning)
+    ops.tuning(0, s3_cfg=int(os.environ["S3_CFG"])).__enter__()
 x = F.pad(torch.randn(B, 224, 224, 3, device=dev), (0, 1)).contiguous()
 w = F.pad(torch.randn(64, 7, 7, 3, device=dev) * 0.1, (0, 1)).contiguous()
 b = torch.randn(64, device=dev)
