@@ -28,8 +28,14 @@ __device__ __forceinline__ int acc_col(int j, int r, int lane) {
   else return 32 * j + (lane & 31);
 }
 
-// QuickGELU, x * sigmoid(1.702 x) (networks/model.py:166-168)
-__device__ __forceinline__ float quick_gelu(float x) { return x * (1.0f / (1.0f + expf(-(1.702f * x)))); }
+// QuickGELU, x * sigmoid(1.702 x) (networks/model.py:166-168), on the
+// hardware exp2 and reciprocal (v_exp_f32, v_rcp_f32: ~1 ulp each; expf and a
+// division cost ~20 VALU per element, 0.3 ms per ViT-B/16 fc1 at 1280 images);
+// x -> -inf: exp2 -> inf, rcp -> 0, result -0 as x * sigmoid gives
+__device__ __forceinline__ float quick_gelu(float x) {
+  const float e = __builtin_amdgcn_exp2f(x * (-1.702f * 1.4426950408889634f));
+  return x * __builtin_amdgcn_rcpf(1.0f + e);
+}
 
 // Stage the BM x BN accumulator tile (32x32 MFMA C/D layout: col = lane & 31,
 // row = (r&3) + 8(r>>2) + 4(lane>>5)) through LDS, then write whole rows: each

@@ -1,8 +1,10 @@
-"""Low-precision GEMM configs on the shapes that matter (ViT-B/16 linears at
-B=320, the bf16 prefilter sweep, the fp8 C5 sweep).  Run once per forced
-config: LP_CFG=1|2|3|4 python tools/lp_bench.py  -> JSON lines (rr_set_tuning
-RR_TUNE_LP_CFG: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 sweep tile;
-unset = the library's pick)."""
+"""Low-precision GEMM configs on the shapes that matter (the ViT-B/16 block's
+linears with their epilogues at LP_B images (default 320), the bf16 prefilter
+sweep, the fp8 C5 sweep; LP_SWEEPS=0 skips the sweeps).  Run once per forced
+config: LP_CFG=1..6 python tools/lp_bench.py  -> JSON lines (rr_set_tuning
+RR_TUNE_LP_CFG: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 sweep tile,
+5 = 8-phase 256x256 sweep, 6 = 8-wave 128x128 at 2 blocks/CU; unset = the
+library's pick)."""
 import json
 import os
 import sys
@@ -34,16 +36,23 @@ if cfg != "auto":
 g = torch.Generator(device=dev).manual_seed(0)
 M = int(os.environ.get("LP_B", "320")) * 197
 SWEEPS = os.environ.get("LP_SWEEPS", "1") == "1"
-for (k, n) in [(768, 2304), (768, 768), (768, 3072), (3072, 768)]:
-    res = torch.randn(M, n, device=dev, generator=g) if os.environ.get("LP_RESIDUAL") == "1" else None
+# the ViT-B/16 block's four linears with their epilogues (networks.VisionTransformer bf16):
+# QKV -> bf16, out-proj + residual, fc1 QuickGELU -> bf16, fc2 + residual
+VIT = [(768, 2304, 0, True, False), (768, 768, 0, False, True), (768, 3072, 2, True, False),
+       (3072, 768, 0, False, True)]
+for (k, n, act, obf, resid) in VIT:
+    res = torch.randn(M, n, device=dev, generator=g) if resid else None
     x = (torch.randn(M, k, device=dev, generator=g) * 0.5).to(torch.bfloat16)
     w = (torch.randn(n, k, device=dev, generator=g) / k ** 0.5).to(torch.bfloat16)
     b = torch.randn(n, device=dev, generator=g)
-    y = ops.linear_bf16(x, w, b, residual=res)
+    y = ops.linear_bf16(x, w, b, residual=res, act=act, out_bf16=obf)
     ref = torch.addmm(b, x[:4096].float(), w.float().t()) + (0 if res is None else res[:4096])
-    err = ((y[:4096] - ref).abs().max() / ref.abs().max()).item()
-    ms = t_ms(lambda: ops.linear_bf16(x, w, b, residual=res))
-    print(json.dumps({"cfg": cfg, "op": f"linear_bf16 {M}x{k}->{n}" + (" +res" if res is not None else ""), "ms": round(ms, 4),
+    if act == 2:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    err = ((y[:4096].float() - ref).abs().max() / ref.abs().max()).item()
+    ms = t_ms(lambda: ops.linear_bf16(x, w, b, residual=res, act=act, out_bf16=obf))
+    tag = (" +res" if resid else "") + (" gelu" if act == 2 else "") + (" ->bf16" if obf else "")
+    print(json.dumps({"cfg": cfg, "op": f"linear_bf16 {M}x{k}->{n}" + tag, "ms": round(ms, 4),
                       "tflops": round(2.0 * M * k * n / ms / 1e9, 1), "rel_err": err}), flush=True)
 # cosine sweeps: bf16 d=2048 (prefilter), bf16 d=512 (C4), fp8 d=2048 (C5)
 N = 1_600_000
