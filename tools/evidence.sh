@@ -8,6 +8,8 @@ TAG=${1:-ev}
 O=$R/gpurun_out/$TAG
 mkdir -p $O
 cd $R
+timeout -k 10 420 python -u bench.py > $O/bench_c3.json 2> $O/bench_c3.log || { echo "bench c3 failed"; exit 1; }
+echo "c3 done"
 bash tools/profile.sh > $O/profile.log 2>&1 || { echo "profile failed"; exit 1; }
 for w in "c4" "c5" "c3 --gallery-kind clustered" "c2"; do
   n=$(echo $w | tr ' ' '_' | tr -d '-')
