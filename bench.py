@@ -220,6 +220,12 @@ def cpu_baseline_c2(n_gallery, n_query, d=512, seed=0):
             "embed_s_per_image": t_embed, "rank_s": t_rank, "torch_default_threads": default_threads}
 
 
+# RR_FORCE_SHARDED=1 (with torch.distributed.run --nproc-per-node 1): run the
+# multi-GPU path — process group (RCCL), ShardedGallery, collectives — on a
+# world of one, so its RCCL calls execute on a 1-GPU box
+DIST_ON = False
+
+
 def run_c2(a, world, rank, dev):
     """C2: ResNet50-GeM 512-d fp32 (Table-1 GeMModel) over a ROxford5k-shaped
     set at imsize 1024 -- 4,993 gallery images + 70 query crops, every image
@@ -264,7 +270,7 @@ def run_c2(a, world, rank, dev):
         mark("gallery_embed")
         qd = torch.cat([net.forward_test_u8(q) for q in queries], 0) if queries else torch.empty((0, 512), device=dev)
         mark("query_embed")
-        if world > 1:
+        if DIST_ON:
             gd = torch.cat(_all_gather_var(gd.contiguous(), None)[0], 0)
             qd = torch.cat(_all_gather_var(qd.contiguous(), None)[0], 0)
         mark("all_gather")
@@ -287,13 +293,13 @@ def run_c2(a, world, rank, dev):
     log(f"[rank {rank}] c2 phases (ms, synchronised step): {phases}")
     timer = ops.KernelTimer(dev.index)
     timer.enable(True)
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         maps = step()
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -301,7 +307,7 @@ def run_c2(a, world, rank, dev):
                                                    ("elementwise", _lib.TIME_ELEM),
                                                    ("cosine_seed", _lib.TIME_COSINE_SEED))}
     timer.enable(False)
-    if world > 1:
+    if DIST_ON:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -348,7 +354,7 @@ def run_c2(a, world, rank, dev):
         log(f"cpu baseline {time.time() - t:.1f}s")
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
         dist.destroy_process_group()
 
@@ -435,7 +441,9 @@ def main():
     # one process per GPU; ranks beyond the visible devices share them (rehearsal)
     dev = torch.device("cuda", local % torch.cuda.device_count())
     torch.cuda.set_device(dev)
-    if world > 1:
+    global DIST_ON
+    DIST_ON = world > 1 or os.environ.get("RR_FORCE_SHARDED") == "1"
+    if DIST_ON:
         backend = os.environ.get("RR_DIST_BACKEND", "nccl")  # "gloo" only for 1-GPU rehearsals
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
@@ -463,12 +471,12 @@ def main():
     ws = torch.empty(ws_full if ws_max is None else max(ws_lo, min(ws_full, ws_max)), dtype=torch.uint8, device=dev)
     counts = [a.batch] * world  # every rank's query count: the sharded search needs no size exchange
     sharded = ShardedGallery(gallery, lo, workspace=ws, dtype=a.dtype, prefilter=pre,
-                             max_workspace_bytes=ws_max) if world > 1 else None
+                             max_workspace_bytes=ws_max) if DIST_ON else None
     gal_bf, gal_bound = (None, None)
-    if pre and world == 1:
+    if pre and not DIST_ON:
         gal_bf, _ = ops.quantize_rows(gallery, "bf16")
         gal_bound = ops.prefilter_gallery_bound(gallery, gal_bf)
-    gal_lp, gal_sc = ops.quantize_rows(gallery, a.dtype) if (a.dtype != "fp32" and world == 1) else (None, None)
+    gal_lp, gal_sc = ops.quantize_rows(gallery, a.dtype) if (a.dtype != "fp32" and not DIST_ON) else (None, None)
     torch.cuda.synchronize()
     log(f"[rank {rank}] setup {time.time() - t_setup:.1f}s: shard [{lo},{hi}) x {a.dim}, batch {a.batch}")
 
@@ -538,13 +546,13 @@ def main():
 
     timer = ops.KernelTimer(dev.index)
     timer.enable(True)
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         out = step()
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
@@ -553,7 +561,7 @@ def main():
                                                    ("cosine_seed", _lib.TIME_COSINE_SEED),
                                                    ("attention", _lib.TIME_ATTN))}
     timer.enable(False)
-    if world > 1:
+    if DIST_ON:
         t = torch.tensor([elapsed], dtype=torch.float64,
                          device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -707,7 +715,7 @@ def main():
         log(f"cpu baseline {time.time() - t:.1f}s")
     if rank == 0:
         print(json.dumps(res), flush=True)
-    if world > 1:
+    if DIST_ON:
         dist.barrier()
         dist.destroy_process_group()
 
