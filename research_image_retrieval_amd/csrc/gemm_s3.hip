@@ -645,7 +645,7 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
   if (g.M == 0) return RR_OK;
   // default stagger: the residual layers only (their 256 KB-per-tile epilogue
   // is the HBM-heavy phase): 256->1024 x23 -5 %, the other residual layers
-  // -1 %, the rest neutral to +2 % (tools/stagger_ab.sh, profiles/r02f_s3_stagger.txt)
+  // -1 %, the rest neutral to +2 % (tools/ab_trunk.sh stagger, profiles/r02f_s3_stagger.txt)
   const int st = h->tune.s3_stagger >= 0 ? h->tune.s3_stagger : (g.residual != nullptr ? 8 : 0);
   hipError_t e;
   {
