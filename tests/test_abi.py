@@ -81,3 +81,22 @@ def test_bounded_workspace_arithmetic():
         assert 0 < cnt_off(nq, n, d, k) < lo and 0 < ovf_off(nq, n, d, k) < lo
         # 2 GB instead of the ~16 GB worst case at the C3 shape
         assert cap_for(nq, n, d, k, 2 << 30) > 100_000
+
+
+def test_conv_algorithmic_bytes_and_flops():
+    """The conv class's roofline inputs (bench.py): R101 at 224x224 is 15.6
+    GFLOP and ~164 MB of algorithmic activation bytes per image (input map,
+    output, residual once each, fp32), plus the split weights once per launch."""
+    from research_image_retrieval_amd import weights as W
+    fl = W.resnet_conv_flops("resnet101", 224, 224)
+    by1 = W.resnet_conv_bytes("resnet101", 224, 224, 1)
+    by2 = W.resnet_conv_bytes("resnet101", 224, 224, 2)
+    assert set(fl) == set(by1) and len(fl) == 104
+    assert abs(sum(fl.values()) / 1e9 - 15.60) < 0.01
+    act = sum(by2.values()) - sum(by1.values())          # per image (weights cancel)
+    wts = sum(by1.values()) - act
+    assert 160e6 < act < 170e6
+    assert abs(wts - 6 * 42.4e6) < 6 * 1.0e6             # ~42.4 M conv parameters x 3 bf16 planes
+    # a residual conv3 reads its identity: 56x56, 64 -> 256 with residual
+    b = W.resnet_conv_bytes("resnet101", 224, 224, 1, weight_bytes=0)["layer1.1.conv3"]
+    assert b == (56 * 56 * 64 + 2 * 56 * 56 * 256) * 4
