@@ -465,18 +465,26 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
 
   // ---- epilogue ----
   // 32x32 C/D map: col (N index) = lane & 31, row (M index) = (r&3) + 8(r>>2) + 4(lane>>5)
-  if (!MF16 && (g.scale_a != nullptr || g.scale_b != nullptr)) {  // per-row dequantisation (fp8)
+  // per-row dequantisation (fp8 only; bf16 / fp32 rows are unscaled — compiled
+  // into those kernels, this block's 160 hoisted scale loads spilled ~150 VGPRs
+  // of the 256x320 bf16 sweep tile).  Row scales one at a time, the FN column
+  // scales held.
+  if constexpr (!MF16 && DT == DT_FP8) {
+    if (g.scale_a != nullptr || g.scale_b != nullptr) {
+      float sb[FN];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int n = n0 + wn * WTN + j * 32 + lr;
-      const float sb = (g.scale_b != nullptr && n < g.N) ? g.scale_b[n] : 1.f;
+      for (int j = 0; j < FN; ++j) {
+        const int n = n0 + wn * WTN + j * 32 + lr;
+        sb[j] = (g.scale_b != nullptr && n < g.N) ? g.scale_b[n] : 1.f;
+      }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int m = m0 + wm * WTM + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * lh;
           const float sa = (g.scale_a != nullptr && m < g.M) ? g.scale_a[m] : 1.f;
-          acc[i][j][r] = acc[i][j][r] * sa * sb;
+#pragma unroll
+          for (int j = 0; j < FN; ++j) acc[i][j][r] = acc[i][j][r] * sa * sb[j];
         }
     }
   }
