@@ -117,7 +117,7 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
     affinity, quota, threads = host_threads()
     default_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
-    n_img, n_q, n_g = 96, 64, 400_000
+    n_img, n_q, n_g = 192, 64, 400_000  # ~10-15 s of CPU work on the box's 16-core share
     sd = W.synthetic_resnet_state_dict(arch, seed)
     ww, wb = W.synthetic_linear(2048, 2048, seed + 1)
     pw, pb = W.synthetic_linear(2048, 2048, seed + 5, scale=1.0 / np.sqrt(2048))
@@ -196,14 +196,15 @@ def cpu_baseline_c2(n_gallery, n_query, d=512, seed=0):
     sd = W.synthetic_resnet_state_dict("resnet50", seed)
     pw, pb = W.synthetic_linear(d, 2048, seed + 2)
     rs = np.random.RandomState(1234)
-    imgs = torch.from_numpy(rs.randint(0, 256, size=(3, 768, 1024, 3), dtype=np.uint8))
+    n_img = 50  # ~10 s of CPU work (0.2 s per image on the box's 16-core share)
+    imgs = torch.from_numpy(rs.randint(0, 256, size=(n_img + 1, 768, 1024, 3), dtype=np.uint8))
     with torch.no_grad():
         embed_ref.gem_model_descriptor(embed_ref.normalize_u8(imgs[:1]), sd, W.RESNET_LAYERS["resnet50"], pw, pb)
         t0 = time.perf_counter()
-        for i in (1, 2):
+        for i in range(1, n_img + 1):
             embed_ref.gem_model_descriptor(embed_ref.normalize_u8(imgs[i:i + 1]), sd, W.RESNET_LAYERS["resnet50"],
                                            pw, pb)
-        t_embed = (time.perf_counter() - t0) / 2
+        t_embed = (time.perf_counter() - t0) / n_img
         gen = torch.Generator().manual_seed(7)
         g = torch.nn.functional.normalize(torch.randn(n_gallery, d, generator=gen), dim=1)
         q = torch.nn.functional.normalize(torch.randn(n_query, d, generator=gen), dim=1)
@@ -214,7 +215,7 @@ def cpu_baseline_c2(n_gallery, n_query, d=512, seed=0):
     total = (n_gallery + n_query) * t_embed + t_rank
     return {"value": (n_gallery + n_query) / total, "unit": "images/s", "cores": threads, "kind": "port",
             "affinity_cpus": affinity, "granted_cpus": granted,
-            "sample": f"2 images embedded at batch 1 (768x1024, resnet50-GeM 512-d, fp32) and the full ranking of "
+            "sample": f"{n_img} images embedded at batch 1 (768x1024, resnet50-GeM 512-d, fp32) and the full ranking of "
                       f"{n_query} queries x {n_gallery} rows (torch.mm + np.argsort); job time = "
                       f"{n_gallery + n_query} x per-image embed + ranking",
             "embed_s_per_image": t_embed, "rank_s": t_rank, "torch_default_threads": default_threads}
