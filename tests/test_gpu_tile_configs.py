@@ -32,7 +32,8 @@ def _check(y, ref, scale, tol):
 # (b, h, w, cin, cout, k, stride, pad, residual): a dense 1x1, a strided 3x3
 # with ragged N, a 1x1/2 projection, and a residual 1x1
 S3_CONVS = [(3, 13, 11, 64, 96, 1, 1, 0, True), (2, 15, 13, 32, 160, 3, 2, 1, False),
-            (2, 14, 14, 64, 256, 1, 2, 0, False), (2, 9, 11, 128, 512, 3, 1, 1, True)]
+            (2, 14, 14, 64, 256, 1, 2, 0, False), (2, 9, 11, 128, 512, 3, 1, 1, True),
+            (2, 7, 9, 32, 128, 1, 1, 0, False)]  # K = 32: a single BK = 32 k-tile
 
 
 @pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7])
