@@ -60,6 +60,23 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
   const int wm = wave % WM, wn = wave / WM;
   const bool vec_ok = ((g.N & 3) == 0) && ((g.ldc & 3) == 0);
   float* ct = lds;  // [SLAB][BN] row-major
+  // The bias columns, loaded before any store: a load issued after a store
+  // may alias it, so the compiler waits vmcnt(0) for it — and vmcnt counts
+  // stores too — turning every row chunk into a store round trip (32 per
+  // 256x256 tile).  A thread's column is the same in every iteration when
+  // NT % C4 == 0 (every configuration that stores C); otherwise one per
+  // iteration.
+  constexpr int BI = (NT % C4 == 0) ? 1 : ITERS;
+  f32x4 bias_v[BI];
+  if (vec_ok) {
+#pragma unroll
+    for (int it = 0; it < BI; ++it) {
+      const int idx = tid + it * NT;
+      const int n = n0 + (idx % C4) * 4;
+      bias_v[it] = (g.bias != nullptr && n < g.N) ? *reinterpret_cast<const f32x4*>(g.bias + n)
+                                                  : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
 #pragma unroll
   for (int p = 0; p < P; ++p) {
     const int rbase = p * SLAB;
@@ -101,6 +118,17 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
           if (m < g.M && n < g.N) res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
         }
       }
+      // One wait for every bias / residual load, before this slab's first
+      // store: once a store is in flight the compiler can only wait for a
+      // load with vmcnt(0) (loads and stores retire out of order), i.e. for
+      // the stores too — one store round trip per row chunk.  The empty asm
+      // redefines the registers, so nothing below waits again.
+#pragma unroll
+      for (int it = 0; it < BI; ++it) asm volatile("" : "+v"(bias_v[it]));
+      if (g.residual != nullptr) {
+#pragma unroll
+        for (int it = 0; it < ITERS; ++it) asm volatile("" : "+v"(res[it]));
+      }
 #pragma unroll
       for (int it = 0; it < ITERS; ++it) {
         const int idx = tid + it * NT;
@@ -108,7 +136,7 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
         const int m = m0 + rbase + row, n = n0 + c4 * 4;
         if (m >= g.M || n >= g.N) continue;
         f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
-        if (g.bias != nullptr) v += *reinterpret_cast<const f32x4*>(g.bias + n);
+        if (g.bias != nullptr) v += bias_v[BI == 1 ? 0 : it];
         if (g.residual != nullptr) v += res[it];
         if (g.relu == 1) {
 #pragma unroll

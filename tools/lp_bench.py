@@ -1,9 +1,9 @@
 """Low-precision GEMM configs on the shapes that matter (the ViT-B/16 block's
 linears with their epilogues at LP_B images (default 320), the bf16 prefilter
 sweep, the fp8 C5 sweep; LP_SWEEPS=0 skips the sweeps).  Run once per forced
-config: LP_CFG=1..6 python tools/lp_bench.py  -> JSON lines (rr_set_tuning
+config: LP_CFG=1..5 python tools/lp_bench.py  -> JSON lines (rr_set_tuning
 RR_TUNE_LP_CFG: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 sweep tile,
-5 = 8-phase 256x256 sweep, 6 = 8-wave 128x128 at 2 blocks/CU; unset = the
+5 = 8-phase 256x256 sweep; unset = the
 library's pick)."""
 import json
 import os

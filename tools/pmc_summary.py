@@ -1,5 +1,6 @@
 """Summarise rocprofv3 --pmc counter CSVs (tools/s3_pmc.sh layout): per
-directory, the gemm_s3 kernel's counters averaged over its dispatches."""
+directory, the named kernel's counters averaged over its dispatches.
+usage: python tools/pmc_summary.py <dir> [kernel-name substring, default gemm_s3]"""
 import csv
 import glob
 import os
@@ -7,6 +8,7 @@ import sys
 from collections import defaultdict
 
 root = sys.argv[1]
+kname = sys.argv[2] if len(sys.argv) > 2 else "gemm_s3"
 for tag in sorted(os.listdir(root)):
     d = os.path.join(root, tag)
     if not os.path.isdir(d):
@@ -14,7 +16,7 @@ for tag in sorted(os.listdir(root)):
     acc = defaultdict(list)
     for f in glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            if "gemm_s3" not in r.get("Kernel_Name", ""):
+            if kname not in r.get("Kernel_Name", ""):
                 continue
             acc[r["Counter_Name"]].append(float(r["Counter_Value"]))
     c = {k: sum(v) / len(v) for k, v in acc.items()}

@@ -6,7 +6,8 @@ def t(fn, it=20):
     s.record()
     for _ in range(it): fn()
     e.record(); torch.cuda.synchronize(); return s.elapsed_time(e)/it
-M=63040
+import os
+M=int(os.environ.get("LP_B", "320"))*197
 for k,n in [(768,2304),(768,768),(768,3072),(3072,768)]:
     x=torch.randn(M,k,device=dev,dtype=torch.bfloat16); w=torch.randn(n,k,device=dev,dtype=torch.bfloat16)
     ms=t(lambda: x@w.t()); print(f"torch bf16 {M}x{k}->{n}: {ms:.4f} ms {2*M*k*n/ms/1e9:.1f} TF/s", flush=True)
