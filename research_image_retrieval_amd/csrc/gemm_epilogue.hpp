@@ -37,6 +37,86 @@ __device__ __forceinline__ float quick_gelu(float x) {
   return x * __builtin_amdgcn_rcpf(1.0f + e);
 }
 
+// Flags of a stored-C launch (GemmArgs bias / residual / relu / out_bf16).
+// The launchers compile the flag sets the networks use into their own kernel
+// instances (template EPI = the flags, checked against ep_flags(g) on the
+// host); EPI = -1 reads them from g per element.  One set per kernel, not a
+// switch inside it: several inlined variants held extra values live through
+// the k-loop and spilled it.
+enum { EP_BIAS = 1, EP_RES = 2, EP_RELU = 4, EP_GELU = 8, EP_BF16 = 16 };
+inline int ep_flags(const GemmArgs& g) {
+  return (g.bias != nullptr ? EP_BIAS : 0) | (g.residual != nullptr ? EP_RES : 0) |
+         (g.relu == 1 ? EP_RELU : g.relu == 2 ? EP_GELU : 0) | (g.out_bf16 ? EP_BF16 : 0);
+}
+
+// Write one staged slab (rows mb.. of the tile, row-major in ct): the LDS
+// reads of a group of row chunks first (counted lgkmcnt waits instead of an
+// LDS round trip between consecutive stores; the whole slab at once when no
+// other slab's accumulators are still live), then bias / residual /
+// activation and the 16-B (fp32) or 8-B (bf16) store.  FL >= 0: the flags
+// fixed at compile time and (BI == 1) one column per thread, so the loop is
+// the arithmetic, a row bound and an address step; FL = -1: the flags read
+// from g per element.
+template <int FL, int P, int ITERS, int NT, int C4, int BN, int BI>
+__device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const float* ct, const f32x4 (&bias_v)[BI],
+                                           const f32x4 (&res)[ITERS], int tid, int mb, int n0) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  constexpr int GR = ITERS < 4 ? ITERS : (P == 1 ? 8 : 4);
+  constexpr bool FIXED = FL >= 0;
+  const bool has_bias = FIXED ? (FL & EP_BIAS) != 0 : g.bias != nullptr;
+  const bool has_res = FIXED ? (FL & EP_RES) != 0 : g.residual != nullptr;
+  const int act = FIXED ? ((FL & EP_RELU) ? 1 : (FL & EP_GELU) ? 2 : 0) : g.relu;
+  const bool obf = FIXED ? (FL & EP_BF16) != 0 : g.out_bf16 != 0;
+  // BI == 1: every iteration of a thread is the same column, NT / C4 rows on
+  const int c40 = tid % C4, r0 = tid / C4;
+  constexpr int RSTEP = NT / C4;
+  const int n_fix = n0 + c40 * 4;
+  const long long o0 = (long long)(mb + r0) * g.ldc + n_fix;
+  const long long ostep = (long long)RSTEP * g.ldc;
+  f32x4 cv[ITERS];
+#pragma unroll
+  for (int it = 0; it < ITERS; ++it) {
+    if (it % GR == 0) {
+#pragma unroll
+      for (int u = it; u < it + GR && u < ITERS; ++u) {
+        const int idx = tid + u * NT;
+        const int row = idx / C4, c4 = idx - row * C4;
+        cv[u] = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
+      }
+    }
+    int m, n;
+    long long o;
+    if constexpr (FIXED && BI == 1) {
+      m = mb + r0 + it * RSTEP;
+      n = n_fix;
+      o = o0 + it * ostep;
+    } else {
+      const int idx = tid + it * NT;
+      const int row = idx / C4, c4 = idx - row * C4;
+      m = mb + row;
+      n = n0 + c4 * 4;
+      o = (long long)m * g.ldc + n;
+    }
+    if (m >= g.M || n >= g.N) continue;
+    f32x4 v = cv[it];
+    if (has_bias) v += bias_v[BI == 1 ? 0 : it];
+    if (has_res) v += res[it];
+    if (act == 1) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    } else if (act == 2) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = quick_gelu(v[e]);
+    }
+    if (obf) {
+      const bf16x4 ob = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(Cb) + o) = ob;
+    } else {
+      *reinterpret_cast<f32x4*>(Cb + o) = v;
+    }
+  }
+}
+
 // Stage the BM x BN accumulator tile (32x32 MFMA C/D layout: col = lane & 31,
 // row = (r&3) + 8(r>>2) + 4(lane>>5)) through LDS, then write whole rows: each
 // lane moves 16 B, 32 lanes cover a 512-B row run, the residual is read the
@@ -44,7 +124,7 @@ __device__ __forceinline__ float quick_gelu(float x) {
 // (one HBM round trip per slab, overlapping the staging).  When the tile exceeds the CAPF floats of LDS it goes in P row
 // slabs.  Called by every thread of the block after the k-loop's last
 // barrier (the LDS is free).
-template <int WM, int WN, int FM, int FN, int CAPF, bool MF16 = false>
+template <int WM, int WN, int FM, int FN, int CAPF, bool MF16 = false, int FL = -1>
 __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, const f32x16 (&acc)[FM][FN], float* lds,
                                                int m0, int n0) {
   constexpr int NT = 64 * WM * WN;
@@ -129,30 +209,7 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) asm volatile("" : "+v"(res[it]));
       }
-#pragma unroll
-      for (int it = 0; it < ITERS; ++it) {
-        const int idx = tid + it * NT;
-        const int row = idx / C4, c4 = idx - row * C4;
-        const int m = m0 + rbase + row, n = n0 + c4 * 4;
-        if (m >= g.M || n >= g.N) continue;
-        f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
-        if (g.bias != nullptr) v += bias_v[BI == 1 ? 0 : it];
-        if (g.residual != nullptr) v += res[it];
-        if (g.relu == 1) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-        } else if (g.relu == 2) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = quick_gelu(v[e]);
-        }
-        if (g.out_bf16) {
-          typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-          const bf16x4 o = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-          *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(Cb) + (long long)m * g.ldc + n) = o;
-        } else {
-          *reinterpret_cast<f32x4*>(Cb + (long long)m * g.ldc + n) = v;
-        }
-      }
+      store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, BN, BI>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0);
     } else {
       for (int idx = tid; idx < SLAB * C4; idx += NT) {
         const int row = idx / C4, c4 = idx - row * C4;

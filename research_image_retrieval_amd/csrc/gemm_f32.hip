@@ -85,7 +85,8 @@ __device__ __forceinline__ void interleave2() {
 // 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
 // 'DVFS give-back' item 7).  Register r of tile (i, j) then maps through
 // acc_row / acc_col<true> (gemm_epilogue.hpp) instead of the 32x32 map.
-template <int WM, int WN, int FM, int FN, int AMODE, int EMODE, int BK, int DT, int MINB, int GL, int MF16 = 0>
+template <int WM, int WN, int FM, int FN, int AMODE, int EMODE, int BK, int DT, int MINB, int GL, int MF16 = 0,
+          int EPI = -1>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, int tiles_n) {
   using ET = typename ElemT<DT>::T;
   static_assert(!MF16 || DT == DT_BF16, "MF16: bf16 only");
@@ -579,11 +580,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   }
   }
 
-  if constexpr (EMODE == E_STORE) epilogue_store<WM, WN, FM, FN, 2 * BUF, (bool)MF16>(g, Cb, acc, lds, m0, n0);
+  if constexpr (EMODE == E_STORE) epilogue_store<WM, WN, FM, FN, 2 * BUF, (bool)MF16, EPI>(g, Cb, acc, lds, m0, n0);
 }
 
-template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0>
-static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
+template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0,
+          int EPI = -1>
+static hipError_t launch_t1(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM;
   const long long tiles_n = (g.N + BN - 1) / BN;
@@ -591,9 +593,26 @@ static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
   const unsigned splits = g.k_split > 0 ? (unsigned)((g.K + g.k_split - 1) / g.k_split) : 1u;
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16>), dim3((unsigned)nblk, splits),
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EPI>), dim3((unsigned)nblk, splits),
                      dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
   return hipGetLastError();
+}
+
+// bf16 stored-C GEMMs (the ViT linears) with their epilogues compiled in:
+// QKV (bias -> bf16), out-proj / fc2 (bias + residual, fp32), fc1 (bias +
+// QuickGELU -> bf16); everything else reads its flags at run time.
+template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0>
+static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
+  if constexpr (EM == E_STORE && DT == DT_BF16) {
+    switch (ep_flags(g)) {
+      case EP_BIAS | EP_BF16: return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_BF16>(g, s);
+      case EP_BIAS | EP_RES: return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_RES>(g, s);
+      case EP_BIAS | EP_GELU | EP_BF16:
+        return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_GELU | EP_BF16>(g, s);
+      default: break;
+    }
+  }
+  return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16>(g, s);
 }
 
 // k-tile depth.  Measured on MI355X (same device, interleaved A/B): BK = 16

@@ -104,7 +104,7 @@ __device__ __forceinline__ void s3_launder(f32x4& v) { asm volatile("" : "+v"(v)
 // 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
 // 'DVFS give-back' item 7).  The k-tile's MFMAs go in two parts around the A
 // split: a0b0 + a1b1 + a0b1 + a1b0 (planes 0-1), then a0b2 + a2b0 (plane 2).
-template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0>
+template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0, int EPI = -1>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
   static_assert(!MF16 || BK == 32, "MF16: BK 32");
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
@@ -562,10 +562,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 #pragma unroll
       for (int j = 0; j < FN; ++j) hi[i][j] += lo[i][j];
   }
-  epilogue_store<WM, WN, FM, FN, BUF, (bool)MF16>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
+  epilogue_store<WM, WN, FM, FN, BUF, (bool)MF16, EPI>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
 }
 
-template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0>
+template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int EPI = -1>
 static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
@@ -576,7 +576,7 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
   constexpr int PER_CU = (MINB * 4) / (WM * WN) > 1 ? (MINB * 4) / (WM * WN) : 1;
   g.stagger_blocks = n_cu * PER_CU;
   g.stagger_sleeps = nblk > 2LL * n_cu * PER_CU ? stagger : 0;  // only grids of several rounds
-  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16>), dim3((unsigned)nblk), dim3(64 * WM * WN),
+  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16, EPI>), dim3((unsigned)nblk), dim3(64 * WM * WN),
                      0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
@@ -617,15 +617,28 @@ static int pick_s3(const GemmArgs& g, int forced) {
   return cfg;
 }
 
+// The picked configs (3, 4, 7) with the ResNet's epilogues compiled in:
+// conv + BN + ReLU, + residual + ReLU, projection conv + BN.
+template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0>
+static hipError_t launch_s3_ep(const GemmArgs& g, hipStream_t s, int n_cu, int st) {
+  switch (ep_flags(g)) {
+    case EP_BIAS | EP_RELU: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS | EP_RELU>(g, s, n_cu, st);
+    case EP_BIAS | EP_RES | EP_RELU:
+      return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS | EP_RES | EP_RELU>(g, s, n_cu, st);
+    case EP_BIAS: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS>(g, s, n_cu, st);
+    default: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16>(g, s, n_cu, st);
+  }
+}
+
 template <int AM>
 static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
   switch (pick_s3(g, forced)) {
     case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1>(g, s, n_cu, st);
-    case 3: return launch_s3_t<4, 2, 2, 2, 32, AM, 1>(g, s, n_cu, st);
-    case 4: return launch_s3_t<2, 4, 2, 2, 32, AM, 1, 1>(g, s, n_cu, st);
+    case 3: return launch_s3_ep<4, 2, 2, 2, 32, AM, 1>(g, s, n_cu, st);
+    case 4: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1>(g, s, n_cu, st);
     case 5: return launch_s3_t<4, 1, 2, 2, 32, AM, 1>(g, s, n_cu, st);
     case 6: return launch_s3_t<4, 1, 2, 2, 16, AM, 2>(g, s, n_cu, st);
-    case 7: return launch_s3_t<8, 1, 1, 2, 16, AM, 4>(g, s, n_cu, st);
+    case 7: return launch_s3_ep<8, 1, 1, 2, 16, AM, 4>(g, s, n_cu, st);
     default: return launch_s3_t<2, 2, 2, 2, 16, AM, 2>(g, s, n_cu, st);
   }
 }
