@@ -298,6 +298,90 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
 
   const int lr = lane & 31, lh = lane >> 5;
 
+  // bf16 16x16x32 with LDS-DMA: the barrier of k-tile kt sits inside its last
+  // k-step, after that step's fragments are in registers: wait for tile kt+1's
+  // DMA, barrier, DMA tile kt+2 into the buffer just drained, read tile kt+1's
+  // first fragments, THEN the last step's MFMAs — they hide the post-barrier
+  // LDS latency that otherwise idles both waves of every SIMD at each k-tile.
+  constexpr bool PIPE16 = GL && MF16 && DT == DT_BF16;
+  if constexpr (PIPE16) {
+    constexpr int S = BK / 16;
+    static_assert(S % 2 == 0, "PIPE16: an even number of k-steps per k-tile");
+    const int l16 = lane & 15, lg = lane >> 4;
+    bf16x8 af[2][FM][2], bf[2][FN][2];
+    auto rd = [&](int buf, int st, bf16x8 (*a)[2], bf16x8 (*b)[2]) {
+      const float* la = lds + buf * BUF;
+      const float* lb = la + BM * BK;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int row = wm * WTM + i * 32 + h * 16 + l16;
+          a[i][h] = *reinterpret_cast<const bf16x8*>(la + row * BK + swz<BK>(row, 4 * st + lg) * 4);
+        }
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int row = wn * WTN + j * 32 + h * 16 + l16;
+          b[j][h] = *reinterpret_cast<const bf16x8*>(lb + row * BK + swz<BK>(row, 4 * st + lg) * 4);
+        }
+    };
+    glds_tile(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (nk > 1) glds_tile(1, 1);
+    rd(0, 0, af[0], bf[0]);
+    __builtin_amdgcn_s_setprio(1);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      auto mfmas = [&](int st) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              acc4[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[st & 1][i][t >> 1], bf[st & 1][j][t & 1],
+                                                                      acc4[i][j][t], 0, 0, 0);
+      };
+#pragma unroll
+      for (int st = 0; st < S; ++st) {
+        if (st + 1 < S) {
+          // next step's reads between this step's MFMAs
+          mfmas(st);
+          rd(cur, st + 1, af[(st + 1) & 1], bf[(st + 1) & 1]);
+          interleave<2 * (FM + FN), 4 * FM * FN>();
+        } else {
+          // this step's fragments: waited for and redefined by an empty asm
+          // on both paths, so the MFMAs below (one copy: two spill the
+          // accumulators) wait for nothing — not for the next tile's reads
+          auto settle = [&]() {
+#pragma unroll
+            for (int i = 0; i < FM; ++i)
+#pragma unroll
+              for (int h = 0; h < 2; ++h) asm volatile("" : "+v"(af[st & 1][i][h]));
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+              for (int h = 0; h < 2; ++h) asm volatile("" : "+v"(bf[st & 1][j][h]));
+          };
+          __builtin_amdgcn_sched_barrier(0);  // the previous step's MFMAs stay above the wait
+          settle();
+          if (kt + 1 < nk) {
+            // every wave is done with buffer cur; tile kt+1's DMA has landed
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __builtin_amdgcn_s_barrier();
+            if (kt + 2 < nk) glds_tile(kt + 2, cur);
+            rd(cur ^ 1, 0, af[0], bf[0]);
+          }
+          mfmas(st);
+        }
+      }
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __syncthreads();  // every wave's last reads done: the epilogue reuses the LDS
+  } else {
   if constexpr (GL) {
     glds_tile(0, 0);
     __syncthreads();
@@ -452,6 +536,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
       if (kt + 1 < nk) store_tile(cur ^ 1);
     }
     __syncthreads();  // with GL: also the vmcnt(0) that retires the DMA
+  }
   }
   if constexpr (MF16) {
 #pragma unroll
