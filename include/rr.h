@@ -68,7 +68,7 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     4 (256x320 for bf16 filter / score sweeps, 256x256 otherwise),
  *                     5 (bf16 sweeps with K % 128 == 0: 256x256 8-phase pipeline;
  *                     otherwise as 3)
- *   RR_TUNE_S3_CFG:   split-bf16 core, 1..7 (gemm_s3.hip tile table)
+ *   RR_TUNE_S3_CFG:   split-bf16 core, 1..8 (gemm_s3.hip tile table)
  *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of
  *                     ~1 us for every other resident block (-1 = the library's pick)
  * Any other key or value: RR_EINVAL. */

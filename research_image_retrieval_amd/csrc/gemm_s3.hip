@@ -30,6 +30,9 @@
 #include "gemm_epilogue.hpp"
 #include "rr_internal.hpp"
 
+#ifndef RR_EXP
+#define RR_EXP 0
+#endif
 namespace rr {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -565,6 +568,371 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   epilogue_store<WM, WN, FM, FN, BUF, (bool)MF16, EPI>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
 }
 
+// ---- Persistent 128x256 tile (config 8) ------------------------------------
+// The config-4 tile (8 waves of 64x64, BK 32, v_mfma_f32_16x16x32_bf16, dense
+// A or the Cin % 32 == 0 conv A) as one block per CU that walks its tiles as
+// ONE continuous k-stream: the B DMA runs one k-tile and the A loads two
+// k-tiles ahead ACROSS tile boundaries, so while a tile's epilogue runs the
+// next tile's first k-tile already sits in LDS and its second is in flight
+// (a fresh block pays that round trip before its first MFMA), and the
+// epilogue's stores drain under the next tile's first k-tiles.  The epilogue
+// stages C through the stage buffer the tile's last k-tile just released (two
+// 64-row slabs of 64 KB), with every bias / residual load issued before the
+// staging.  Same per-accumulator k order and epilogue arithmetic as config 4:
+// the results are bit-identical to it.
+// a fresh, opaque copy of v: per-thread address math built from it inside a
+// tile loop's epilogue / loader switch cannot be hoisted out of the loop (its
+// results would then be live through the whole k-loop and spill it)
+__device__ __forceinline__ int s3_opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_n, int ntiles) {
+  constexpr int WM = 2, FM = 2, FN = 2, BK = 32, NT = 512, NW = 8;
+  constexpr int WTM = 64, WTN = 64, BM = 128, BN = 256, SL = BK / 8;
+  constexpr int A_EL = 3 * BM * BK, BUF = A_EL + 3 * BN * BK;
+  constexpr int B_INS = 3 * BN / (64 / SL) / NW;  // LDS-DMA instructions per wave per k-tile (6)
+  constexpr int A_LD = 2;                         // A loads per thread per k-tile
+  static_assert(B_INS * NW * (64 / SL) == 3 * BN, "B staging must tile the block");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+
+  // round stagger: every block is resident from the start, so half of them
+  // (every other XCD slot) start later and the halves stay out of phase
+  if (g.stagger_sleeps > 0 && ((blockIdx.x >> 3) & 1))
+    for (int i = 0; i < g.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(32);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int nk = g.K / BK;
+  const int my_tiles = (ntiles - bid + G - 1) / G;
+  const int J = my_tiles * nk;  // k-tiles in this block's stream
+  // local tile tl -> origin: virtual block v = bid + tl*G keeps this block's
+  // XCD (G % 8 == 0 whenever a block owns more than one tile), then the same
+  // bijective XCD remap as the one-tile-per-block kernel
+  auto tile_origin = [&](int tl, int& m0, int& n0) {
+    const int v = bid + tl * G;
+    const int xcd = v & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
+    const int tn = wgid % tiles_n, tm = wgid / tiles_n;
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+
+  // ---- A loader (one 8-k chunk of one row per thread), two k-tiles ahead
+  // of the MFMAs; load_a() issues the loader's k-tile and advances it one
+  // k-tile along the stream (into the next tile after a tile's last).  Past
+  // the stream's end the loaders run on into one virtual tile v >= ntiles,
+  // which the remap sends to another block's tile or past M (A then reads
+  // row M - 1; B's column tile is always a real one): every address stays
+  // valid, nothing reads what they stage, and every iteration issues the same
+  // loads, as the counted waits assume ----
+  // rows past M load row M - 1 (only their own, unstored, output rows see it)
+  const float* a_ptr = g.A;
+  int a_kt = 0, a_tl = 0;
+  auto a_tile = [&](int tl) {
+    int m0, n0;
+    tile_origin(tl, m0, n0);
+    const int t = s3_opaque(tid);
+    const int m = min(m0 + t / SL, g.M - 1);
+    a_ptr = g.A + (long long)m * g.lda + (t % SL) * 8;
+  };
+  a_tile(0);
+  f32x4 ra2[2][2];
+  auto load_a = [&](int rb) {
+    s3_load2<1>(reinterpret_cast<const f32x4*>(a_ptr + a_kt * BK), ra2[rb]);
+    if (++a_kt == nk) {
+      a_kt = 0;
+      a_tile(++a_tl);
+    }
+  };
+  u32x4 pk[3];
+  auto split_a = [&](int rb) {
+    uint32_t h[8], m[8], l[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x = ra2[rb][e >> 2][e & 3];
+      const float r1 = x - __uint_as_float(__float_as_uint(x) & 0xffff0000u);
+      const float r2 = r1 - __uint_as_float(__float_as_uint(r1) & 0xffff0000u);
+      h[e] = __float_as_uint(x);
+      m[e] = __float_as_uint(r1);
+      l[e] = __float_as_uint(r2);
+    }
+    pk[0] = u32x4{pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
+    pk[1] = u32x4{pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7])};
+    pk[2] = u32x4{pack2(l[0], l[1]), pack2(l[2], l[3]), pack2(l[4], l[5]), pack2(l[6], l[7])};
+  };
+  auto write_a = [&](int buf) {
+    uint16_t* la = lds + buf * BUF;
+    const int a_slot = tid % SL, a_row = tid / SL;
+    const int off = a_row * BK + pswz<BK>(a_row, a_slot) * 8;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(la + p * BM * BK + off) = pk[p];
+  };
+  auto launder_a = [&](int rb) {
+    s3_launder(ra2[rb][0]);
+    s3_launder(ra2[rb][1]);
+  };
+
+  // ---- B loader: instruction i of a wave DMAs plane i/2, plane rows
+  // 128 (i&1) + 16 wave + lane/4 (N % 256 == 0: no row past N) ----
+  const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
+  const int b_r = wave * (64 / SL) + lane / SL;
+  const int b_sw = pswz<BK>(b_r, lane % SL) * 8;  // the same for every i
+  const uint16_t* b_src = Bp;
+  int b_kt = 0, b_tl = 0;
+  auto b_tile = [&](int tl) {
+    int m0, n0;
+    tile_origin(tl, m0, n0);
+    b_src = Bp + (long long)(n0 + b_r) * g.ldb + b_sw;
+  };
+  b_tile(0);
+  auto glds_b = [&](int buf) {
+    uint16_t* lb = lds + buf * BUF + A_EL;
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src + (i >> 1) * g.b_plane + (long long)(i & 1) * (BN / 2) * g.ldb +
+                                                     b_kt * BK),
+                                       (__attribute__((address_space(3))) void*)(lb + (i * NW + wave) * (64 / SL) * BK),
+                                       16, 0, 0);
+    if (++b_kt == nk) {
+      b_kt = 0;
+      b_tile(++b_tl);
+    }
+  };
+
+  // ---- MFMAs: four 16x16x32 sub-tiles per 32x32 tile, as config 4 ----
+  f32x4 hi4[FM][FN][4], lo4[FM][FN][4];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          hi4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+          lo4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+  };
+  zero_acc();
+  bf16x8 fa[3][FM][2], fb[3][FN][2];
+  const int l16 = lane & 15, lg = lane >> 4;
+  auto rd_mf = [&](int cur, int p) {
+    const uint16_t* la = lds + cur * BUF;
+    const uint16_t* lb = la + A_EL;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = wm * WTM + i * 32 + h * 16 + l16;
+        fa[p][i][h] = *reinterpret_cast<const bf16x8*>(la + (p * BM + row) * BK + pswz<BK>(row, lg) * 8);
+      }
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = wn * WTN + j * 32 + h * 16 + l16;
+        fb[p][j][h] = *reinterpret_cast<const bf16x8*>(lb + (p * BN + row) * BK + pswz<BK>(row, lg) * 8);
+      }
+  };
+#define RR_MF16(a, b, c) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
+  auto mf_hi = [&]() {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) RR_MF16(fa[0][i][t >> 1], fb[0][j][t & 1], hi4[i][j][t]);
+  };
+  auto mf_lo1 = [&]() {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          RR_MF16(fa[1][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
+          RR_MF16(fa[0][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
+          RR_MF16(fa[1][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
+        }
+  };
+  auto mf_lo2 = [&]() {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          RR_MF16(fa[0][i][t >> 1], fb[2][j][t & 1], lo4[i][j][t]);
+          RR_MF16(fa[2][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
+        }
+  };
+#undef RR_MF16
+
+  // ---- epilogue of local tile tl through stage buffer `buf` (free) ----
+  // Two slabs by MFMA row tile i: slab s = rows 64 wm + 32 s + [0, 32) of every
+  // wave, so staging slab 0 frees half of every wave's accumulators before
+  // slab 1's residual is loaded (both slabs' residuals in registers at once
+  // beside all accumulators spilled the k-loop).  Residual rows are loaded by
+  // inline asm (rows past M clamped to M - 1; never stored), so one explicit
+  // vmcnt(0) covers both slabs: slab 1's loads fly while slab 0 is staged.
+  constexpr int C4 = BN / 4, HITERS = 32 * C4 / NT;  // 4 row chunks per thread and 32-row band
+  auto epilogue = [&](int tl, int buf) {
+    // the two accumulator tiles summed first (128 registers -> 64)
+    f32x16 acc[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * t + e] = hi4[i][j][t][e] + lo4[i][j][t][e];
+    int m0, n0;
+    tile_origin(tl, m0, n0);
+    const int te = s3_opaque(tid);
+    const int c40 = te % C4, r0 = te / C4;
+    f32x4 bias_v[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+    if ((EPI & EP_BIAS) && g.bias != nullptr) bias_v[0] = *reinterpret_cast<const f32x4*>(g.bias + n0 + c40 * 4);
+    asm volatile("" : "+v"(bias_v[0]));
+    f32x4 res[2][2][HITERS];  // [slab][band][row chunk]
+    auto load_res = [&](int sl) {
+      if constexpr ((EPI & EP_RES) != 0) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int it = 0; it < HITERS; ++it) {
+            const int m = min(m0 + q * 64 + sl * 32 + r0 + it * (NT / C4), g.M - 1);
+            const float* p = g.residual + (long long)m * g.ldc + n0 + c40 * 4;
+            asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(res[sl][q][it]) : "v"(p) : "memory");
+          }
+      }
+    };
+    float* ct = reinterpret_cast<float*>(lds + buf * BUF);  // [2 bands x 32 rows][BN]
+    const int le = te & 63;
+    auto stage = [&](int sl) {
+      float* cw = ct + (wm * 32) * BN + wn * WTN;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cw[acc_row<true>(0, r, le) * BN + acc_col<true>(j, r, le)] = acc[sl][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    auto store = [&](int sl) {
+      if constexpr ((EPI & EP_RES) != 0) {
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int it = 0; it < HITERS; ++it) asm volatile("" : "+v"(res[sl][q][it]));
+      }
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        store_slab<EPI, 2, HITERS, NT, C4, BN, 1>(g, g.C, ct + q * 32 * BN, bias_v, res[sl][q], te,
+                                                  m0 + q * 64 + sl * 32, n0);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();  // every LDS read of the slab done
+      asm volatile("" ::: "memory");
+    };
+    load_res(0);
+    stage(0);
+    load_res(1);
+    if constexpr ((EPI & EP_RES) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store(0);
+    stage(1);
+    store(1);  // its barrier also frees `buf` for the next k-tiles
+    zero_acc();  // here, not at the sum: 128 registers of zeros held through the stores spilled
+  };
+
+  // ---- the stream: k-tile j of the block = k-tile j % nk of local tile j / nk ----
+  load_a(0);
+  glds_b(0);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_INS) : "memory");  // A(0) landed
+  launder_a(0);
+  split_a(0);
+  write_a(0);
+  load_a(1);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B(0) landed
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  int c_kt = 0, c_tl = 0;
+  // iteration j (stage cur = j & 1 holds k-tile j, register buffer cur ^ 1
+  // holds A(j+1)): B DMA of j+1, A loads of j+2, the k-tile's MFMAs with the
+  // split of A(j+1) among them (the dense-A order of config 4), then — after
+  // the last k-tile of a tile — its epilogue through stage cur.  The
+  // epilogue's stores are issued after A(j+2) and before the next loads: the
+  // next A wait (vmcnt(A_LD + B_INS)) counts only loads after it, so it is
+  // exact if the stores retire in order and waits longer (never shorter) if
+  // they do not.
+  auto iter = [&](int cur) __attribute__((always_inline)) {
+    glds_b(cur ^ 1);
+    load_a(cur);
+    rd_mf(cur, 0);
+    rd_mf(cur, 1);
+    mf_hi();
+    mf_lo1();
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
+    launder_a(cur ^ 1);
+    split_a(cur ^ 1);
+    rd_mf(cur, 2);
+    mf_lo2();
+    write_a(cur ^ 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of j+1 landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (++c_kt == nk) {
+      c_kt = 0;
+      epilogue(c_tl++, cur);
+    }
+  };
+  for (int j = 0; j < J; j += 2) {
+    iter(0);
+    if (j + 1 < J) iter(1);
+  }
+  // the clamped tail loads are still in flight: keep both buffers live until
+  // they have landed, so no later value is allocated to them
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  launder_a(0);
+  launder_a(1);
+}
+
+template <int EPI>
+static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
+  const long long tiles_m = (g.M + 127) / 128, tiles_n = g.N / 256;
+  const long long ntiles = tiles_m * tiles_n;
+  if (ntiles <= 0) return hipSuccess;
+  if (ntiles * (g.K / 32) > 0x7fffffffLL) return hipErrorInvalidValue;
+  // one block per CU; a block that owns several tiles must stay on its XCD
+  // (grid a multiple of 8)
+  const int slots = std::max(8, n_cu & ~7);
+  const int grid = ntiles <= slots ? (int)ntiles : slots;
+  g.stagger_blocks = grid;
+  g.stagger_sleeps = ntiles > 2LL * grid ? stagger : 0;
+  hipLaunchKernelGGL((gemm_s3p_kernel<EPI>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
+  return hipGetLastError();
+}
+
+// config 8 serves dense A (1x1 convs), N % 256 == 0 and the ResNet's flag
+// sets (conv + BN + ReLU, + residual + ReLU, the projection conv); the rest
+// falls back to the library's pick
+static bool s3_persist_ok(const GemmArgs& g, int amode) {
+  const int f = ep_flags(g);
+  return (g.N % 256) == 0 && amode == A_DENSE &&
+         (f == (EP_BIAS | EP_RELU) || f == (EP_BIAS | EP_RES | EP_RELU) || f == EP_BIAS);
+}
+static hipError_t launch_s3p(const GemmArgs& g, hipStream_t s, int n_cu, int st) {
+  switch (ep_flags(g)) {
+    case EP_BIAS | EP_RELU: return launch_s3p_t<EP_BIAS | EP_RELU>(g, s, n_cu, st);
+    case EP_BIAS | EP_RES | EP_RELU: return launch_s3p_t<EP_BIAS | EP_RES | EP_RELU>(g, s, n_cu, st);
+    default: return launch_s3p_t<EP_BIAS>(g, s, n_cu, st);
+  }
+}
+
 template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int EPI = -1>
 static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
@@ -591,6 +959,8 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //   7: 256x64,  8 waves of 32x64, BK 16, 2/CU (60 KB), 4 waves per SIMD
 //      (<= 128 registers): the picked 256x64 tile (the N = 64 layers and the
 //      stem 2-7 % faster than 6, profiles/r02f_s3_cfg7.txt)
+//   8: config 4 as a persistent k-stream (gemm_s3p_kernel): dense A, N % 256
+//      == 0 — the picked tile for the 1x1 layers it serves
 // (all others on v_mfma_f32_32x32x16_bf16).  Measured per R101 layer at 320
 // images (tools/s3_bench.py): 3 is the fastest wherever N >= 128 (1.1-1.3x
 // config 1 per FLOP); 4 on 16x16x32 runs every N % 256 == 0 layer 3-14 %
@@ -602,7 +972,7 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 // all six terms (less accurate than exact fp32).  rr_set_tuning(RR_TUNE_S3_CFG)
 // forces a config (tests, tools).
 static int pick_s3(const GemmArgs& g, int forced) {
-  if (forced >= 1 && forced <= 7) return forced;
+  if (forced >= 1 && forced <= 8) return forced;
   if ((g.N % 256) == 0) return 4;
   // rounds of resident blocks x tile area per CU / relative per-FLOP speed
   auto cost = [&](long long bm, long long bn, long long per_cu, double speed) {
@@ -632,7 +1002,18 @@ static hipError_t launch_s3_ep(const GemmArgs& g, hipStream_t s, int n_cu, int s
 
 template <int AM>
 static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
-  switch (pick_s3(g, forced)) {
+  int cfg = pick_s3(g, forced);
+  // config 8 is the default wherever it serves (every dense R101 layer with
+  // N % 256 == 0: 1.0-1.1x config 4, residual expansions -4 to -9 %,
+  // profiles/r02k_s3p_ab.txt)
+  if (forced == 0 && AM == A_DENSE && s3_persist_ok(g, AM)) cfg = 8;
+  if (cfg == 8) {
+    if constexpr (AM == A_DENSE) {
+      if (s3_persist_ok(g, AM)) return launch_s3p(g, s, n_cu, st);
+    }
+    cfg = pick_s3(g, 0);  // a shape or flag set config 8 does not serve
+  }
+  switch (cfg) {
     case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1>(g, s, n_cu, st);
     case 3: return launch_s3_ep<4, 2, 2, 2, 32, AM, 1>(g, s, n_cu, st);
     case 4: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1>(g, s, n_cu, st);

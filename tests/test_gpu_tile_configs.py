@@ -36,7 +36,7 @@ S3_CONVS = [(3, 13, 11, 64, 96, 1, 1, 0, True), (2, 15, 13, 32, 160, 3, 2, 1, Fa
             (2, 7, 9, 32, 128, 1, 1, 0, False)]  # K = 32: a single BK = 32 k-tile
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8])
 @pytest.mark.parametrize("shape", S3_CONVS)
 def test_s3_conv_every_tile_config(cuda, cfg, shape):
     b, h, w, cin, cout, k, s, p, res = shape
@@ -69,7 +69,7 @@ def test_s3_stem_every_tile_config(cuda, cfg, b, h, w):
     _check(y, ref, scale, 4e-7)
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6, 7, 8])
 def test_s3_linear_every_tile_config(cuda, cfg):
     g = torch.Generator().manual_seed(cfg)
     m, k, n = 517, 320, 320
@@ -152,3 +152,31 @@ def test_s3_round_stagger_changes_nothing_but_timing(cuda):
         with ops.tuning(cuda.index, s3_stagger=st):
             outs.append(ops.conv2d_s3(x, w3, bias, 1, 0, r, True).cpu())
     assert all(torch.equal(outs[0], o) for o in outs[1:])
+
+
+@pytest.mark.parametrize("b,h,cin,cout,res,relu", [(4, 56, 256, 1024, True, True), (3, 37, 64, 256, True, True),
+                                                   (2, 29, 512, 256, False, True), (1, 14, 1024, 512, False, False),
+                                                   (9, 14, 128, 512, True, True)])
+def test_s3_persistent_tile_bit_identical(cuda, b, h, cin, cout, res, relu):
+    """Config 8 (one block per CU walking its tiles as one k-stream, the
+    epilogue in the freed stage) computes exactly what config 4 computes: the
+    same k order and epilogue arithmetic.  Shapes with several tiles per block
+    (b = 4: 392 tiles), ragged M, K = 64 (one pair of k-tiles per tile), no
+    residual and no ReLU (the projection conv)."""
+    g = torch.Generator().manual_seed(b * 1000 + cin + cout)
+    x = torch.relu(torch.randn(b, h, h, cin, generator=g)).to(cuda)
+    wt = (torch.randn(cout, 1, 1, cin, generator=g) * (2.0 / cin) ** 0.5).to(cuda)
+    bias = (torch.randn(cout, generator=g) * 0.1).to(cuda)
+    r = torch.randn(b, h, h, cout, generator=g).to(cuda) if res else None
+    w3 = ops.split3_bf16(wt)
+    outs = {}
+    for cfg in (4, 8):
+        with ops.tuning(cuda.index, s3_cfg=cfg):
+            outs[cfg] = ops.conv2d_s3(x, w3, bias, 1, 0, r, relu).cpu()
+    assert torch.equal(outs[4], outs[8])
+    ref = torch.einsum("bhwc,oc->bhwo", x.double().cpu(), wt[:, 0, 0].double().cpu()) + bias.double().cpu()
+    if res:
+        ref = ref + r.double().cpu()
+    if relu:
+        ref = torch.relu(ref)
+    assert (outs[8].double() - ref).abs().max().item() < 1e-4
