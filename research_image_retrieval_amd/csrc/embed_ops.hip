@@ -69,6 +69,40 @@ __global__ void resize_bilinear_kernel(const float* __restrict__ x, int B, int H
   }
 }
 
+// max pool, NHWC, one block per output row (b, oh), 4 channels per thread
+// (C % 4 == 0); padding taps are -inf.  A block's outputs share their input
+// columns and consecutive blocks share an input row, so the overlapping 3x3
+// windows are re-read from L2 instead of HBM (the flat grid-stride form below
+// read 6.4 GB per 4.1 GB stem output at 1280 images); 32-bit index math.
+__global__ __launch_bounds__(256) void maxpool4_row_kernel(const float* __restrict__ x, int H, int W, int C, int k,
+                                                           int stride, int pad, int OH, int OW, float* __restrict__ y) {
+  const int C4 = C >> 2;
+  const int row = blockIdx.x;  // b * OH + oh
+  const int b = row / OH, oh = row - b * OH;
+  const float* xb = x + (long long)b * H * W * C;
+  float* yr = y + (long long)row * OW * C;
+  const int n = OW * C4;
+  for (int o = threadIdx.x; o < n; o += blockDim.x) {
+    const int ow = o / C4, c4 = o - ow * C4;
+    float4 m = make_float4(-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff());
+    for (int dh = 0; dh < k; ++dh) {
+      const int ih = oh * stride - pad + dh;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      const float* xr = xb + (long long)ih * W * C + c4 * 4;
+      for (int dw = 0; dw < k; ++dw) {
+        const int iw = ow * stride - pad + dw;
+        if ((unsigned)iw >= (unsigned)W) continue;
+        const float4 v = *reinterpret_cast<const float4*>(xr + iw * C);
+        m.x = fmaxf(m.x, v.x);
+        m.y = fmaxf(m.y, v.y);
+        m.z = fmaxf(m.z, v.z);
+        m.w = fmaxf(m.w, v.w);
+      }
+    }
+    *reinterpret_cast<float4*>(yr + o * 4) = m;
+  }
+}
+
 // max pool, NHWC, 4 channels per thread (C % 4 == 0); padding taps are -inf.
 __global__ void maxpool4_kernel(const float* __restrict__ x, int B, int H, int W, int C, int k, int stride, int pad,
                                 int OH, int OW, float* __restrict__ y) {
@@ -224,7 +258,11 @@ extern "C" int rr_maxpool2d(rr_handle_t h, const float* x, int b, int hgt, int w
   if (total == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeElem, s);
-  if ((c & 3) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0)
+  const bool vec = (c & 3) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0;
+  if (vec && (long long)b * oh <= 0x7fffffffLL && (long long)wid * c < 0x7fffffffLL)
+    hipLaunchKernelGGL(maxpool4_row_kernel, dim3((unsigned)((long long)b * oh)), dim3(256), 0, s, x, hgt, wid, c, k,
+                       stride, pad, oh, ow, y);
+  else if (vec)
     hipLaunchKernelGGL(maxpool4_kernel, grid_for(total / 4, 256), dim3(256), 0, s, x, b, hgt, wid, c, k, stride, pad,
                        oh, ow, y);
   else

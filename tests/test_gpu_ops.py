@@ -46,10 +46,13 @@ def test_conv2d(cuda, b, h, w, cin, cout, k, s, p, res, relu):
     assert err < 1e-4 * max(1.0, ref.abs().max().item()), err
 
 
-def test_maxpool(cuda):
-    x = torch.randn(2, 17, 19, 64)
-    ref = F.max_pool2d(x.permute(0, 3, 1, 2), 3, 2, 1).permute(0, 2, 3, 1)
-    out = ops.maxpool2d(x.to(cuda), 3, 2, 1).cpu()
+@pytest.mark.parametrize("shape,k,s,p", [((2, 17, 19, 64), 3, 2, 1), ((3, 112, 112, 64), 3, 2, 1),
+                                         ((2, 9, 7, 8), 2, 2, 0), ((1, 5, 6, 4), 3, 1, 1)])
+def test_maxpool(cuda, shape, k, s, p):
+    """The row-blocked kernel (one block per output row) == torch max_pool2d."""
+    x = torch.randn(*shape)
+    ref = F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1)
+    out = ops.maxpool2d(x.to(cuda), k, s, p).cpu()
     assert torch.equal(out, ref)
 
 
