@@ -103,6 +103,71 @@ __global__ __launch_bounds__(256) void maxpool4_row_kernel(const float* __restri
   }
 }
 
+// The ResNet stem's 3x3 / stride 2 / pad 1 max pool, NHWC, C % 4 == 0: one
+// block per pair of output rows, each thread a 2x2 block of outputs x 4
+// channels from the 5x5 input window they share (25 loads for 4 outputs
+// instead of 36), row by row: per input row the max of columns 0-2 and of
+// columns 2-4.  Padding taps are -inf.
+typedef float mp_f32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void maxpool3s2_kernel(const float* __restrict__ x, int H, int W, int C, int OH,
+                                                         int OW, float* __restrict__ y) {
+  const int C4 = C >> 2;
+  const int OH2 = (OH + 1) >> 1, OW2 = (OW + 1) >> 1;
+  const int b = blockIdx.x / OH2, oh0 = 2 * (blockIdx.x - b * OH2);
+  const float* xb = x + (long long)b * H * W * C;
+  float* yb = y + (long long)b * OH * OW * C;
+  const float ninf = -__builtin_inff();
+  const int n = OW2 * C4;
+  for (int o = threadIdx.x; o < n; o += blockDim.x) {
+    const int owp = o / C4, c4 = o - owp * C4;
+    const int ow0 = 2 * owp;
+    mp_f32x4 m[2][2];  // [output row][output col]
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) m[r][q] = mp_f32x4{ninf, ninf, ninf, ninf};
+#pragma unroll
+    for (int dr = 0; dr < 5; ++dr) {
+      const int ih = 2 * oh0 - 1 + dr;
+      if ((unsigned)ih >= (unsigned)H) continue;
+      const float* xr = xb + (long long)ih * W * C + c4 * 4;
+      mp_f32x4 col[5];
+#pragma unroll
+      for (int dc = 0; dc < 5; ++dc) {
+        const int iw = 2 * ow0 - 1 + dc;
+        col[dc] = (unsigned)iw < (unsigned)W ? *reinterpret_cast<const mp_f32x4*>(xr + iw * C) : mp_f32x4{ninf, ninf, ninf, ninf};
+      }
+      mp_f32x4 p0, p1;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        p0[e] = fmaxf(fmaxf(col[0][e], col[1][e]), col[2][e]);
+        p1[e] = fmaxf(fmaxf(col[2][e], col[3][e]), col[4][e]);
+      }
+      // input row dr feeds output row 0 (dr 0-2) and output row 1 (dr 2-4)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (dr <= 2) {
+          m[0][0][e] = fmaxf(m[0][0][e], p0[e]);
+          m[0][1][e] = fmaxf(m[0][1][e], p1[e]);
+        }
+        if (dr >= 2) {
+          m[1][0][e] = fmaxf(m[1][0][e], p0[e]);
+          m[1][1][e] = fmaxf(m[1][1][e], p1[e]);
+        }
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      if (oh0 + r >= OH) continue;
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        if (ow0 + q >= OW) continue;
+        *reinterpret_cast<mp_f32x4*>(yb + ((long long)(oh0 + r) * OW + ow0 + q) * C + c4 * 4) = m[r][q];
+      }
+    }
+  }
+}
+
 // max pool, NHWC, 4 channels per thread (C % 4 == 0); padding taps are -inf.
 __global__ void maxpool4_kernel(const float* __restrict__ x, int B, int H, int W, int C, int k, int stride, int pad,
                                 int OH, int OW, float* __restrict__ y) {
@@ -259,7 +324,11 @@ extern "C" int rr_maxpool2d(rr_handle_t h, const float* x, int b, int hgt, int w
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeElem, s);
   const bool vec = (c & 3) == 0 && ((uintptr_t)x & 15) == 0 && ((uintptr_t)y & 15) == 0;
-  if (vec && (long long)b * oh <= 0x7fffffffLL && (long long)wid * c < 0x7fffffffLL)
+  if (vec && k == 3 && stride == 2 && pad == 1 && (long long)b * ((oh + 1) / 2) <= 0x7fffffffLL &&
+      (long long)wid * c < 0x7fffffffLL)
+    hipLaunchKernelGGL(maxpool3s2_kernel, dim3((unsigned)((long long)b * ((oh + 1) / 2))), dim3(256), 0, s, x, hgt,
+                       wid, c, oh, ow, y);
+  else if (vec && (long long)b * oh <= 0x7fffffffLL && (long long)wid * c < 0x7fffffffLL)
     hipLaunchKernelGGL(maxpool4_row_kernel, dim3((unsigned)((long long)b * oh)), dim3(256), 0, s, x, hgt, wid, c, k,
                        stride, pad, oh, ow, y);
   else if (vec)

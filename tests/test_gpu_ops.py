@@ -47,9 +47,11 @@ def test_conv2d(cuda, b, h, w, cin, cout, k, s, p, res, relu):
 
 
 @pytest.mark.parametrize("shape,k,s,p", [((2, 17, 19, 64), 3, 2, 1), ((3, 112, 112, 64), 3, 2, 1),
+                                         ((1, 1, 1, 4), 3, 2, 1), ((2, 2, 3, 8), 3, 2, 1), ((1, 6, 5, 12), 3, 2, 1),
                                          ((2, 9, 7, 8), 2, 2, 0), ((1, 5, 6, 4), 3, 1, 1)])
 def test_maxpool(cuda, shape, k, s, p):
-    """The row-blocked kernel (one block per output row) == torch max_pool2d."""
+    """The 2x2-blocked 3x3/2 kernel (odd and even output sizes, 1x1 input)
+    and the row-blocked kernel == torch max_pool2d."""
     x = torch.randn(*shape)
     ref = F.max_pool2d(x.permute(0, 3, 1, 2), k, s, p).permute(0, 2, 3, 1)
     out = ops.maxpool2d(x.to(cuda), k, s, p).cpu()
