@@ -37,9 +37,18 @@ from research_image_retrieval_amd.extract import _rescale  # noqa: E402
 
 METRIC = "images embedded+ranked/sec on 1.6M×2048 gallery; mAP on ROxf/RPar"
 # MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) per input dtype, HBM3E peak.
-# "s3": fp32 products as six bf16 MFMA products (gemm_s3.hip), so its ceiling
-# in algorithmic fp32 FLOP/s is the bf16 peak / 6.
-PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "fp8": 5000.0, "s3": 2500.0 / 6}
+# "s3": fp32 products as six bf16 MFMA products (gemm_s3.hip, SP 3), so its
+# ceiling in algorithmic fp32 FLOP/s is the bf16 peak / 6; "h2": three fp16
+# MFMA products (the f16x2 split, SP 2), the fp16 dense peak (= bf16's) / 3.
+PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "fp8": 5000.0, "s3": 2500.0 / 6, "h2": 2500.0 / 3}
+SPLIT_MATH = {
+    "s3": (6, "fp32 via exact 3-way bf16 split: 6 bf16 MFMA products per fp32 product, fp32 accumulation; "
+              "peak = bf16 dense peak / 6"),
+    "h2": (3, "fp32-accurate f16x2 split at power-of-two scales: 3 fp16 MFMA products per fp32 product "
+              "(a0b0 + a0b1 + a1b0, error vs float64 <= the exact-fp32 core's, tests/test_gpu_h2.py), fp32 "
+              "accumulation; peak = fp16 dense peak / 3"),
+}
+WEIGHT_BYTES = {"s3": 6, "h2": 4, "f32": 4}
 PEAK_HBM_GBS = 8000.0
 
 
@@ -79,7 +88,7 @@ def make_gallery(n_total, d, lo, hi, device, seed=0, kind="gaussian"):
     return g
 
 
-def build_extractor(arch, device, seed=0, conv_math="s3"):
+def build_extractor(arch, device, seed=0, conv_math="h2"):
     net = GeM(2048, backbone=arch, seed=seed, device=device, conv_math=conv_math)
     pw = ConvDimReduction(2048, 2048, device=device)
     w, b = W.synthetic_linear(2048, 2048, seed + 5, scale=1.0 / np.sqrt(2048))
@@ -344,14 +353,15 @@ def run_c2(a, world, rank, dev):
     ms, n = cls["conv_gemm"]
     if n:
         sec = ms / 1e3 / a.steps
-        dt = "s3" if a.conv_math == "s3" else "fp32"
+        dt = a.conv_math if a.conv_math in SPLIT_MATH else "fp32"
         ach = img_flops / sec / 1e12
         rk["conv_gemm"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
                            "frac": round(ach / PEAK_TFLOPS[dt], 4), "dtype": "fp32", "ms_per_step": round(ms / a.steps, 3),
                            "launches_per_step": n / a.steps, "algorithmic_flop_per_launch": img_flops / max(1.0, n / a.steps),
                            "algorithmic_bytes_per_launch": None, "traffic": None}
-        if dt == "s3":
-            rk["conv_gemm"]["math"] = "fp32 via exact 3-way bf16 split (6 bf16 MFMA products per fp32 product); peak = bf16 dense peak / 6"
+        if dt in SPLIT_MATH:
+            rk["conv_gemm"]["math"] = SPLIT_MATH[dt][1]
+            rk["conv_gemm"]["mfma_flop_per_launch"] = SPLIT_MATH[dt][0] * img_flops / max(1.0, n / a.steps)
     for name in ("select", "elementwise", "cosine_seed"):
         ms, n = cls[name]
         rk[name] = {"ms_per_step": round(ms / a.steps, 3), "launches_per_step": n / a.steps}
@@ -424,9 +434,11 @@ def main():
     ap.add_argument("--ranker", choices=("exhaustive", "prefilter"), default="prefilter",
                     help="fp32 exact ranking: exhaustive fp32 MFMA sweep, or the bf16-bound prefilter + exact "
                          "fp32 rescoring (bit-identical results)")
-    ap.add_argument("--conv-math", choices=("s3", "f32"), default="s3",
-                    help="ResNet trunk convs: s3 = fp32-accurate 3-way bf16 split on the bf16 matrix cores "
-                         "(error vs float64 <= the exact-fp32 core's, tests/test_gpu_s3.py); f32 = exact fp32 MFMA")
+    ap.add_argument("--conv-math", choices=("h2", "s3", "f32"), default="h2",
+                    help="ResNet trunk convs: h2 = fp32-accurate f16x2 split on the fp16 matrix cores, 3 MFMA "
+                         "products per fp32 product (tests/test_gpu_h2.py); s3 = 3-way bf16 split, 6 products "
+                         "(tests/test_gpu_s3.py); both with error vs float64 <= the exact-fp32 core's; "
+                         "f32 = exact fp32 MFMA")
     ap.add_argument("--ws-budget-gb", type=float, default=4.0,
                     help="ranker workspace budget per rank (bounded candidate buffers, overflowed queries re-run; "
                          "0 = the worst-case size, ~Q*N*8 bytes)")
@@ -633,13 +645,12 @@ def main():
     if a.workload in ("c3", "c5"):
         # per-layer algorithmic bytes (weights.resnet_conv_bytes) and the layer-wise
         # roofline floor sum_l max(FLOP_l / peak, bytes_l / HBM peak) of the conv class
-        s3 = a.conv_math == "s3"
-        pk = PEAK_TFLOPS["s3" if s3 else "fp32"] * 1e12
+        pk = PEAK_TFLOPS[a.conv_math if a.conv_math in SPLIT_MATH else "fp32"] * 1e12
         conv_bytes_step, floor = 0.0, 0.0
         for sc in (scales if a.workload == "c5" else (1.0,)):
             hh = int(224.0 * sc)
             fl_l = W.resnet_conv_flops(a.arch, hh, hh)
-            by_l = W.resnet_conv_bytes(a.arch, hh, hh, a.batch, weight_bytes=6 if s3 else 4)
+            by_l = W.resnet_conv_bytes(a.arch, hh, hh, a.batch, weight_bytes=WEIGHT_BYTES[a.conv_math])
             for name in fl_l:
                 conv_bytes_step += by_l[name]
                 floor += max(fl_l[name] * a.batch / pk, by_l[name] / (PEAK_HBM_GBS * 1e9))
@@ -657,7 +668,7 @@ def main():
         flop_filter = 2.0 * q_total * rows_filter * a.dim
     # (class, algorithmic FLOPs, algorithmic HBM bytes or None, dtype of its MFMA)
     searches = 2 if a.workload == "c5" else 1
-    conv_dt = a.dtype if a.workload == "c4" else ("s3" if a.conv_math == "s3" else "fp32")
+    conv_dt = a.dtype if a.workload == "c4" else (a.conv_math if a.conv_math in SPLIT_MATH else "fp32")
     # attention (C4): bf16 MFMA when the ViT runs in bf16; per layer it reads
     # the QKV rows once and writes the head outputs
     attn_dt = "bf16" if (a.workload == "c4" and a.dtype != "fp32") else "fp32"
@@ -684,17 +695,20 @@ def main():
             ach = fl_step / sec / 1e12
             e = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                  "frac": round(ach / peak, 4)}
-        if dt == "s3":
-            e["math"] = ("fp32 via exact 3-way bf16 split: 6 bf16 MFMA products per fp32 product, fp32 accumulation; "
-                         "peak = bf16 dense peak / 6 (every conv incl. the stem; the whiten and PCA-w linears, 0.2% of the FLOPs, run on the exact-fp32 core)")
-            e["mfma_flop_per_launch"] = 6.0 * fl_step / max(1.0, n / a.steps)
-        e.update({"dtype": "fp32" if dt == "s3" else dt, "ms_per_step": round(ms / a.steps, 3),
+        if dt in SPLIT_MATH:
+            e["math"] = SPLIT_MATH[dt][1] + (" (every conv incl. the stem; the whiten and PCA-w linears, 0.2% of "
+                                             "the FLOPs, run on the exact-fp32 core)")
+            e["mfma_flop_per_launch"] = SPLIT_MATH[dt][0] * fl_step / max(1.0, n / a.steps)
+            if dt == "h2":  # the previous core's ceiling, for comparison across rounds
+                e["frac_of_bf16x3_ceiling"] = round(e["achieved"] / PEAK_TFLOPS["s3"], 4) if e["unit"] == "TFLOP/s" else None
+        e.update({"dtype": "fp32" if dt in SPLIT_MATH else dt, "ms_per_step": round(ms / a.steps, 3),
                   "launches_per_step": n / a.steps,
                   "algorithmic_flop_per_launch": fl_step / max(1.0, n / a.steps),
                   "algorithmic_bytes_per_launch": (by_step / max(1.0, n / a.steps)) if by_step else None,
                   "traffic": ((traffic or {}).get(name) or {}).get("hbm_bytes_per_launch")
                   if (traffic and traffic.get("workload") == a.workload and a.gallery == 1_600_000
-                      and a.batch == traffic.get("batch", 320) and pre and a.conv_math == "s3") else None})
+                      and a.batch == traffic.get("batch", 320) and pre
+                      and a.conv_math == traffic.get("conv_math", "s3")) else None})
         if name == "conv_gemm" and conv_floor_ms is not None:
             e["layer_roofline_floor_ms_per_step"] = round(conv_floor_ms, 3)
             e["frac_of_layer_floor"] = round(conv_floor_ms / (ms / a.steps), 4)

@@ -37,6 +37,11 @@ extern "C" {
 #define RR_EWORKSPACE (-3) /* workspace too small */
 #define RR_EOVERFLOW (-4) /* candidate buffer overflow (see rr_cosine_topk) */
 
+/* Words of an activation's max-|x| record (rr_conv2d_h2, rr_amax_f32): the
+ * float bit patterns of per-wave maxima, hashed over this many words so no
+ * single address takes every atomic.  Zero them before the producing call. */
+#define RR_AMAX_SLOTS 64
+
 typedef struct rr_handle_s* rr_handle_t;
 
 /* ---- handle ------------------------------------------------------------ */
@@ -68,7 +73,7 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     4 (256x320 for bf16 filter / score sweeps, 256x256 otherwise),
  *                     5 (bf16 sweeps with K % 128 == 0: 256x256 8-phase pipeline;
  *                     otherwise as 3)
- *   RR_TUNE_S3_CFG:   split-bf16 core, 1..8 (gemm_s3.hip tile table)
+ *   RR_TUNE_S3_CFG:   split cores (bf16x3 and f16x2), 1..8 (gemm_s3.hip tile table)
  *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of
  *                     ~1 us for every other resident block (-1 = the library's pick)
  * Any other key or value: RR_EINVAL. */
@@ -280,6 +285,40 @@ int rr_linear_s3(rr_handle_t h, const float* x, int m, int k, const void* w3,
  * remainder, p2 = the rest).  Done once per weight tensor.                 */
 int rr_split3_bf16(rr_handle_t h, const float* x, long long n, void* planes,
                    void* stream);
+
+/* fp32-accurate convolution on the fp16 matrix cores (gemm_s3.hip, f16x2
+ * split): the same operation, layouts and epilogue as rr_conv2d_s3 at half
+ * its MFMA count.  Every fp32 operand is scaled by a power of two and split
+ * into two fp16 pieces, x 2^e = x0 + x1 + r with |r| <= 2^-22 |x 2^e|; a.b
+ * keeps a0b0 + (a0b1 + a1b0) (dropped terms <= 3 2^-22 |a||b|), three fp16
+ * MFMAs with exact products and fp32 accumulation (a0b0 in its own
+ * accumulator), and the accumulator is scaled back exactly.  Weights come
+ * from rr_split2_f16: w2 = planes [2][cout][K] (fp16 bit patterns), w_iscale
+ * [cout] the inverse row scales.  x_amax: the RR_AMAX_SLOTS-word max-|x|
+ * record of x (from the producing call's y_amax, or rr_amax_f32); y_amax
+ * (optional, zeroed by the caller): receives max |y| over the finite stored
+ * values.  Needs cin % 32 == 0, or cin == 4 for the NHWC4 stem (w2 then holds
+ * the flattened [kh][kw][4] filter zero-padded to K = kh*kw*4 rounded up to
+ * 32).  Replaces the same reference ops as rr_conv2d
+ * (networks/backbone.py:103-109, :305-346; models/gem_pooling.py:44,61).    */
+int rr_conv2d_h2(rr_handle_t h, const float* x, const unsigned* x_amax, int b,
+                 int hgt, int wid, int cin, const void* w2,
+                 const float* w_iscale, const float* bias, int cout, int kh,
+                 int kw, int stride, int pad, const float* residual, int relu,
+                 float* y, unsigned* y_amax, void* stream);
+
+/* fp16 2-way split of the rows of w [rows][k] (done once per weight tensor):
+ * row n is scaled by 2^e_n, its max |w| then in [2^14, 2^15), and split into
+ * planes [2][rows][kpad] (fp16 bit patterns, zero past k; kpad >= k, a
+ * multiple of 32 for rr_conv2d_h2); iscale[n] = 2^-e_n.                    */
+int rr_split2_f16(rr_handle_t h, const float* w, int rows, int k, int kpad,
+                  void* planes, float* iscale, void* stream);
+
+/* max |x| over the finite values of x[n] into the RR_AMAX_SLOTS words at
+ * amax (atomic max; zero them first): the x_amax record rr_conv2d_h2 needs
+ * for an input no earlier call produced.                                   */
+int rr_amax_f32(rr_handle_t h, const float* x, long long n, unsigned* amax,
+                void* stream);
 
 /* Max pool (torchvision ResNet stem maxpool 3x3/2 pad 1), NHWC. */
 int rr_maxpool2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int c,

@@ -10,6 +10,7 @@ namespace rr {
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef int i32x4 __attribute__((ext_vector_type(4)));
 typedef int i32x8 __attribute__((ext_vector_type(8)));
 
@@ -43,10 +44,52 @@ __device__ __forceinline__ float quick_gelu(float x) {
 // host); EPI = -1 reads them from g per element.  One set per kernel, not a
 // switch inside it: several inlined variants held extra values live through
 // the k-loop and spilled it.
-enum { EP_BIAS = 1, EP_RES = 2, EP_RELU = 4, EP_GELU = 8, EP_BF16 = 16 };
+// EP_SCALE / EP_AMAX (the f16x2 split core only, always compiled-in flag
+// sets): the accumulator times a per-column power-of-two scale before the
+// bias, and the max |C| of the stored values published to c_amax.
+enum { EP_BIAS = 1, EP_RES = 2, EP_RELU = 4, EP_GELU = 8, EP_BF16 = 16, EP_SCALE = 32, EP_AMAX = 64 };
 inline int ep_flags(const GemmArgs& g) {
   return (g.bias != nullptr ? EP_BIAS : 0) | (g.residual != nullptr ? EP_RES : 0) |
          (g.relu == 1 ? EP_RELU : g.relu == 2 ? EP_GELU : 0) | (g.out_bf16 ? EP_BF16 : 0);
+}
+
+// ---- f16x2 split scales (gemm_s3.hip, SP 2) ----
+// A tensor's max |x| lives in RR_AMAX_SLOTS words (float bit patterns of
+// non-negative values, so unsigned order = float order), each the max over
+// the waves that hashed to it: no single hot address.  Non-finite values are
+// left out (an inf / NaN input still turns its own outputs into NaN).
+__device__ __forceinline__ float amax_acc(float am, float x) {
+  const float a = __builtin_fabsf(x);
+  return a < __builtin_inff() ? __builtin_fmaxf(am, a) : am;
+}
+__device__ __forceinline__ void amax_publish(uint32_t* slots, float am, int slot) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am = __builtin_fmaxf(am, __shfl_xor(am, o));
+  if ((threadIdx.x & 63) == 0)
+    __hip_atomic_fetch_max(slots + (slot & (RR_AMAX_SLOTS - 1)), __float_as_uint(am), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+}
+// the max over the slots (every lane of the wave gets it)
+__device__ __forceinline__ uint32_t amax_load_slot(const uint32_t* slots) {
+  return __hip_atomic_load(slots + (threadIdx.x & (RR_AMAX_SLOTS - 1)), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float amax_reduce(uint32_t u) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const uint32_t v = (uint32_t)__shfl_xor((int)u, o);
+    u = v > u ? v : u;
+  }
+  return __uint_as_float(u);
+}
+// Power-of-two split exponent: amax * 2^e in [2^14, 2^15), so the fp16 high
+// piece of every scaled value is finite (< 65504) and values down to 2^-18 of
+// the max keep both pieces normal (22 significant bits); 0 for a zero or
+// non-finite max.  e >= -113 for every finite max; capped at 126 (a max
+// below 2^-111) so 2^e and 2^-e stay normal floats.
+__device__ __forceinline__ int h2_exp(float amax) {
+  if (!(amax > 0.f && amax < __builtin_inff())) return 0;
+  const int e = 15 - __builtin_amdgcn_frexp_expf(amax);
+  return e > 126 ? 126 : e;
 }
 
 // Write one staged slab (rows mb.. of the tile, row-major in ct): the LDS
@@ -59,7 +102,8 @@ inline int ep_flags(const GemmArgs& g) {
 // from g per element.
 template <int FL, int P, int ITERS, int NT, int C4, int BN, int BI>
 __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const float* ct, const f32x4 (&bias_v)[BI],
-                                           const f32x4 (&res)[ITERS], int tid, int mb, int n0) {
+                                           const f32x4 (&res)[ITERS], int tid, int mb, int n0, const f32x4 (&sc_v)[BI],
+                                           float& am) {
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   constexpr int GR = ITERS < 4 ? ITERS : (P == 1 ? 8 : 4);
   constexpr bool FIXED = FL >= 0;
@@ -99,6 +143,7 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
     }
     if (m >= g.M || n >= g.N) continue;
     f32x4 v = cv[it];
+    if constexpr (FIXED && (FL & EP_SCALE) != 0) v *= sc_v[BI == 1 ? 0 : it];
     if (has_bias) v += bias_v[BI == 1 ? 0 : it];
     if (has_res) v += res[it];
     if (act == 1) {
@@ -107,6 +152,10 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
     } else if (act == 2) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) v[e] = quick_gelu(v[e]);
+    }
+    if constexpr (FIXED && (FL & EP_AMAX) != 0) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) am = amax_acc(am, v[e]);
     }
     if (obf) {
       const bf16x4 ob = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
@@ -126,7 +175,7 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
 // barrier (the LDS is free).
 template <int WM, int WN, int FM, int FN, int CAPF, bool MF16 = false, int FL = -1>
 __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, const f32x16 (&acc)[FM][FN], float* lds,
-                                               int m0, int n0) {
+                                               int m0, int n0, float a_isc = 1.f) {
   constexpr int NT = 64 * WM * WN;
   constexpr int WTM = 32 * FM, WTN = 32 * FN;
   constexpr int BM = WTM * WM, BN = WTN * WN;
@@ -147,7 +196,10 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
   // NT % C4 == 0 (every configuration that stores C); otherwise one per
   // iteration.
   constexpr int BI = (NT % C4 == 0) ? 1 : ITERS;
-  f32x4 bias_v[BI];
+  constexpr bool SCALED = FL >= 0 && (FL & EP_SCALE) != 0;
+  static_assert(!(FL >= 0 && (FL & (EP_SCALE | EP_AMAX))) || BI == 1, "scaled epilogues: one column per thread");
+  f32x4 bias_v[BI], sc_v[BI];
+  float am = 0.f;
   if (vec_ok) {
 #pragma unroll
     for (int it = 0; it < BI; ++it) {
@@ -155,6 +207,8 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
       const int n = n0 + (idx % C4) * 4;
       bias_v[it] = (g.bias != nullptr && n < g.N) ? *reinterpret_cast<const f32x4*>(g.bias + n)
                                                   : f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (SCALED) sc_v[it] = (n < g.N ? *reinterpret_cast<const f32x4*>(g.col_scale + n)
+                                                : f32x4{0.f, 0.f, 0.f, 0.f}) * a_isc;
     }
   }
 #pragma unroll
@@ -205,11 +259,15 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
       // redefines the registers, so nothing below waits again.
 #pragma unroll
       for (int it = 0; it < BI; ++it) asm volatile("" : "+v"(bias_v[it]));
+      if constexpr (SCALED) {
+#pragma unroll
+        for (int it = 0; it < BI; ++it) asm volatile("" : "+v"(sc_v[it]));
+      }
       if (g.residual != nullptr) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) asm volatile("" : "+v"(res[it]));
       }
-      store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, BN, BI>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0);
+      store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, BN, BI>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0, sc_v, am);
     } else {
       for (int idx = tid; idx < SLAB * C4; idx += NT) {
         const int row = idx / C4, c4 = idx - row * C4;
@@ -221,15 +279,20 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
         for (int e = 0; e < 4; ++e) {
           if (n + e >= g.N) break;
           float x = v[e];
+          if constexpr (SCALED) x *= g.col_scale[n + e] * a_isc;
           if (g.bias != nullptr) x += g.bias[n + e];
           if (g.residual != nullptr) x += g.residual[o + e];
           if (g.relu == 1) x = fmaxf(x, 0.f);
           else if (g.relu == 2) x = quick_gelu(x);
+          if constexpr (FL >= 0 && (FL & EP_AMAX) != 0) am = amax_acc(am, x);
           if (g.out_bf16) reinterpret_cast<__bf16*>(Cb)[o + e] = (__bf16)x;
           else Cb[o + e] = x;
         }
       }
     }
+  }
+  if constexpr (FL >= 0 && (FL & EP_AMAX) != 0) {
+    if (g.c_amax != nullptr) amax_publish(g.c_amax, am, blockIdx.x * (NT / 64) + wave);
   }
 }
 

@@ -30,13 +30,58 @@
 #include "gemm_epilogue.hpp"
 #include "rr_internal.hpp"
 
-#ifndef RR_EXP
-#define RR_EXP 0
-#endif
 namespace rr {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+// Split kinds (template SP = planes per operand):
+//   3: bf16 x3 (above), six bf16 MFMAs per product;
+//   2: fp16 x2 at a power-of-two scale, three fp16 MFMAs per product.  An
+//      operand scaled so its max |x| lies in [2^14, 2^15) (h2_exp) splits as
+//      x 2^e = x0 + x1 + r, x0 = RNE16(x 2^e), x1 = RNE16(x 2^e - x0) (the
+//      difference is exact in fp32), |r| <= 2^-22 |x 2^e|: fp16 carries 11
+//      significant bits to bf16's 8, so two pieces hold 22 bits.  a.b keeps
+//      a0b0 (own accumulator) + a0b1 + a1b0; dropped: a1b1 and the two
+//      remainders, each <= 2^-22 |a||b| with random sign, so their sum over a
+//      long dot product stays below the fp32 accumulation's own rounding.
+//      Products of fp16 pieces are exact in the fp32 accumulator, and the
+//      scales are powers of two: the epilogue's acc * 2^-(ea + eb_n) is exact.
+//      Values below 2^-18 of their tensor's max lose relative precision (an
+//      absolute error <= 2^-40 of that max).  Same k-loop, LDS layout and
+//      epilogues as SP 3 with two planes per operand instead of three.
+template <int SP>
+struct S3Frag {
+  typedef bf16x8 T;
+};
+template <>
+struct S3Frag<2> {
+  typedef f16x8 T;
+};
+template <int SP>
+__device__ __forceinline__ f32x4 s3_mf16(const typename S3Frag<SP>::T& a, const typename S3Frag<SP>::T& b, f32x4 c) {
+  if constexpr (SP == 2) return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+template <int SP>
+__device__ __forceinline__ f32x16 s3_mf32(const typename S3Frag<SP>::T& a, const typename S3Frag<SP>::T& b, f32x16 c) {
+  if constexpr (SP == 2) return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+  else return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+
+// fp16 x2 split of 8 fp32 values (one 8-k chunk) at scale sc into two packed
+// planes: hi = RNE16(x sc), lo = RNE16(x sc - hi)
+__device__ __forceinline__ void split2h8(const f32x4 (&r)[2], float sc, u32x4& p0, u32x4& p1) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x2 v = f32x2{r[q >> 1][2 * (q & 1)], r[q >> 1][2 * (q & 1) + 1]} * sc;
+    const f16x2 h = __builtin_convertvector(v, f16x2);
+    const f16x2 l = __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2);
+    p0[q] = __builtin_bit_cast(uint32_t, h);
+    p1[q] = __builtin_bit_cast(uint32_t, l);
+  }
+}
 
 // exact 3-way split of x into bf16 pieces, returned as fp32 bit patterns
 // whose low 16 bits are zero
@@ -107,23 +152,35 @@ __device__ __forceinline__ void s3_launder(f32x4& v) { asm volatile("" : "+v"(v)
 // 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
 // 'DVFS give-back' item 7).  The k-tile's MFMAs go in two parts around the A
 // split: a0b0 + a1b1 + a0b1 + a1b0 (planes 0-1), then a0b2 + a2b0 (plane 2).
-template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0, int EPI = -1>
+template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0, int EPI = -1, int SP = 3>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
   static_assert(!MF16 || BK == 32, "MF16: BK 32");
+  static_assert(SP == 2 || SP == 3, "split kind");
+  static_assert(SP == 3 || (EPI >= 0 && (EPI & EP_SCALE)), "f16x2: scaled epilogue");
+  typedef typename S3Frag<SP>::T frag_t;
+  constexpr int NP = SP;                     // planes per operand
   constexpr int NT = 64 * WM * WN, NW = WM * WN;
   constexpr int WTM = 32 * FM, WTN = 32 * FN;
   constexpr int BM = WTM * WM, BN = WTN * WN;
   constexpr int SL = BK / 8;                 // 16-B slots per plane row
-  constexpr int A_EL = 3 * BM * BK;          // bf16 per stage: A planes
-  constexpr int BUF = A_EL + 3 * BN * BK;    // bf16 per stage: A + B planes
+  constexpr int A_EL = NP * BM * BK;         // 16-bit elements per stage: A planes
+  constexpr int BUF = A_EL + NP * BN * BK;   // 16-bit elements per stage: A + B planes
   constexpr int A_RPP = NT / SL;             // A rows staged per pass
   constexpr int A_CH = BM / A_RPP;           // A chunks (8 k each) per thread
   constexpr int B_RPI = 64 / SL;             // plane rows per LDS-DMA wave instruction
-  constexpr int B_TI = 3 * BN / B_RPI;       // LDS-DMA wave instructions per k-tile
+  constexpr int B_TI = NP * BN / B_RPI;      // LDS-DMA wave instructions per k-tile
   constexpr int B_INS = (B_TI + NW - 1) / NW; // ... per wave (the last round may be partial)
-  static_assert(BM % A_RPP == 0 && (3 * BN) % B_RPI == 0, "staging must tile the block");
+  static_assert(BM % A_RPP == 0 && (NP * BN) % B_RPI == 0, "staging must tile the block");
   static_assert(BK == 16 || BK == 32, "BK");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+  // f16x2 at one block per CU: room for the whole fp32 C tile, so the
+  // epilogue stages it in one slab (two planes leave the stages smaller)
+  constexpr int LDS_U16 = (SP == 2 && MINB == 1 && BM * BN > BUF) ? 2 * BM * BN : 2 * BUF;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
+
+  // the A operand's split scale (f16x2): its max-|x| record is loaded first,
+  // so it has landed by the prologue's first counted wait
+  uint32_t a_amax_w = 0;
+  if constexpr (SP == 2) a_amax_w = amax_load_slot(g.a_amax);
 
   // round stagger (GemmArgs): half of the first round's blocks start later,
   // so in every later round half the CUs run their k-loop while the other
@@ -133,6 +190,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     for (int i = 0; i < g.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(32);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float a_sc = 1.f, a_isc = 1.f;
   const int wm = wave % WM, wn = wave / WM;
   const int lr = lane & 31, lh = lane >> 5;
 
@@ -239,9 +297,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     }
   };
   // split the staged fp32 chunks into the three packed bf16 planes
-  u32x4 pk[A_CH][3];
+  u32x4 pk[A_CH][NP];
   auto split_a = [&](int rb) {
     const f32x4(&ra)[A_CH][2] = ra2[rb];
+    if constexpr (SP == 2) {
+#pragma unroll
+      for (int i = 0; i < A_CH; ++i) split2h8(ra[i], a_sc, pk[i][0], pk[i][1]);
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < A_CH; ++i) {
       uint32_t h[8], m[8], l[8];
@@ -258,7 +321,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       }
       pk[i][0] = u32x4{pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
       pk[i][1] = u32x4{pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7])};
-      pk[i][2] = u32x4{pack2(l[0], l[1]), pack2(l[2], l[3]), pack2(l[4], l[5]), pack2(l[6], l[7])};
+      pk[i][NP - 1] = u32x4{pack2(l[0], l[1]), pack2(l[2], l[3]), pack2(l[4], l[5]), pack2(l[6], l[7])};
     }
   };
   auto write_a = [&](int buf) {
@@ -268,7 +331,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       const int row = a_row + i * A_RPP;
       const int off = row * BK + pswz<BK>(row, a_slot) * 8;
 #pragma unroll
-      for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(la + p * BM * BK + off) = pk[i][p];
+      for (int p = 0; p < NP; ++p) *reinterpret_cast<u32x4*>(la + p * BM * BK + off) = pk[i][p];
     }
   };
   auto store_a = [&](int rb, int buf) {
@@ -315,40 +378,42 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     const uint16_t* la = lds + cur * BUF;
     const uint16_t* lb = la + A_EL;
     {
-      bf16x8 a[3][FM], b[3][FN];
+      frag_t a[NP][FM], b[NP][FN];
 #pragma unroll
-      for (int p = 0; p < 3; ++p) {
+      for (int p = 0; p < NP; ++p) {
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
           const int row = wm * WTM + i * 32 + lr;
-          a[p][i] = *reinterpret_cast<const bf16x8*>(la + (p * BM + row) * BK + pswz<BK>(row, 2 * st + lh) * 8);
+          a[p][i] = *reinterpret_cast<const frag_t*>(la + (p * BM + row) * BK + pswz<BK>(row, 2 * st + lh) * 8);
         }
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int row = wn * WTN + j * 32 + lr;
-          b[p][j] = *reinterpret_cast<const bf16x8*>(lb + (p * BN + row) * BK + pswz<BK>(row, 2 * st + lh) * 8);
+          b[p][j] = *reinterpret_cast<const frag_t*>(lb + (p * BN + row) * BK + pswz<BK>(row, 2 * st + lh) * 8);
         }
       }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) hi[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[0][j], hi[i][j], 0, 0, 0);
+        for (int j = 0; j < FN; ++j) hi[i][j] = s3_mf32<SP>(a[0][i], b[0][j], hi[i][j]);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           f32x16& L = lo[i][j];
-          L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[1][j], L, 0, 0, 0);
-          L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[2][j], L, 0, 0, 0);
-          L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[2][i], b[0][j], L, 0, 0, 0);
-          L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[0][i], b[1][j], L, 0, 0, 0);
-          L = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[1][i], b[0][j], L, 0, 0, 0);
+          if constexpr (SP == 3) {
+            L = s3_mf32<SP>(a[1][i], b[1][j], L);
+            L = s3_mf32<SP>(a[0][i], b[NP - 1][j], L);
+            L = s3_mf32<SP>(a[NP - 1][i], b[0][j], L);
+          }
+          L = s3_mf32<SP>(a[0][i], b[1][j], L);
+          L = s3_mf32<SP>(a[1][i], b[0][j], L);
         }
     }
   };
   // ---- MF16: 16x16x32 tiles, sub-tile t = 2a + b (row half a, column half b) ----
   f32x4 hi4[MF16 ? FM : 1][MF16 ? FN : 1][4], lo4[MF16 ? FM : 1][MF16 ? FN : 1][4];
-  bf16x8 fa[MF16 ? 3 : 1][MF16 ? FM : 1][2], fb[MF16 ? 3 : 1][MF16 ? FN : 1][2];
+  frag_t fa[MF16 ? NP : 1][MF16 ? FM : 1][2], fb[MF16 ? NP : 1][MF16 ? FN : 1][2];
   if constexpr (MF16) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -371,22 +436,22 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int row = wm * WTM + i * 32 + h * 16 + l16;
-        fa[MF16 ? p : 0][i][h] = *reinterpret_cast<const bf16x8*>(la + (p * BM + row) * BK + pswz<BK>(row, lg) * 8);
+        fa[MF16 ? p : 0][i][h] = *reinterpret_cast<const frag_t*>(la + (p * BM + row) * BK + pswz<BK>(row, lg) * 8);
       }
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int row = wn * WTN + j * 32 + h * 16 + l16;
-        fb[MF16 ? p : 0][j][h] = *reinterpret_cast<const bf16x8*>(lb + (p * BN + row) * BK + pswz<BK>(row, lg) * 8);
+        fb[MF16 ? p : 0][j][h] = *reinterpret_cast<const frag_t*>(lb + (p * BN + row) * BK + pswz<BK>(row, lg) * 8);
       }
   };
-#define RR_MF16(a, b, c) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
-  // k-tile of MFMAs in two parts.  lo1: the plane-1 products (a1b1, a0b1,
-  // a1b0) into lo; rest: a0b0 into hi, then the plane-2 products (a0b2,
-  // a2b0) into lo — the same per-accumulator order as one pass — with the A
-  // split + LDS store of the next stage interleaved one VALU per MFMA (the
-  // plane-1 fragments are dead by then, which leaves the registers for it).
+#define RR_MF16(a, b, c) c = s3_mf16<SP>(a, b, c)
+  // k-tile of MFMAs in two parts.  lo1: the plane-1 products into lo (SP 3:
+  // a1b1, a0b1, a1b0; SP 2: a0b1, a1b0); rest: a0b0 into hi, then (SP 3) the
+  // plane-2 products (a0b2, a2b0) into lo — the same per-accumulator order as
+  // one pass — with the A split + LDS store of the next stage interleaved
+  // (the plane-1 fragments are dead by then, which leaves the registers for it).
   auto mf_lo1 = [&](int cur) {
     if constexpr (MF16) {
       rd_mf(cur, 0);
@@ -397,7 +462,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            RR_MF16(fa[1][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
+            if constexpr (SP == 3) RR_MF16(fa[1][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
             RR_MF16(fa[0][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
             RR_MF16(fa[1][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
           }
@@ -406,10 +471,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   // with two A chunks per thread the plane-0 fragments are re-read for the
   // plane-2 products rather than held across the A split (holding them spills)
   constexpr bool MF_REREAD = A_CH >= 2;
-  // dense A (1x1 convs, linears): a0b0 + the plane-1 products, then the
+  // dense A (1x1 convs, linears), SP 3: a0b0 + the plane-1 products, then the
   // split, then the plane-2 products (the order above measured slower there)
   auto mf_dense0 = [&](int cur) {
-    if constexpr (MF16) {
+    if constexpr (MF16 && SP == 3) {
       rd_mf(cur, 0);
       rd_mf(cur, 1);
 #pragma unroll
@@ -431,17 +496,17 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     }
   };
   auto mf_dense1 = [&](int cur) {
-    if constexpr (MF16) {
+    if constexpr (MF16 && SP == 3) {
       if constexpr (MF_REREAD) rd_mf(cur, 0);
-      rd_mf(cur, 2);
+      rd_mf(cur, NP - 1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int t = 0; t < 4; ++t) {
-            RR_MF16(fa[0][i][t >> 1], fb[2][j][t & 1], lo4[i][j][t]);
-            RR_MF16(fa[2][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
+            RR_MF16(fa[0][i][t >> 1], fb[NP - 1][j][t & 1], lo4[i][j][t]);
+            RR_MF16(fa[NP - 1][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
           }
     }
   };
@@ -449,27 +514,39 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     if constexpr (MF16) {
       split_a(nxt);
       write_a(nxt);  // the other stage is free since the last barrier
+      // f16x2: the conv A loader's state leaves no room to hold the plane-0
+      // fragments across the split (2 registers spilled): re-read them
+      if constexpr (SP == 2 && (MF_REREAD || AMODE != A_DENSE)) rd_mf(cur, 0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int t = 0; t < 4; ++t) RR_MF16(fa[0][i][t >> 1], fb[0][j][t & 1], hi4[i][j][t]);
-      if constexpr (MF_REREAD) rd_mf(cur, 0);
-      rd_mf(cur, 2);
+      if constexpr (SP == 3) {
+        if constexpr (MF_REREAD) rd_mf(cur, 0);
+        rd_mf(cur, NP - 1);
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j)
+          for (int j = 0; j < FN; ++j)
 #pragma unroll
-          for (int t = 0; t < 4; ++t) {
-            RR_MF16(fa[0][i][t >> 1], fb[2][j][t & 1], lo4[i][j][t]);
-            RR_MF16(fa[2][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
-          }
+            for (int t = 0; t < 4; ++t) {
+              RR_MF16(fa[0][i][t >> 1], fb[NP - 1][j][t & 1], lo4[i][j][t]);
+              RR_MF16(fa[NP - 1][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
+            }
 #pragma unroll
-      for (int x = 0; x < 3 * FM * FN * 4; ++x) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-        __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // 1 VALU
+        for (int x = 0; x < 3 * FM * FN * 4; ++x) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 1, 0);  // 1 VALU
+        }
+      } else {
+        // SP 2: the split's VALU (about 3 per element) two per MFMA gap
+#pragma unroll
+        for (int x = 0; x < FM * FN * 4; ++x) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // 2 VALU
+        }
       }
     }
   };
@@ -497,6 +574,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     glds_b(0, 0);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_INS) : "memory");  // A(0) landed
     launder_a(0);
+    if constexpr (SP == 2) {
+      // uniform: the exponent and both powers of two stay in scalar registers
+      const int e = __builtin_amdgcn_readfirstlane(h2_exp(amax_reduce(a_amax_w)));
+      a_sc = __int_as_float((127 + e) << 23);
+      a_isc = __int_as_float((127 - e) << 23);
+    }
     store_a(0, 0);
     load_a(nk > 1 ? 1 : 0, 1);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B(0) landed
@@ -506,7 +589,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
     auto iter = [&](int kt, int cur) __attribute__((always_inline)) {
       glds_b(min(kt + 1, nk - 1), cur ^ 1);
       load_a(min(kt + 2, nk - 1), cur);
-      if constexpr (MF16 && AMODE == A_DENSE) {
+      if constexpr (MF16 && AMODE == A_DENSE && SP == 3) {
         mf_dense0(cur);
         asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
         launder_a(cur ^ 1);
@@ -565,7 +648,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 #pragma unroll
       for (int j = 0; j < FN; ++j) hi[i][j] += lo[i][j];
   }
-  epilogue_store<WM, WN, FM, FN, BUF, (bool)MF16, EPI>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0);
+  epilogue_store<WM, WN, FM, FN, LDS_U16 / 2, (bool)MF16, EPI>(g, g.C, hi, reinterpret_cast<float*>(lds), m0, n0, a_isc);
 }
 
 // ---- Persistent 128x256 tile (config 8) ------------------------------------
@@ -588,15 +671,23 @@ __device__ __forceinline__ int s3_opaque(int v) {
   return v;
 }
 
-template <int EPI>
+template <int EPI, int SP = 3>
 __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_n, int ntiles) {
+  static_assert(SP == 3 || (EPI & EP_SCALE), "f16x2: scaled epilogue");
+  typedef typename S3Frag<SP>::T frag_t;
+  constexpr int NP = SP;
   constexpr int WM = 2, FM = 2, FN = 2, BK = 32, NT = 512, NW = 8;
   constexpr int WTM = 64, WTN = 64, BM = 128, BN = 256, SL = BK / 8;
-  constexpr int A_EL = 3 * BM * BK, BUF = A_EL + 3 * BN * BK;
-  constexpr int B_INS = 3 * BN / (64 / SL) / NW;  // LDS-DMA instructions per wave per k-tile (6)
-  constexpr int A_LD = 2;                         // A loads per thread per k-tile
-  static_assert(B_INS * NW * (64 / SL) == 3 * BN, "B staging must tile the block");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF];
+  constexpr int A_EL = NP * BM * BK, BUF = A_EL + NP * BN * BK;
+  // stage stride: a stage also stages one 64-row slab of C (64 KB) in the epilogue
+  constexpr int STG = BUF > 64 * BN * 2 ? BUF : 64 * BN * 2;
+  constexpr int B_INS = NP * BN / (64 / SL) / NW;  // LDS-DMA instructions per wave per k-tile (6 / 4)
+  constexpr int A_LD = 2;                          // A loads per thread per k-tile
+  static_assert(B_INS * NW * (64 / SL) == NP * BN, "B staging must tile the block");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STG];
+  uint32_t a_amax_w = 0;
+  if constexpr (SP == 2) a_amax_w = amax_load_slot(g.a_amax);
+  float a_sc = 1.f, a_isc = 1.f, am = 0.f;
 
   // round stagger: every block is resident from the start, so half of them
   // (every other XCD slot) start later and the halves stay out of phase
@@ -648,8 +739,12 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
       a_tile(++a_tl);
     }
   };
-  u32x4 pk[3];
+  u32x4 pk[NP];
   auto split_a = [&](int rb) {
+    if constexpr (SP == 2) {
+      split2h8(ra2[rb], a_sc, pk[0], pk[1]);
+      return;
+    }
     uint32_t h[8], m[8], l[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -662,14 +757,14 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
     }
     pk[0] = u32x4{pack2(h[0], h[1]), pack2(h[2], h[3]), pack2(h[4], h[5]), pack2(h[6], h[7])};
     pk[1] = u32x4{pack2(m[0], m[1]), pack2(m[2], m[3]), pack2(m[4], m[5]), pack2(m[6], m[7])};
-    pk[2] = u32x4{pack2(l[0], l[1]), pack2(l[2], l[3]), pack2(l[4], l[5]), pack2(l[6], l[7])};
+    pk[NP - 1] = u32x4{pack2(l[0], l[1]), pack2(l[2], l[3]), pack2(l[4], l[5]), pack2(l[6], l[7])};
   };
   auto write_a = [&](int buf) {
-    uint16_t* la = lds + buf * BUF;
+    uint16_t* la = lds + buf * STG;
     const int a_slot = tid % SL, a_row = tid / SL;
     const int off = a_row * BK + pswz<BK>(a_row, a_slot) * 8;
 #pragma unroll
-    for (int p = 0; p < 3; ++p) *reinterpret_cast<u32x4*>(la + p * BM * BK + off) = pk[p];
+    for (int p = 0; p < NP; ++p) *reinterpret_cast<u32x4*>(la + p * BM * BK + off) = pk[p];
   };
   auto launder_a = [&](int rb) {
     s3_launder(ra2[rb][0]);
@@ -690,7 +785,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
   };
   b_tile(0);
   auto glds_b = [&](int buf) {
-    uint16_t* lb = lds + buf * BUF + A_EL;
+    uint16_t* lb = lds + buf * STG + A_EL;
 #pragma unroll
     for (int i = 0; i < B_INS; ++i)
       __builtin_amdgcn_global_load_lds((const void*)(b_src + (i >> 1) * g.b_plane + (long long)(i & 1) * (BN / 2) * g.ldb +
@@ -717,27 +812,27 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
         }
   };
   zero_acc();
-  bf16x8 fa[3][FM][2], fb[3][FN][2];
+  frag_t fa[NP][FM][2], fb[NP][FN][2];
   const int l16 = lane & 15, lg = lane >> 4;
   auto rd_mf = [&](int cur, int p) {
-    const uint16_t* la = lds + cur * BUF;
+    const uint16_t* la = lds + cur * STG;
     const uint16_t* lb = la + A_EL;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int row = wm * WTM + i * 32 + h * 16 + l16;
-        fa[p][i][h] = *reinterpret_cast<const bf16x8*>(la + (p * BM + row) * BK + pswz<BK>(row, lg) * 8);
+        fa[p][i][h] = *reinterpret_cast<const frag_t*>(la + (p * BM + row) * BK + pswz<BK>(row, lg) * 8);
       }
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int row = wn * WTN + j * 32 + h * 16 + l16;
-        fb[p][j][h] = *reinterpret_cast<const bf16x8*>(lb + (p * BN + row) * BK + pswz<BK>(row, lg) * 8);
+        fb[p][j][h] = *reinterpret_cast<const frag_t*>(lb + (p * BN + row) * BK + pswz<BK>(row, lg) * 8);
       }
   };
-#define RR_MF16(a, b, c) c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0)
+#define RR_MF16(a, b, c) c = s3_mf16<SP>(a, b, c)
   auto mf_hi = [&]() {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -753,7 +848,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          RR_MF16(fa[1][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
+          if constexpr (SP == 3) RR_MF16(fa[1][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
           RR_MF16(fa[0][i][t >> 1], fb[1][j][t & 1], lo4[i][j][t]);
           RR_MF16(fa[1][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
         }
@@ -765,8 +860,8 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
-          RR_MF16(fa[0][i][t >> 1], fb[2][j][t & 1], lo4[i][j][t]);
-          RR_MF16(fa[2][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
+          RR_MF16(fa[0][i][t >> 1], fb[NP - 1][j][t & 1], lo4[i][j][t]);
+          RR_MF16(fa[NP - 1][i][t >> 1], fb[0][j][t & 1], lo4[i][j][t]);
         }
   };
 #undef RR_MF16
@@ -794,9 +889,11 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
     tile_origin(tl, m0, n0);
     const int te = s3_opaque(tid);
     const int c40 = te % C4, r0 = te / C4;
-    f32x4 bias_v[1] = {f32x4{0.f, 0.f, 0.f, 0.f}};
+    f32x4 bias_v[1] = {f32x4{0.f, 0.f, 0.f, 0.f}}, sc_v[1];
     if ((EPI & EP_BIAS) && g.bias != nullptr) bias_v[0] = *reinterpret_cast<const f32x4*>(g.bias + n0 + c40 * 4);
+    if constexpr ((EPI & EP_SCALE) != 0) sc_v[0] = *reinterpret_cast<const f32x4*>(g.col_scale + n0 + c40 * 4) * a_isc;
     asm volatile("" : "+v"(bias_v[0]));
+    if constexpr ((EPI & EP_SCALE) != 0) asm volatile("" : "+v"(sc_v[0]));
     f32x4 res[2][2][HITERS];  // [slab][band][row chunk]
     auto load_res = [&](int sl) {
       if constexpr ((EPI & EP_RES) != 0) {
@@ -810,7 +907,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
           }
       }
     };
-    float* ct = reinterpret_cast<float*>(lds + buf * BUF);  // [2 bands x 32 rows][BN]
+    float* ct = reinterpret_cast<float*>(lds + buf * STG);  // [2 bands x 32 rows][BN]
     const int le = te & 63;
     auto stage = [&](int sl) {
       float* cw = ct + (wm * 32) * BN + wn * WTN;
@@ -832,7 +929,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         store_slab<EPI, 2, HITERS, NT, C4, BN, 1>(g, g.C, ct + q * 32 * BN, bias_v, res[sl][q], te,
-                                                  m0 + q * 64 + sl * 32, n0);
+                                                  m0 + q * 64 + sl * 32, n0, sc_v, am);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every LDS read of the slab done
       asm volatile("" ::: "memory");
@@ -852,6 +949,12 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
   glds_b(0);
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_INS) : "memory");  // A(0) landed
   launder_a(0);
+  if constexpr (SP == 2) {
+    // uniform: the exponent and both powers of two stay in scalar registers
+    const int e = __builtin_amdgcn_readfirstlane(h2_exp(amax_reduce(a_amax_w)));
+    a_sc = __int_as_float((127 + e) << 23);
+    a_isc = __int_as_float((127 - e) << 23);
+  }
   split_a(0);
   write_a(0);
   load_a(1);
@@ -873,13 +976,28 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
     load_a(cur);
     rd_mf(cur, 0);
     rd_mf(cur, 1);
-    mf_hi();
-    mf_lo1();
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
-    launder_a(cur ^ 1);
-    split_a(cur ^ 1);
-    rd_mf(cur, 2);
-    mf_lo2();
+    if constexpr (SP == 3) {
+      mf_hi();
+      mf_lo1();
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
+      launder_a(cur ^ 1);
+      split_a(cur ^ 1);
+      rd_mf(cur, NP - 1);
+      mf_lo2();
+    } else {
+      // f16x2: the plane-1 products, then a0b0 with the split of A(j+1) two
+      // VALU per MFMA gap (same per-accumulator order as config 4)
+      mf_lo1();
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
+      launder_a(cur ^ 1);
+      split_a(cur ^ 1);
+      mf_hi();
+#pragma unroll
+      for (int x = 0; x < FM * FN * 4; ++x) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // 2 VALU
+      }
+    }
     write_a(cur ^ 1);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of j+1 landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -899,9 +1017,12 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   launder_a(0);
   launder_a(1);
+  if constexpr ((EPI & EP_AMAX) != 0) {
+    if (g.c_amax != nullptr) amax_publish(g.c_amax, am, bid * NW + wave);
+  }
 }
 
-template <int EPI>
+template <int EPI, int SP = 3>
 static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   const long long tiles_m = (g.M + 127) / 128, tiles_n = g.N / 256;
   const long long ntiles = tiles_m * tiles_n;
@@ -913,27 +1034,44 @@ static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
   const int grid = ntiles <= slots ? (int)ntiles : slots;
   g.stagger_blocks = grid;
   g.stagger_sleeps = ntiles > 2LL * grid ? stagger : 0;
-  hipLaunchKernelGGL((gemm_s3p_kernel<EPI>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
+  hipLaunchKernelGGL((gemm_s3p_kernel<EPI, SP>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
   return hipGetLastError();
 }
 
+// f16x2 epilogue flag sets: the scale, the max-|C| record (skipped at run
+// time when c_amax is NULL) and the bias (zeros when NULL) always compiled
+// in; residual and ReLU select the instance
+constexpr int H2_EP = EP_SCALE | EP_AMAX | EP_BIAS;
+
 // config 8 serves dense A (1x1 convs), N % 256 == 0 and the ResNet's flag
-// sets (conv + BN + ReLU, + residual + ReLU, the projection conv); the rest
-// falls back to the library's pick
+// sets (conv + BN + ReLU, + residual + ReLU, the projection conv; f16x2: any
+// residual / ReLU combination); the rest falls back to the library's pick
+template <int SP>
 static bool s3_persist_ok(const GemmArgs& g, int amode) {
   const int f = ep_flags(g);
-  return (g.N % 256) == 0 && amode == A_DENSE &&
-         (f == (EP_BIAS | EP_RELU) || f == (EP_BIAS | EP_RES | EP_RELU) || f == EP_BIAS);
+  if ((g.N % 256) != 0 || amode != A_DENSE) return false;
+  if constexpr (SP == 2) return true;
+  return f == (EP_BIAS | EP_RELU) || f == (EP_BIAS | EP_RES | EP_RELU) || f == EP_BIAS;
 }
+template <int SP>
 static hipError_t launch_s3p(const GemmArgs& g, hipStream_t s, int n_cu, int st) {
-  switch (ep_flags(g)) {
-    case EP_BIAS | EP_RELU: return launch_s3p_t<EP_BIAS | EP_RELU>(g, s, n_cu, st);
-    case EP_BIAS | EP_RES | EP_RELU: return launch_s3p_t<EP_BIAS | EP_RES | EP_RELU>(g, s, n_cu, st);
-    default: return launch_s3p_t<EP_BIAS>(g, s, n_cu, st);
+  if constexpr (SP == 2) {
+    switch (ep_flags(g) & (EP_RES | EP_RELU)) {
+      case EP_RELU: return launch_s3p_t<H2_EP | EP_RELU, 2>(g, s, n_cu, st);
+      case EP_RES | EP_RELU: return launch_s3p_t<H2_EP | EP_RES | EP_RELU, 2>(g, s, n_cu, st);
+      case EP_RES: return launch_s3p_t<H2_EP | EP_RES, 2>(g, s, n_cu, st);
+      default: return launch_s3p_t<H2_EP, 2>(g, s, n_cu, st);
+    }
+  } else {
+    switch (ep_flags(g)) {
+      case EP_BIAS | EP_RELU: return launch_s3p_t<EP_BIAS | EP_RELU>(g, s, n_cu, st);
+      case EP_BIAS | EP_RES | EP_RELU: return launch_s3p_t<EP_BIAS | EP_RES | EP_RELU>(g, s, n_cu, st);
+      default: return launch_s3p_t<EP_BIAS>(g, s, n_cu, st);
+    }
   }
 }
 
-template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int EPI = -1>
+template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int EPI = -1, int SP = 3>
 static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
@@ -944,16 +1082,17 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
   constexpr int PER_CU = (MINB * 4) / (WM * WN) > 1 ? (MINB * 4) / (WM * WN) : 1;
   g.stagger_blocks = n_cu * PER_CU;
   g.stagger_sleeps = nblk > 2LL * n_cu * PER_CU ? stagger : 0;  // only grids of several rounds
-  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16, EPI>), dim3((unsigned)nblk), dim3(64 * WM * WN),
-                     0, s, g, (int)tiles_n);
+  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16, EPI, SP>), dim3((unsigned)nblk),
+                     dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
 
-// Tile configs (waves WMxWN, MFMA tiles per wave FMxFN, BK, blocks per CU):
+// Tile configs (waves WMxWN, MFMA tiles per wave FMxFN, BK, blocks per CU;
+// LDS of the bf16x3 split, two thirds of it for f16x2):
 //   1: 128x128, 4 waves of 64x64, BK 16, 2/CU (48 KB LDS)
 //   2: 128x128, 4 waves of 64x64, BK 32, 1/CU (96 KB)
 //   3: 256x128, 8 waves of 64x64, BK 32, 1/CU (144 KB)
-//   4: 128x256, 8 waves of 64x64, BK 32, 1/CU (144 KB), v_mfma_f32_16x16x32_bf16
+//   4: 128x256, 8 waves of 64x64, BK 32, 1/CU (144 KB), v_mfma_f32_16x16x32_{bf16,f16}
 //   5: 256x64,  4 waves of 64x64, BK 32, 1/CU (120 KB)
 //   6: 256x64,  4 waves of 64x64, BK 16, 2/CU (60 KB)
 //   7: 256x64,  8 waves of 32x64, BK 16, 2/CU (60 KB), 4 waves per SIMD
@@ -961,16 +1100,17 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //      stem 2-7 % faster than 6, profiles/r02f_s3_cfg7.txt)
 //   8: config 4 as a persistent k-stream (gemm_s3p_kernel): dense A, N % 256
 //      == 0 — the picked tile for the 1x1 layers it serves
-// (all others on v_mfma_f32_32x32x16_bf16).  Measured per R101 layer at 320
-// images (tools/s3_bench.py): 3 is the fastest wherever N >= 128 (1.1-1.3x
-// config 1 per FLOP); 4 on 16x16x32 runs every N % 256 == 0 layer 3-14 %
-// faster than 3 (the 16x16 shape holds a higher clock on random operands,
-// MI355X_MICROARCH.md 'DVFS give-back' item 7; the same shape is slower in the
-// one-wave-per-SIMD configs 2 and 5 and spills in 3).  Not kept:
-// an all-DMA ring with the A split at fragment-read time (10-15 % slower), a
-// one-wave-per-SIMD 256x128 variant (1.16x slower), a single accumulator for
-// all six terms (less accurate than exact fp32).  rr_set_tuning(RR_TUNE_S3_CFG)
-// forces a config (tests, tools).
+// (all others on v_mfma_f32_32x32x16_{bf16,f16}).  The f16x2 split is built
+// for the picked configs 3, 4, 7 and 8 (a forced 1, 2, 5 or 6 runs the pick).
+// Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the fastest
+// wherever N >= 128 (1.1-1.3x config 1 per FLOP); 4 on 16x16x32 runs every
+// N % 256 == 0 layer 3-14 % faster than 3 (the 16x16 shape holds a higher
+// clock on random operands, MI355X_MICROARCH.md 'DVFS give-back' item 7; the
+// same shape is slower in the one-wave-per-SIMD configs 2 and 5 and spills in
+// 3).  Not kept: an all-DMA ring with the A split at fragment-read
+// time (10-15 % slower), a one-wave-per-SIMD 256x128 variant (1.16x slower), a
+// single accumulator for all six terms (less accurate than exact fp32).
+// rr_set_tuning(RR_TUNE_S3_CFG) forces a config (tests, tools).
 static int pick_s3(const GemmArgs& g, int forced) {
   if (forced >= 1 && forced <= 8) return forced;
   if ((g.N % 256) == 0) return 4;
@@ -986,17 +1126,36 @@ static int pick_s3(const GemmArgs& g, int forced) {
   if (cost(256, 64, 2, 1.0) < best) best = cost(256, 64, 2, 1.0), cfg = 7;
   return cfg;
 }
+// f16x2: config 1 (no f16x2 build) -> 3 where it tiles no worse than 7
+static int pick_h2(const GemmArgs& g, int forced) {
+  int cfg = pick_s3(g, forced);
+  if (cfg == 3 || cfg == 4 || cfg == 7 || cfg == 8) return cfg;
+  cfg = pick_s3(g, 0);
+  if (cfg == 1) cfg = (g.N % 128) == 0 ? 3 : 7;
+  return cfg;
+}
 
 // The picked configs (3, 4, 7) with the ResNet's epilogues compiled in:
-// conv + BN + ReLU, + residual + ReLU, projection conv + BN.
-template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0>
+// conv + BN + ReLU, + residual + ReLU, projection conv + BN (f16x2: the four
+// residual / ReLU combinations of H2_EP).
+template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int SP = 3>
 static hipError_t launch_s3_ep(const GemmArgs& g, hipStream_t s, int n_cu, int st) {
-  switch (ep_flags(g)) {
-    case EP_BIAS | EP_RELU: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS | EP_RELU>(g, s, n_cu, st);
-    case EP_BIAS | EP_RES | EP_RELU:
-      return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS | EP_RES | EP_RELU>(g, s, n_cu, st);
-    case EP_BIAS: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS>(g, s, n_cu, st);
-    default: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16>(g, s, n_cu, st);
+  if constexpr (SP == 2) {
+    switch (ep_flags(g) & (EP_RES | EP_RELU)) {
+      case EP_RELU: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RELU, 2>(g, s, n_cu, st);
+      case EP_RES | EP_RELU:
+        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RES | EP_RELU, 2>(g, s, n_cu, st);
+      case EP_RES: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RES, 2>(g, s, n_cu, st);
+      default: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP, 2>(g, s, n_cu, st);
+    }
+  } else {
+    switch (ep_flags(g)) {
+      case EP_BIAS | EP_RELU: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS | EP_RELU>(g, s, n_cu, st);
+      case EP_BIAS | EP_RES | EP_RELU:
+        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS | EP_RES | EP_RELU>(g, s, n_cu, st);
+      case EP_BIAS: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS>(g, s, n_cu, st);
+      default: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16>(g, s, n_cu, st);
+    }
   }
 }
 
@@ -1006,10 +1165,10 @@ static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int
   // config 8 is the default wherever it serves (every dense R101 layer with
   // N % 256 == 0: 1.0-1.1x config 4, residual expansions -4 to -9 %,
   // profiles/r02k_s3p_ab.txt)
-  if (forced == 0 && AM == A_DENSE && s3_persist_ok(g, AM)) cfg = 8;
+  if (forced == 0 && AM == A_DENSE && s3_persist_ok<3>(g, AM)) cfg = 8;
   if (cfg == 8) {
     if constexpr (AM == A_DENSE) {
-      if (s3_persist_ok(g, AM)) return launch_s3p(g, s, n_cu, st);
+      if (s3_persist_ok<3>(g, AM)) return launch_s3p<3>(g, s, n_cu, st);
     }
     cfg = pick_s3(g, 0);  // a shape or flag set config 8 does not serve
   }
@@ -1024,7 +1183,24 @@ static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int
   }
 }
 
-int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls) {
+template <int AM>
+static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
+  int cfg = pick_h2(g, forced);
+  if (forced == 0 && AM == A_DENSE && s3_persist_ok<2>(g, AM)) cfg = 8;
+  if (cfg == 8) {
+    if constexpr (AM == A_DENSE) {
+      if (s3_persist_ok<2>(g, AM)) return launch_s3p<2>(g, s, n_cu, st);
+    }
+    cfg = pick_h2(g, 0);
+  }
+  switch (cfg) {
+    case 4: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1, 2>(g, s, n_cu, st);
+    case 7: return launch_s3_ep<8, 1, 1, 2, 16, AM, 4, 0, 2>(g, s, n_cu, st);
+    default: return launch_s3_ep<4, 2, 2, 2, 32, AM, 1, 0, 2>(g, s, n_cu, st);
+  }
+}
+
+int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls, int sp) {
   if (g.M < 0 || g.N <= 0 || g.K <= 0) return set_error(h, RR_EINVAL, "gemm_s3: bad shape");
   if (g.K % 32) return set_error(h, RR_EINVAL, "gemm_s3: K must be a multiple of 32");
   if (amode == A_DENSE && ((g.lda & 3) || ((uintptr_t)g.A & 15)))
@@ -1036,6 +1212,13 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
     return set_error(h, RR_EINVAL, "gemm_s3: unsupported A mode");
   if ((g.ldb & 7) || (g.b_plane & 7) || ((uintptr_t)g.B & 15))
     return set_error(h, RR_EINVAL, "gemm_s3: B planes need ldb % 8 == 0, plane stride % 8 == 0, 16-B alignment");
+  if (sp != 2 && sp != 3) return set_error(h, RR_EINVAL, "gemm_s3: split kind must be 2 or 3");
+  if (sp == 2) {
+    if (g.col_scale == nullptr || g.a_amax == nullptr || ((uintptr_t)g.col_scale & 15))
+      return set_error(h, RR_EINVAL, "gemm_h2: needs 16-B aligned column scales and the A max-|x| record");
+    if (g.relu == 2 || g.out_bf16 || (g.N & 3) || (g.ldc & 3))
+      return set_error(h, RR_EINVAL, "gemm_h2: fp32 output, ReLU or none, N % 4 == 0");
+  }
   if (g.M == 0) return RR_OK;
   // default stagger: the residual layers only (their 256 KB-per-tile epilogue
   // is the HBM-heavy phase): 256->1024 x23 -5 %, the other residual layers
@@ -1045,11 +1228,17 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
   {
     TimedLaunch tl(h, timer_cls, s);
     const int f = h->tune.s3_cfg;
-    e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s, f, device_cu_count(h), st)
-        : amode == A_CONV ? launch_s3_am<A_CONV>(g, s, f, device_cu_count(h), st)
-                          : launch_s3_am<A_CONV_C4>(g, s, f, device_cu_count(h), st);
+    const int n_cu = device_cu_count(h);
+    if (sp == 2)
+      e = amode == A_DENSE ? launch_h2_am<A_DENSE>(g, s, f, n_cu, st)
+          : amode == A_CONV ? launch_h2_am<A_CONV>(g, s, f, n_cu, st)
+                            : launch_h2_am<A_CONV_C4>(g, s, f, n_cu, st);
+    else
+      e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s, f, n_cu, st)
+          : amode == A_CONV ? launch_s3_am<A_CONV>(g, s, f, n_cu, st)
+                            : launch_s3_am<A_CONV_C4>(g, s, f, n_cu, st);
   }
-  return check_hip(h, e, "gemm_s3 launch");
+  return check_hip(h, e, sp == 2 ? "gemm_h2 launch" : "gemm_s3 launch");
 }
 
 // ---- weight split: x[n] -> planes [3][n] of bf16 (x0, x1, x2) ----
@@ -1068,6 +1257,68 @@ int launch_split3(rr_handle_s* h, const float* x, long long n, uint16_t* planes,
   const long long blocks = std::min<long long>((n + 255) / 256, 4096);
   hipLaunchKernelGGL(split3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, n, planes);
   return check_hip(h, hipGetLastError(), "split3 launch");
+}
+
+// ---- weight split, f16x2: row n of w [rows][k] at scale 2^e_n (h2_exp of
+// the row's max |w|) -> planes [2][rows][kpad] (zero past k), iscale[n] ----
+__global__ __launch_bounds__(256) void split2h_kernel(const float* __restrict__ w, int rows, int k, int kpad,
+                                                      uint16_t* __restrict__ planes, float* __restrict__ iscale) {
+  __shared__ float red[4];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const float* wr = w + (long long)n * k;
+  float am = 0.f;
+  for (int i = tid; i < k; i += 256) am = amax_acc(am, wr[i]);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o));
+  if ((tid & 63) == 0) red[tid >> 6] = am;
+  __syncthreads();
+  am = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  const int e = h2_exp(am);
+  const float sc = __builtin_amdgcn_ldexpf(1.f, e);
+  if (tid == 0) iscale[n] = __builtin_amdgcn_ldexpf(1.f, -e);
+  const long long plane = (long long)rows * kpad;
+  uint16_t* p0 = planes + (long long)n * kpad;
+  for (int i = tid; i < kpad; i += 256) {
+    const float v = i < k ? wr[i] * sc : 0.f;
+    const _Float16 hi = (_Float16)v;
+    const _Float16 lo = (_Float16)(v - (float)hi);
+    p0[i] = __builtin_bit_cast(uint16_t, hi);
+    p0[plane + i] = __builtin_bit_cast(uint16_t, lo);
+  }
+}
+
+int launch_split2h(rr_handle_s* h, const float* w, int rows, int k, int kpad, uint16_t* planes, float* iscale,
+                   hipStream_t s) {
+  if (rows <= 0) return RR_OK;
+  hipLaunchKernelGGL(split2h_kernel, dim3((unsigned)rows), dim3(256), 0, s, w, rows, k, kpad, planes, iscale);
+  return check_hip(h, hipGetLastError(), "split2h launch");
+}
+
+// ---- max |x| of a tensor into its RR_AMAX_SLOTS-word record ----
+__global__ __launch_bounds__(256) void amax_kernel(const float* __restrict__ x, long long n, uint32_t* slots) {
+  float am = 0.f;
+  const long long gs = (long long)gridDim.x * blockDim.x;
+  const long long i0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (((uintptr_t)x & 15) == 0) {
+    const long long n4 = n >> 2;
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+    for (long long i = i0; i < n4; i += gs) {
+      const f32x4 v = x4[i];
+      am = amax_acc(amax_acc(am, v[0]), v[1]);
+      am = amax_acc(amax_acc(am, v[2]), v[3]);
+    }
+    for (long long i = (n4 << 2) + i0; i < n; i += gs) am = amax_acc(am, x[i]);
+  } else {
+    for (long long i = i0; i < n; i += gs) am = amax_acc(am, x[i]);
+  }
+  amax_publish(slots, am, blockIdx.x * 4 + (threadIdx.x >> 6));
+}
+
+int launch_amax(rr_handle_s* h, const float* x, long long n, uint32_t* slots, hipStream_t s) {
+  if (n <= 0) return RR_OK;
+  const long long blocks = std::min<long long>((n / 4 + 255) / 256 + 1, 2048);
+  hipLaunchKernelGGL(amax_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, n, slots);
+  return check_hip(h, hipGetLastError(), "amax launch");
 }
 
 }  // namespace rr

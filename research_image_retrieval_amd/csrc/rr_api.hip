@@ -447,6 +447,67 @@ int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin
   return launch_gemm_s3(h, dense ? A_DENSE : (cin == 4 ? A_CONV_C4 : A_CONV), g, (hipStream_t)stream, kTimeGemm);
 }
 
+int rr_conv2d_h2(rr_handle_t h, const float* x, const unsigned* x_amax, int b, int hgt, int wid, int cin,
+                 const void* w2, const float* w_iscale, const float* bias, int cout, int kh, int kw, int stride,
+                 int pad, const float* residual, int relu, float* y, unsigned* y_amax, void* stream) {
+  RR_ENTRY(h);
+  if (!x || !x_amax || !w2 || !w_iscale || !y || b < 0 || hgt <= 0 || wid <= 0 || cin <= 0 || cout <= 0 ||
+      kh <= 0 || kw <= 0 || stride <= 0 || pad < 0 || relu < 0 || relu > 1)
+    return set_error(h, RR_EINVAL, "rr_conv2d_h2: bad argument");
+  if (cin % 32 && cin != 4) return set_error(h, RR_EINVAL, "rr_conv2d_h2: cin must be a multiple of 32, or 4 (NHWC4 stem)");
+  if (cout % 4) return set_error(h, RR_EINVAL, "rr_conv2d_h2: cout must be a multiple of 4");
+  const int oh = (hgt + 2 * pad - kh) / stride + 1, ow = (wid + 2 * pad - kw) / stride + 1;
+  if (oh <= 0 || ow <= 0) return set_error(h, RR_EINVAL, "rr_conv2d_h2: empty output");
+  const long long M = (long long)b * oh * ow;
+  if (M > 0x7fffffffLL) return set_error(h, RR_EINVAL, "rr_conv2d_h2: too many output pixels");
+  if (((uintptr_t)x & 15) || ((uintptr_t)w2 & 15) || ((uintptr_t)w_iscale & 15))
+    return set_error(h, RR_EINVAL, "rr_conv2d_h2: x/w2/w_iscale must be 16-byte aligned");
+  GemmArgs g;
+  g.A = x;
+  g.M = (int)M;
+  g.K = kh * kw * cin;
+  g.H = hgt;
+  g.W = wid;
+  g.Cin = cin;
+  g.OH = oh;
+  g.OW = ow;
+  g.KH = kh;
+  g.KW = kw;
+  g.stride = stride;
+  g.pad = pad;
+  if (cin == 4) g.K = (g.K + 31) / 32 * 32;  // NHWC4 stem: planes zero-padded to a multiple of 32
+  g.B = reinterpret_cast<const float*>(w2);
+  g.ldb = g.K;
+  g.b_plane = (long long)cout * g.K;
+  g.N = cout;
+  g.C = y;
+  g.ldc = cout;
+  g.bias = bias;
+  g.residual = residual;
+  g.relu = relu;
+  g.col_scale = w_iscale;
+  g.a_amax = x_amax;
+  g.c_amax = y_amax;
+  const bool dense = kh == 1 && kw == 1 && stride == 1 && pad == 0 && cin != 4;
+  if (dense) g.lda = cin;
+  return launch_gemm_s3(h, dense ? A_DENSE : (cin == 4 ? A_CONV_C4 : A_CONV), g, (hipStream_t)stream, kTimeGemm, 2);
+}
+
+int rr_split2_f16(rr_handle_t h, const float* w, int rows, int k, int kpad, void* planes, float* iscale,
+                  void* stream) {
+  RR_ENTRY(h);
+  if (!w || !planes || !iscale || rows < 0 || k <= 0 || kpad < k) return set_error(h, RR_EINVAL, "rr_split2_f16: bad argument");
+  TimedLaunch tl(h, kTimeElem, (hipStream_t)stream);
+  return launch_split2h(h, w, rows, k, kpad, reinterpret_cast<uint16_t*>(planes), iscale, (hipStream_t)stream);
+}
+
+int rr_amax_f32(rr_handle_t h, const float* x, long long n, unsigned* amax, void* stream) {
+  RR_ENTRY(h);
+  if (!x || !amax || n < 0) return set_error(h, RR_EINVAL, "rr_amax_f32: bad argument");
+  TimedLaunch tl(h, kTimeElem, (hipStream_t)stream);
+  return launch_amax(h, x, n, amax, (hipStream_t)stream);
+}
+
 int rr_linear_s3(rr_handle_t h, const float* x, int m, int k, const void* w3, const float* bias, int n,
                  const float* residual, int act, float* y, void* stream) {
   RR_ENTRY(h);

@@ -17,7 +17,7 @@ struct rr_handle_s {
     int gemm_cfg = 0;  // fp32 core: 22, 41 or 88
     int gemm_bk = 0;   // fp32 core k-tile depth: 16 or 32
     int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 sweeps)
-    int s3_cfg = 0;    // split-bf16 core: 1..7 (gemm_s3.hip)
+    int s3_cfg = 0;    // split cores: 1..8 (gemm_s3.hip tile table)
     int s3_stagger = -1;  // split-bf16 core round stagger in ~1 us sleeps (-1: the library's pick)
   } tune;
   int n_cu = 0;  // compute units of the handle's device (device_cu_count)
@@ -190,8 +190,15 @@ struct GemmArgs {
   int k_split = 0;
   long long c_split_stride = 0;
   int sym = 0;  // E_STORE of a symmetric product: skip tiles strictly below the diagonal
-  // split-bf16 GEMM (gemm_s3.hip): B = three bf16 planes, b_plane elements apart
+  // split GEMM (gemm_s3.hip): B = three bf16 planes (SP 3) or two fp16 planes
+  // (SP 2), b_plane elements apart
   long long b_plane = 0;
+  // f16x2 split (SP 2): B row n was split at scale 2^e_n, col_scale[n] = 2^-e_n;
+  // A's max |x| is read from a_amax (RR_AMAX_SLOTS words); the epilogue
+  // publishes max |C| to c_amax when it is set
+  const float* col_scale = nullptr;
+  const uint32_t* a_amax = nullptr;
+  uint32_t* c_amax = nullptr;
   // round stagger: of the first stagger_blocks blocks (one full round of
   // resident blocks), every other XCD-slot one sleeps stagger_sleeps x ~2k
   // cycles before starting, so later rounds run half the CUs out of phase
@@ -201,9 +208,17 @@ struct GemmArgs {
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,
                 int dt = DT_F32);
 
-// fp32-accurate GEMM on bf16 MFMA (gemm_s3.hip): A fp32 (A_DENSE or A_CONV),
-// B = bf16 planes [3][N][ldb] from launch_split3, E_STORE epilogue
-int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls);
+// fp32-accurate GEMM on the 16-bit matrix cores (gemm_s3.hip): A fp32
+// (A_DENSE, A_CONV or A_CONV_C4), E_STORE epilogue; sp = 3: B = bf16 planes
+// [3][N][ldb] from launch_split3; sp = 2: B = fp16 planes [2][N][ldb] +
+// col_scale from launch_split2h, A scaled by its a_amax
+int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls, int sp = 3);
+// fp16 2-way split of the rows of w [rows][k] into planes [2][rows][kpad]
+// (zero-padded) at a per-row power-of-two scale, iscale[row] = its inverse
+int launch_split2h(rr_handle_s* h, const float* w, int rows, int k, int kpad, uint16_t* planes, float* iscale,
+                   hipStream_t s);
+// max |x| over x[n] into the RR_AMAX_SLOTS words at slots (atomic max)
+int launch_amax(rr_handle_s* h, const float* x, long long n, uint32_t* slots, hipStream_t s);
 
 // bf16 256x256 8-phase pipeline (gemm_8p.hip): dense A/B, K % 128 == 0
 bool gemm_8p_eligible(const GemmArgs& g);

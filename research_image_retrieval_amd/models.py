@@ -34,7 +34,7 @@ class GeMModel(_Extractor):
     in_channels = 4
 
     def __init__(self, backbone="resnet50", pretrained=False, num_classes=1000, feature_dim=2048, gem_p=3.0,
-                 state_dict=None, seed=0, device="cuda", conv_math="s3", stride_on="3x3"):
+                 state_dict=None, seed=0, device="cuda", conv_math="h2", stride_on="3x3"):
         if pretrained:
             raise ValueError("pretrained weights need a download; pass a local state_dict instead "
                              "(models/gem_pooling.py:35 defaults to pretrained=True)")

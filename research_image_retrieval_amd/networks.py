@@ -22,10 +22,13 @@ class ResNet:
 
     forward(x_nhwc [B,H,W,3]) -> [B,H/32,W/32,2048] NHWC.
 
-    conv_math: "s3" (default) runs every conv with Cin % 32 == 0 on the
-    split-bf16 core (fp32-accurate, weights split once here); "f32" keeps all
-    convs on the exact-fp32 MFMA core.  The stem runs on the split-bf16 core
-    too (NHWC4 taps, K padded to 224) unless conv_math == "f32".
+    conv_math: "h2" (default) runs every conv, the stem included (NHWC4
+    taps, K padded to 224), on the f16x2 split core (fp32-accurate: error vs
+    float64 at or below the exact-fp32 core's, tests/test_gpu_h2.py; three
+    fp16 MFMAs per product; weights split once here, each conv publishes max
+    |y| for the next one's split scale); "s3" runs them on the split-bf16 core
+    (six bf16 MFMAs per product); "f32" keeps all convs on the exact-fp32 MFMA
+    core.
 
     stride_on: "3x3" (default) = torchvision v1.5 bottlenecks; "1x1" = the
     reference's own torchvision-free R101, ResNet_DOLG
@@ -36,9 +39,9 @@ class ResNet:
     outputdim_block5 = 2048
     outputdim_block4 = 1024
 
-    def __init__(self, name="resnet101", state_dict=None, seed=0, device="cuda", conv_math="s3", stride_on="3x3"):
-        if conv_math not in ("s3", "f32"):
-            raise ValueError("conv_math must be 's3' or 'f32'")
+    def __init__(self, name="resnet101", state_dict=None, seed=0, device="cuda", conv_math="h2", stride_on="3x3"):
+        if conv_math not in ("h2", "s3", "f32"):
+            raise ValueError("conv_math must be 'h2', 's3' or 'f32'")
         W.block_strides(1, stride_on)  # validates
         self.stride_on = stride_on
         if name not in W.RESNET_LAYERS:
@@ -55,9 +58,12 @@ class ResNet:
         self.conv_math = conv_math
         self.convs_s3 = {}
         self.stem_s3 = None
+        self.convs_h2 = {}
         if conv_math == "s3":
             self.convs_s3 = {k: ops.split3_bf16(w) for k, (w, _) in self.convs.items() if w.shape[-1] % 32 == 0}
             self.stem_s3 = ops.split3_stem(self.convs["conv1"][0])
+        elif conv_math == "h2":
+            self.convs_h2 = {k: ops.H2Conv(w) for k, (w, _) in self.convs.items()}
 
     def _conv(self, x, name, stride, pad, relu, residual=None):
         w, b = self.convs[name]
@@ -68,12 +74,39 @@ class ResNet:
             return ops.conv2d_s3(x, w3, b, stride, pad, residual, relu)
         return ops.conv2d(x, w, b, stride, pad, residual, relu)
 
+    def _forward_h2(self, x, return_x3):
+        """The trunk on the f16x2 core: every conv reads its input's max-|x|
+        record and writes its output's (one zeroed [2 + 3 blocks, 64] tensor per
+        forward); the max-pool output reuses the stem's record (every stem
+        output lies in some 3x3/2 window, so the max is the same)."""
+        cv, h2 = self.convs, self.convs_h2
+        rec = ops.amax_records(2 + 3 * sum(self.layers), x.device)
+        ops.amax_f32(x, rec[0])
+        x = ops.conv2d_h2(x, rec[0], h2["conv1"], cv["conv1"][1], 2, 3, None, True, rec[1])
+        x = ops.maxpool2d(x, 3, 2, 1)
+        xa, r, x3 = rec[1], 2, None
+        for li, nb in enumerate(self.layers):
+            for bi in range(nb):
+                p = f"layer{li + 1}.{bi}"
+                s1, s2 = W.block_strides(2 if (bi == 0 and li > 0) else 1, self.stride_on)
+                d = f"{p}.downsample.0"
+                idn = ops.conv2d_h2(x, xa, h2[d], cv[d][1], s1 * s2, 0, None, False) if bi == 0 else x
+                y = ops.conv2d_h2(x, xa, h2[f"{p}.conv1"], cv[f"{p}.conv1"][1], s1, 0, None, True, rec[r])
+                y = ops.conv2d_h2(y, rec[r], h2[f"{p}.conv2"], cv[f"{p}.conv2"][1], s2, 1, None, True, rec[r + 1])
+                x = ops.conv2d_h2(y, rec[r + 1], h2[f"{p}.conv3"], cv[f"{p}.conv3"][1], 1, 0, idn, True, rec[r + 2])
+                xa, r = rec[r + 2], r + 3
+            if li == 2:
+                x3 = x
+        return (x3, x) if return_x3 else x
+
     def forward(self, x, return_x3=False):
         """x: NHWC fp32 with 3 channels or 4 (zero 4th channel, preferred).
         return_x3: also return layer3's output, as ResNet_DOLG.forward's
         (x3, x4) (networks/backbone.py:236-242)."""
         if x.shape[-1] == 3:
             x = torch.nn.functional.pad(x, (0, 1))
+        if self.conv_math == "h2":
+            return self._forward_h2(x.contiguous(), return_x3)
         x = self._conv(x, "conv1", 2, 3, True)
         x = ops.maxpool2d(x, 3, 2, 1)
         x3 = None
@@ -147,7 +180,7 @@ class GeM(_Extractor):
     in_channels = 4
 
     def __init__(self, outputdim=2048, backbone="resnet101", state_dict=None, whiten=None, seed=0, device="cuda",
-                 conv_math="s3"):
+                 conv_math="h2"):
         if outputdim != 2048:
             raise ValueError("networks.GeM requires outputdim == 2048 (whiten is Conv2d(outputdim, 2048), "
                              "networks/RetrievalNet.py:332)")

@@ -184,6 +184,96 @@ def linear_s3(x, w3, bias=None, residual=None, act=0):
     return y
 
 
+AMAX_SLOTS = 64  # RR_AMAX_SLOTS: words of one tensor's max-|x| record
+
+
+def amax_records(n, device):
+    """n zeroed max-|x| records [n, RR_AMAX_SLOTS] (int32 words holding float
+    bits) for rr_conv2d_h2's x_amax / y_amax."""
+    return torch.zeros((n, AMAX_SLOTS), dtype=torch.int32, device=device)
+
+
+def amax_f32(x, record):
+    """Fold max |x| (finite values) into a zeroed record (rr_amax_f32)."""
+    x = _f32(x.contiguous(), "amax_f32")
+    if record.dtype != torch.int32 or record.numel() != AMAX_SLOTS or not record.is_contiguous():
+        raise ValueError("amax_f32: record must be contiguous int32 [RR_AMAX_SLOTS]")
+    dev = _dev(x)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_amax_f32(hd, _ptr(x), x.numel(), _ptr(record), _stream(dev)), hd, "rr_amax_f32")
+    return record
+
+
+def amax_value(record):
+    """The max a record holds, as a Python float (host read: tests, tools)."""
+    return float(record.view(torch.float32).max().item())
+
+
+def split2_f16(w, kpad=None):
+    """fp16 x2 split of the rows of w ([N, K] or [Cout, KH, KW, Cin]) at a
+    per-row power-of-two scale (rr_split2_f16): returns (planes int16 [2, N,
+    kpad] of fp16 bit patterns, zero past K; iscale fp32 [N] = 2^-e_n)."""
+    w = _f32(w.contiguous(), "split2_f16")
+    dev = _dev(w)
+    rows = w.shape[0]
+    k = w.numel() // max(rows, 1)
+    kpad = k if kpad is None else int(kpad)
+    if kpad < k:
+        raise ValueError("split2_f16: kpad < K")
+    planes = torch.empty((2, rows, kpad), dtype=torch.int16, device=w.device)
+    iscale = torch.empty((rows,), dtype=torch.float32, device=w.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_split2_f16(hd, _ptr(w), rows, k, kpad, _ptr(planes), _ptr(iscale), _stream(dev)), hd,
+               "rr_split2_f16")
+    return planes, iscale
+
+
+class H2Conv:
+    """Weights of one conv on the f16x2 split core: planes [2, Cout, Kp],
+    inverse row scales [Cout], filter (KH, KW, Cin).  Cin == 4 is the NHWC4
+    stem (K = KH*KW*4 zero-padded to a multiple of 32)."""
+
+    def __init__(self, w):
+        w = _f32(w.contiguous(), "H2Conv")
+        cout, kh, kw, cin = w.shape
+        if cin % 32 and cin != 4:
+            raise ValueError("H2Conv: Cin must be a multiple of 32, or 4 (NHWC4 stem)")
+        k = kh * kw * cin
+        self.kpad = (k + 31) // 32 * 32 if cin == 4 else k
+        self.planes, self.iscale = split2_f16(w.reshape(cout, k), self.kpad)
+        self.cout, self.kh, self.kw, self.cin = cout, kh, kw, cin
+
+
+def conv2d_h2(x, x_amax, wc, bias, stride=1, pad=0, residual=None, relu=False, y_amax=None):
+    """conv2d on the f16x2 split core (rr_conv2d_h2): fp32-accurate, wc an
+    H2Conv, x_amax the max-|x| record of x; y_amax (optional, zeroed) gets
+    max |y| for the next conv."""
+    _f32(x, "conv2d_h2 x")
+    if not isinstance(wc, H2Conv):
+        raise TypeError("conv2d_h2: wc must be an ops.H2Conv")
+    dev = _dev(x)
+    b, h, wd, cin = x.shape
+    if cin != wc.cin:
+        raise ValueError(f"conv2d_h2: Cin mismatch {cin} vs {wc.cin}")
+    for r, nm in ((x_amax, "x_amax"), (y_amax, "y_amax")):
+        if r is not None and (r.dtype != torch.int32 or r.numel() != AMAX_SLOTS or not r.is_contiguous()):
+            raise ValueError(f"conv2d_h2: {nm} must be a contiguous int32 [RR_AMAX_SLOTS] record")
+    oh = (h + 2 * pad - wc.kh) // stride + 1
+    ow = (wd + 2 * pad - wc.kw) // stride + 1
+    y = torch.empty((b, oh, ow, wc.cout), dtype=torch.float32, device=x.device)
+    if residual is not None:
+        _f32(residual, "conv2d_h2 residual")
+        if tuple(residual.shape) != tuple(y.shape):
+            raise ValueError("conv2d_h2: residual shape mismatch")
+    if bias is not None:
+        _f32(bias, "conv2d_h2 bias")
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_conv2d_h2(hd, _ptr(x), _ptr(x_amax), b, h, wd, cin, _ptr(wc.planes), _ptr(wc.iscale),
+                                       _ptr(bias), wc.cout, wc.kh, wc.kw, stride, pad, _ptr(residual), int(relu),
+                                       _ptr(y), _ptr(y_amax), _stream(dev)), hd, "rr_conv2d_h2")
+    return y
+
+
 def resize_bilinear(x_nhwc, out_h, out_w, scale_factor=None):
     """NHWC bilinear resize, align_corners=False.  With ``scale_factor`` the
     source index uses 1/scale_factor, as F.interpolate(scale_factor=s) does."""

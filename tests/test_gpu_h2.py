@@ -1,0 +1,239 @@
+"""The f16x2 split core (gemm_s3.hip, SP 2; rr_conv2d_h2): the power-of-two
+scaled 2-way fp16 split, and fp32-grade accuracy of the convolutions it runs,
+measured against float64 next to the exact-fp32 MFMA core and the split-bf16
+core on the same inputs (the bar tests/test_gpu_s3.py set for the s3 core:
+error relative to sum |a||b| per output, max and mean, at most the exact-fp32
+core's), plus the max-|y| records the convs hand to each other.
+
+The reference computes these convolutions in fp32 on the CPU
+(networks/backbone.py:60-109, :305-346)."""
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from oracle import embed_ref
+from research_image_retrieval_amd import ops
+from research_image_retrieval_amd import weights as W
+from research_image_retrieval_amd.networks import GeM
+
+pytestmark = pytest.mark.gpu
+
+DESC_TOL = 1e-6  # as tests/test_gpu_embed.py
+
+
+def _planes_to_f64(p):
+    return p.view(torch.float16).double()
+
+
+def _rel_err(got, ref64, scale64):
+    e = (got.double() - ref64).abs() / scale64.clamp_min(1e-300)
+    return e.max().item(), e.mean().item()
+
+
+def test_split2_scaled_pieces(cuda):
+    """Each row's scale is a power of two putting its max |w| in [2^14, 2^15);
+    w 2^e = p0 + p1 + r with |r| <= 2^-22 |w 2^e| (ulp-level for tiny values);
+    padding columns are zero."""
+    rs = np.random.RandomState(0)
+    rows, k = 37, 300
+    w = (rs.standard_normal((rows, k)) * np.exp2(rs.randint(-30, 30, (rows, 1)))).astype(np.float32)
+    w[3] = 0.0
+    w[5, :7] = [1e-30, -2e-31, 3.4e37, 0.0, -0.0, 1e-3, 7.0]
+    planes, isc = ops.split2_f16(torch.from_numpy(w).to(cuda), kpad=320)
+    planes, isc = planes.cpu(), isc.cpu().double()
+    assert planes.shape == (2, rows, 320) and bool((planes[:, :, k:] == 0).all())
+    e = -torch.log2(isc)
+    assert torch.equal(e, e.round()), "scales must be powers of two"
+    amax = torch.from_numpy(np.abs(w)).double().max(1).values
+    live = amax > 0
+    sc_max = amax[live] / isc[live]
+    assert bool((sc_max >= 2.0 ** 14).all()) and bool((sc_max < 2.0 ** 15).all())
+    assert float(isc[3]) == 1.0  # a zero row keeps scale 1
+    p = _planes_to_f64(planes[:, :, :k])
+    ws = torch.from_numpy(w).double() / isc[:, None]
+    r = (p[0] + p[1] - ws).abs()
+    # fp16 subnormal quantum 2^-24 bounds the remainder of tiny scaled values
+    assert bool((r <= torch.maximum(ws.abs() * 2.0 ** -22, torch.full_like(r, 2.0 ** -25))).all())
+
+
+def test_amax_record(cuda):
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(1000003, generator=g)
+    x[12345] = -77.5
+    x[999] = float("inf")  # non-finite values are left out
+    x[1001] = float("nan")
+    rec = ops.amax_records(1, cuda)[0]
+    ops.amax_f32(x.to(cuda), rec)
+    assert ops.amax_value(rec) == 77.5
+    # unaligned start
+    rec2 = ops.amax_records(1, cuda)[0]
+    ops.amax_f32(x.to(cuda)[1:], rec2)
+    assert ops.amax_value(rec2) == 77.5
+
+
+CONV_SHAPES = [  # b, h, w, cin, cout, k, stride, pad, residual
+    (2, 14, 14, 64, 128, 3, 1, 1, False),
+    (3, 15, 13, 32, 96, 3, 2, 1, False),
+    (2, 28, 28, 64, 256, 1, 2, 0, False),
+    (2, 9, 11, 256, 64, 1, 1, 0, True),
+    (4, 7, 7, 512, 2048, 1, 1, 0, True),
+    (2, 14, 14, 256, 256, 3, 1, 1, True),
+    (3, 21, 19, 128, 512, 1, 1, 0, True),
+]
+
+
+def _conv_case(cuda, b, h, w, cin, cout, k, s, p, res, xscale=1.0, seed=0):
+    g = torch.Generator().manual_seed(b * h + cin + cout + seed)
+    x = torch.relu(torch.randn(b, h, w, cin, generator=g)) * xscale
+    wt = torch.randn(cout, k, k, cin, generator=g) * (2.0 / (k * k * cin)) ** 0.5
+    bias = torch.randn(cout, generator=g) * 0.1 * xscale
+    oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    r = torch.randn(b, oh, ow, cout, generator=g) * xscale if res else None
+    xn, wn = x.permute(0, 3, 1, 2).double(), wt.permute(0, 3, 1, 2).double()
+    conv = F.conv2d(xn, wn, None, s, p).permute(0, 2, 3, 1)
+    scale = F.conv2d(xn.abs(), wn.abs(), None, s, p).permute(0, 2, 3, 1)
+    ref = torch.relu(conv + bias.double() + (r.double() if res else 0.0))
+    return x, wt, bias, r, ref, scale
+
+
+def _run_h2(cuda, x, wt, bias, r, s, p, y_rec=True):
+    xd = x.to(cuda)
+    rec = ops.amax_records(2, cuda)
+    ops.amax_f32(xd, rec[0])
+    y = ops.conv2d_h2(xd, rec[0], ops.H2Conv(wt.to(cuda)), bias.to(cuda), s, p, None if r is None else r.to(cuda),
+                      True, rec[1] if y_rec else None)
+    return y, rec
+
+
+@pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res", CONV_SHAPES)
+def test_conv2d_h2_vs_float64(cuda, b, h, w, cin, cout, k, s, p, res):
+    x, wt, bias, r, ref, scale = _conv_case(cuda, b, h, w, cin, cout, k, s, p, res)
+    y_h2, rec = _run_h2(cuda, x, wt, bias, r, s, p)
+    xd, wd = x.to(cuda), wt.to(cuda)
+    rd = r.to(cuda) if res else None
+    y_f32 = ops.conv2d(xd, wd, bias.to(cuda), s, p, rd, True).cpu()
+    y_s3 = ops.conv2d_s3(xd, ops.split3_bf16(wd), bias.to(cuda), s, p, rd, True).cpu()
+    y_h2 = y_h2.cpu()
+    live = ref > 0
+    eh2 = _rel_err(y_h2[live], ref[live], scale[live])
+    ef32 = _rel_err(y_f32[live], ref[live], scale[live])
+    es3 = _rel_err(y_s3[live], ref[live], scale[live])
+    print(f"conv {b}x{h}x{w}x{cin}->{cout} k{k}s{s}: h2 max {eh2[0]:.3g} mean {eh2[1]:.3g} | "
+          f"s3 max {es3[0]:.3g} mean {es3[1]:.3g} | f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
+    assert eh2[0] <= max(ef32[0], 1e-7) and eh2[1] <= ef32[1] * 1.05 + 1e-9
+    # the output's max-|y| record holds exactly max |y|
+    assert ops.amax_value(rec[1]) == float(y_h2.abs().max())
+
+
+@pytest.mark.parametrize("xscale", [2.0 ** -60, 2.0 ** 50, 3.0e-7])
+def test_conv2d_h2_scale_invariant(cuda, xscale):
+    """The split scales follow the data: activations and residuals at 2^-60 or
+    2^50 (far outside fp16's range) keep the same relative accuracy, and a
+    power-of-two input scale scales the output exactly."""
+    shape = (2, 14, 14, 256, 256, 3, 1, 1, True)
+    x, wt, bias, r, ref, scale = _conv_case(cuda, *shape, xscale=xscale, seed=11)
+    y, _ = _run_h2(cuda, x, wt, bias, r, 1, 1, y_rec=False)
+    live = ref > 0
+    e = _rel_err(y.cpu()[live], ref[live], scale[live])
+    print(f"xscale {xscale:g}: h2 max {e[0]:.3g} mean {e[1]:.3g}")
+    assert e[0] < 4e-7
+    if xscale in (2.0 ** -60, 2.0 ** 50):
+        x1, _, b1, r1, _, _ = _conv_case(cuda, *shape, xscale=1.0, seed=11)
+        y1, _ = _run_h2(cuda, x1, wt, b1, r1, 1, 1, y_rec=False)
+        assert torch.equal(y.cpu(), y1.cpu() * xscale)
+
+
+@pytest.mark.parametrize("b,h,w", [(2, 224, 224), (3, 37, 53)])
+def test_stem_h2_vs_float64(cuda, b, h, w):
+    """The NHWC4 stem (7x7/2, pad 3, K padded to 224) on the f16x2 core."""
+    g = torch.Generator().manual_seed(b * h + w)
+    x = torch.randn(b, h, w, 3, generator=g) * 1.5
+    x4 = F.pad(x, (0, 1)).contiguous()
+    wt = torch.randn(64, 7, 7, 3, generator=g) * (2.0 / 147) ** 0.5
+    w4 = F.pad(wt, (0, 1)).contiguous()
+    bias = torch.randn(64, generator=g) * 0.1
+    xn, wn = x.permute(0, 3, 1, 2).double(), wt.permute(0, 3, 1, 2).double()
+    ref = torch.relu(F.conv2d(xn, wn, None, 2, 3).permute(0, 2, 3, 1) + bias.double())
+    scale = F.conv2d(xn.abs(), wn.abs(), None, 2, 3).permute(0, 2, 3, 1)
+    y_h2, _ = _run_h2(cuda, x4, w4, bias, None, 2, 3)
+    y_h2 = y_h2.cpu()
+    y_f32 = ops.conv2d(x4.to(cuda), w4.to(cuda), bias.to(cuda), 2, 3, None, True).cpu()
+    assert y_h2.shape == ref.shape
+    live = ref > 0
+    eh2 = _rel_err(y_h2[live], ref[live], scale[live])
+    ef32 = _rel_err(y_f32[live], ref[live], scale[live])
+    print(f"stem {b}x{h}x{w}: h2 max {eh2[0]:.3g} mean {eh2[1]:.3g} | f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
+    assert eh2[0] <= max(ef32[0], 1e-7) and eh2[1] <= ef32[1] * 1.05 + 1e-9
+
+
+TILE_SHAPES = [  # shapes that reach each f16x2 config's edges: ragged M, N = 64 / 96 / 128 / 256k
+    (2, 9, 11, 256, 64, 1, 1, 0, True),
+    (3, 15, 13, 32, 96, 3, 2, 1, False),
+    (2, 14, 14, 64, 128, 3, 1, 1, False),
+    (3, 21, 19, 128, 512, 1, 1, 0, True),
+    (2, 14, 14, 256, 256, 3, 1, 1, True),
+]
+
+
+@pytest.mark.parametrize("cfg", [3, 4, 7, 8])
+@pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res", TILE_SHAPES)
+def test_conv2d_h2_tile_configs(cuda, cfg, b, h, w, cin, cout, k, s, p, res):
+    """Every f16x2 tile config forced on every shape: fp32-grade vs float64
+    (configs that do not serve a shape fall back to the pick)."""
+    x, wt, bias, r, ref, scale = _conv_case(cuda, b, h, w, cin, cout, k, s, p, res, seed=cfg)
+    with ops.tuning(0, s3_cfg=cfg):
+        y, rec = _run_h2(cuda, x, wt, bias, r, s, p)
+    y = y.cpu()
+    live = ref > 0
+    e = _rel_err(y[live], ref[live], scale[live])
+    assert e[0] < 4e-7, (cfg, e)
+    assert ops.amax_value(rec[1]) == float(y.abs().max())
+
+
+def test_h2_persistent_tile_bit_identical(cuda):
+    """Config 8 (persistent k-stream) and config 4 keep the same
+    per-accumulator k order and epilogue arithmetic: identical bits."""
+    x, wt, bias, r, _, _ = _conv_case(cuda, 3, 29, 31, 256, 1024, 1, 1, 0, True, seed=5)
+    outs = {}
+    for cfg in (4, 8):
+        with ops.tuning(0, s3_cfg=cfg):
+            outs[cfg] = _run_h2(cuda, x, wt, bias, r, 1, 0)[0].cpu()
+    assert torch.equal(outs[4], outs[8])
+
+
+def test_conv2d_h2_nonfinite_inputs(cuda):
+    """An inf / NaN activation turns the outputs that read it into NaN / inf
+    as fp32 does, and leaves every other output fp32-accurate (non-finite
+    values stay out of the max-|x| record)."""
+    x, wt, bias, r, ref, scale = _conv_case(cuda, 2, 14, 14, 64, 128, 3, 1, 1, False, seed=3)
+    x[0, 5, 5, 7] = float("inf")
+    x[1, 9, 2, 3] = float("nan")
+    y, _ = _run_h2(cuda, x, wt, bias, None, 1, 1)
+    y = y.cpu()
+    touched = torch.zeros(2, 14, 14, dtype=torch.bool)
+    touched[0, 4:7, 4:7] = True
+    touched[1, 8:11, 1:4] = True
+    assert bool((~torch.isfinite(y[touched]) | (y[touched] == 0)).any())
+    ok = ~touched[..., None].expand_as(y) & (ref > 0)
+    e = _rel_err(y[ok], ref[ok], scale[ok])
+    assert e[0] < 4e-7
+
+
+def test_resnet_h2_descriptors_vs_float64(cuda):
+    """The whole R50-GeM extractor: f16x2 trunk vs exact-fp32 trunk, both
+    against the oracle evaluated in float64."""
+    rs = np.random.RandomState(3)
+    img = torch.from_numpy(rs.randint(0, 256, size=(3, 64, 72, 3), dtype=np.uint8))
+    x = embed_ref.normalize_u8(img)
+    got = {}
+    for math in ("h2", "f32"):
+        net = GeM(2048, backbone="resnet50", seed=4, device=cuda, conv_math=math)
+        got[math] = net.forward_test(x.to(cuda)).cpu().double()
+    sd = {k: v.double() for k, v in W.synthetic_resnet_state_dict("resnet50", 4).items()}
+    ww, wb = W.synthetic_linear(2048, 2048, 5)
+    ref = embed_ref.gem_net_forward_test(x.double(), sd, W.RESNET_LAYERS["resnet50"], ww.double(), wb.double())
+    e_h2 = (got["h2"] - ref).abs().max().item()
+    e_f32 = (got["f32"] - ref).abs().max().item()
+    print(f"R50-GeM descriptors vs float64: h2 {e_h2:.3g}  f32 {e_f32:.3g}")
+    assert e_h2 < DESC_TOL and e_h2 <= 2.0 * e_f32

@@ -33,7 +33,7 @@ def fixture():
     return np.load(os.path.join(GOLD, "resnet_dolg.npz"))
 
 
-@pytest.mark.parametrize("conv_math", ["s3", "f32"])
+@pytest.mark.parametrize("conv_math", ["h2", "s3", "f32"])
 @pytest.mark.parametrize("tag", ["b2_224", "b1_odd"])
 def test_trunk_vs_reference_resnet_dolg(cuda, fixture, conv_math, tag):
     sd = W.to_dolg_keys(W.synthetic_resnet_state_dict("resnet101", int(fixture["weight_seed"])))
