@@ -31,7 +31,7 @@ sys.path.insert(0, ROOT)
 
 from research_image_retrieval_amd import _lib, ops  # noqa: E402
 from research_image_retrieval_amd import weights as W  # noqa: E402
-from research_image_retrieval_amd.distributed import ShardedGallery, shard_bounds  # noqa: E402
+from research_image_retrieval_amd.distributed import ShardedGallery, shard_bounds, sharded_step  # noqa: E402
 from research_image_retrieval_amd.networks import GeM, ConvDimReduction, GeMPCAw, VisionTransformer  # noqa: E402
 from research_image_retrieval_amd.extract import _rescale  # noqa: E402
 
@@ -176,7 +176,6 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
 
 
 # ---- config C2: ResNet50-GeM 512-d at imsize 1024 over a ROxford5k-shaped set ----
-C2_GALLERY, C2_QUERIES = 4993, 70  # revisitop ROxford5k: 4,993 images, 70 queries
 # (H, W) after thumbnail(1024) and the share of the gallery at that size
 C2_SIZES = ((768, 1024, 0.70), (1024, 768, 0.22), (683, 1024, 0.06), (1024, 683, 0.02))
 C2_BATCH = 128  # same-size gallery images per extractor call (the reference runs batch 1; 16 -> 128: +15 %)
@@ -192,12 +191,13 @@ def c2_layout(n_gallery, n_query, seed=1234):
     return [(h, w, c) for (h, w, _), c in zip(C2_SIZES, counts)], qs
 
 
-def cpu_baseline_c2(n_gallery, n_query, d=512, seed=0):
+def cpu_baseline_c2(sets, d=512, seed=0):
     """The reference CPU path for C2, timed on a bounded sample: batch-1
-    extraction of 2 gallery images at 768x1024 (utils/helpfunc.py:18-48 through
-    the oracle's R50-GeM-512 restatement), and the full ranking of all queries
-    (torch.mm + np.argsort, iris_evaluate.py:383-386) against the whole
-    gallery; the job time = all images x per-image embed + the ranking."""
+    extraction of 50 gallery images at 768x1024 (utils/helpfunc.py:18-48
+    through the oracle's R50-GeM-512 restatement), and the full ranking of
+    every set's queries against its whole gallery (torch.mm + np.argsort,
+    iris_evaluate.py:383-386); the job time = all images x per-image embed +
+    the rankings.  sets: [(n_gallery, n_query), ...]."""
     from oracle import embed_ref
     affinity, granted, threads = host_threads()
     default_threads = torch.get_num_threads()
@@ -215,18 +215,21 @@ def cpu_baseline_c2(n_gallery, n_query, d=512, seed=0):
                                            pw, pb)
         t_embed = (time.perf_counter() - t0) / n_img
         gen = torch.Generator().manual_seed(7)
-        g = torch.nn.functional.normalize(torch.randn(n_gallery, d, generator=gen), dim=1)
-        q = torch.nn.functional.normalize(torch.randn(n_query, d, generator=gen), dim=1)
-        t0 = time.perf_counter()
-        np.argsort(-torch.mm(q, g.t()).numpy(), axis=1)
-        t_rank = time.perf_counter() - t0
+        t_rank = 0.0
+        for n_gallery, n_query in sets:
+            g = torch.nn.functional.normalize(torch.randn(n_gallery, d, generator=gen), dim=1)
+            q = torch.nn.functional.normalize(torch.randn(n_query, d, generator=gen), dim=1)
+            t0 = time.perf_counter()
+            np.argsort(-torch.mm(q, g.t()).numpy(), axis=1)
+            t_rank += time.perf_counter() - t0
     torch.set_num_threads(default_threads)
-    total = (n_gallery + n_query) * t_embed + t_rank
-    return {"value": (n_gallery + n_query) / total, "unit": "images/s", "cores": threads, "kind": "port",
+    n_all = sum(g_ + q_ for g_, q_ in sets)
+    total = n_all * t_embed + t_rank
+    return {"value": n_all / total, "unit": "images/s", "cores": threads, "kind": "port",
             "affinity_cpus": affinity, "granted_cpus": granted,
             "sample": f"{n_img} images embedded at batch 1 (768x1024, resnet50-GeM 512-d, fp32) and the full ranking of "
-                      f"{n_query} queries x {n_gallery} rows (torch.mm + np.argsort); job time = "
-                      f"{n_gallery + n_query} x per-image embed + ranking",
+                      + " + ".join(f"{q_} queries x {g_} rows" for g_, q_ in sets)
+                      + f" (torch.mm + np.argsort); job time = {n_all} x per-image embed + rankings",
             "embed_s_per_image": t_embed, "rank_s": t_rank, "torch_default_threads": default_threads}
 
 
@@ -236,43 +239,69 @@ def cpu_baseline_c2(n_gallery, n_query, d=512, seed=0):
 DIST_ON = False
 
 
+C2_SETS = {"roxford5k": (4993, 70), "rparis6k": (6322, 70)}  # revisitop sizes (dataset/configdataset.py:27-57)
+
+
 def run_c2(a, world, rank, dev):
-    """C2: ResNet50-GeM 512-d fp32 (Table-1 GeMModel) over a ROxford5k-shaped
-    set at imsize 1024 -- 4,993 gallery images + 70 query crops, every image
-    embedded (gallery images in same-size batches, queries one by one at their
-    own crop size), full ranks of the queries against the gallery and the
-    revisited mAP (utils/evaluate.py:153-194) on the host.  One step = the
-    whole set; N ranks split the images (strong scaling), descriptors are
-    all-gathered over RCCL and rank 0 ranks and scores."""
+    """C2: ResNet50-GeM 512-d fp32 (Table-1 GeMModel) over full ROxford5k- and
+    RParis6k-shaped sets at imsize 1024 -- 4,993 + 6,322 gallery images and
+    70 + 70 query crops, every image embedded (gallery images in same-size
+    batches, queries one by one at their own crop size), full ranks of each
+    dataset's queries against its gallery and the revisited mAP
+    (utils/evaluate.py:153-194) on the host.  One step = both sets (or the one
+    --c2-dataset names); N ranks split the images (strong scaling),
+    descriptors are all-gathered over RCCL and rank 0 ranks and scores.
+
+    Conv-class time for the roofline: the gallery phases run on one stream,
+    so their per-launch HIP events do not overlap and are summed; the query
+    phases run batch-1 crops on concurrent streams, whose event spans overlap,
+    so each query phase counts with its whole wall time on the main stream
+    (an upper bound on its conv time).  The sum never exceeds the step."""
     from research_image_retrieval_amd.distributed import _all_gather_var
     from research_image_retrieval_amd.evaluate import compute_map_and_print
     from research_image_retrieval_amd.models import get_model
     sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
-    n_g, n_q = a.c2_gallery, a.c2_queries
-    groups, qsizes = c2_layout(n_g, n_q)
+    import inputs as I  # noqa: E402  (synthetic revisitop-shaped ground truth)
+    names = list(C2_SETS) if a.c2_dataset == "both" else [a.c2_dataset]
     net = get_model("gem_r50", 1000, feature_dim=512, seed=0, device=dev, conv_math=a.conv_math)
-    # this rank's images (contiguous share of the gallery order, and of the queries)
-    glo, ghi = shard_bounds(n_g, world, rank)
-    qlo, qhi = shard_bounds(n_q, world, rank)
     gen = torch.Generator(device=dev)
     gen.manual_seed(1234)
-    batches, start = [], 0
-    for h, w, c in groups:
-        lo, hi = max(start, glo), min(start + c, ghi)
-        for b0 in range(lo, hi, a.c2_batch):
-            nb = min(a.c2_batch, hi - b0)
-            batches.append(torch.randint(0, 256, (nb, h, w, 3), dtype=torch.uint8, device=dev, generator=gen))
-        start += c
-    queries = [torch.randint(0, 256, (1, h, w, 3), dtype=torch.uint8, device=dev, generator=gen)
-               for (h, w) in qsizes[qlo:qhi]]
-    import inputs as I  # noqa: E402  (synthetic ROxford5k-shaped ground truth)
-    gnd, _ = I.map_inputs(31, nq=n_q, n=n_g)
+    sets = []
+    for si, name in enumerate(names):
+        n_g, n_q = C2_SETS[name]
+        if a.c2_gallery:
+            n_g = a.c2_gallery
+        if a.c2_queries:
+            n_q = a.c2_queries
+        groups, qsizes = c2_layout(n_g, n_q, seed=1234 + si)
+        # this rank's images (contiguous share of the gallery order, and of the queries)
+        glo, ghi = shard_bounds(n_g, world, rank)
+        qlo, qhi = shard_bounds(n_q, world, rank)
+        batches, start = [], 0
+        for h, w, c in groups:
+            lo, hi = max(start, glo), min(start + c, ghi)
+            for b0 in range(lo, hi, a.c2_batch):
+                nb = min(a.c2_batch, hi - b0)
+                batches.append(torch.randint(0, 256, (nb, h, w, 3), dtype=torch.uint8, device=dev, generator=gen))
+            start += c
+        queries = [torch.randint(0, 256, (1, h, w, 3), dtype=torch.uint8, device=dev, generator=gen)
+                   for (h, w) in qsizes[qlo:qhi]]
+        gnd, _ = I.map_inputs(31 + si, nq=n_q, n=n_g)
+        img_flops = sum(c_ * (sum(W.resnet_conv_flops("resnet50", h, w).values()) + 2 * 2048 * 512)
+                        for (h, w, c_) in [(h, w, max(0, min(s0 + c, ghi) - max(s0, glo)))
+                                           for (h, w, c), s0 in zip(groups, np.cumsum([0] + [g[2] for g in groups]))])
+        img_flops += sum(sum(W.resnet_conv_flops("resnet50", h, w).values()) + 2 * 2048 * 512
+                         for (h, w) in qsizes[qlo:qhi])
+        sets.append({"name": name, "n_g": n_g, "n_q": n_q, "batches": batches, "queries": queries, "gnd": gnd,
+                     "flops": img_flops})
     torch.cuda.synchronize()
     # batch-1 query crops (all sizes differ): small grids, so C2_QSTREAMS of them
     # run concurrently on side streams
     qstreams = [torch.cuda.Stream(dev) for _ in range(a.c2_qstreams)] if a.c2_qstreams > 1 else []
+    timer = ops.KernelTimer(dev.index)
+    acct = {"conv_ms": 0.0, "conv_n": 0, "qphase_ms": 0.0, "on": False}
 
-    def embed_queries():
+    def embed_queries(queries):
         if not queries:
             return torch.empty((0, 512), device=dev)
         if not qstreams:
@@ -296,25 +325,42 @@ def run_c2(a, world, rank, dev):
                 torch.cuda.synchronize()
                 marks.append((name, time.perf_counter()))
         mark("start")
-        gd = torch.cat([net.forward_test_u8(b) for b in batches], 0) if batches else \
-            torch.empty((0, 512), device=dev)
-        mark("gallery_embed")
-        qd = embed_queries()
-        mark("query_embed")
-        if DIST_ON:
-            gd = torch.cat(_all_gather_var(gd.contiguous(), None)[0], 0)
-            qd = torch.cat(_all_gather_var(qd.contiguous(), None)[0], 0)
-        mark("all_gather")
-        if rank != 0:
-            return None
-        s, i = ops.cosine_topk(qd.contiguous(), gd.contiguous(), n_g)  # full ranks (k = N)
-        ranks = i.cpu().numpy().T.copy()
-        mark("rank")
-        import contextlib
-        with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
-            m = compute_map_and_print("roxford5k", "c2", "global", ranks, gnd)
-        mark("map")
-        return m
+        maps, qev = {}, []
+        for st in sets:
+            if acct["on"]:
+                timer.enable(True)
+            gd = torch.cat([net.forward_test_u8(b) for b in st["batches"]], 0) if st["batches"] else \
+                torch.empty((0, 512), device=dev)
+            if acct["on"]:  # gallery phase: one stream, events do not overlap
+                ms, n = timer.collect(_lib.TIME_GEMM)
+                acct["conv_ms"] += ms
+                acct["conv_n"] += n
+                timer.enable(False)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+            mark(st["name"] + "_gallery_embed")
+            qd = embed_queries(st["queries"])
+            if acct["on"]:  # query phase: concurrent streams, counted by its wall time
+                e1.record()
+                qev.append((e0, e1))
+            mark(st["name"] + "_query_embed")
+            if DIST_ON:
+                gd = torch.cat(_all_gather_var(gd.contiguous(), None)[0], 0)
+                qd = torch.cat(_all_gather_var(qd.contiguous(), None)[0], 0)
+            mark(st["name"] + "_all_gather")
+            if rank != 0:
+                continue
+            s, i = ops.cosine_topk(qd.contiguous(), gd.contiguous(), st["n_g"])  # full ranks (k = N)
+            ranks = i.cpu().numpy().T.copy()
+            mark(st["name"] + "_rank")
+            import contextlib
+            with contextlib.redirect_stdout(sys.stderr):  # stdout carries only the JSON line
+                maps[st["name"]] = compute_map_and_print(st["name"], "c2", "global", ranks, st["gnd"])
+            mark(st["name"] + "_map")
+        for e0, e1 in qev:
+            e1.synchronize()
+            acct["qphase_ms"] += e0.elapsed_time(e1)
+        return maps
 
     for _ in range(a.warmup):
         step()
@@ -322,8 +368,7 @@ def run_c2(a, world, rank, dev):
     step(marks)  # one more untimed step with a sync at every phase boundary
     phases = {b[0]: round((b[1] - a_[1]) * 1e3, 2) for a_, b in zip(marks, marks[1:])}
     log(f"[rank {rank}] c2 phases (ms, synchronised step): {phases}")
-    timer = ops.KernelTimer(dev.index)
-    timer.enable(True)
+    acct["on"] = True
     if DIST_ON:
         dist.barrier()
     torch.cuda.synchronize()
@@ -334,55 +379,56 @@ def run_c2(a, world, rank, dev):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    cls = {name: timer.collect(c) for name, c in (("conv_gemm", _lib.TIME_GEMM), ("select", _lib.TIME_SELECT),
-                                                   ("elementwise", _lib.TIME_ELEM),
-                                                   ("cosine_seed", _lib.TIME_COSINE_SEED))}
-    timer.enable(False)
     if DIST_ON:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-    units = n_g + n_q
+    units = sum(st["n_g"] + st["n_q"] for st in sets)
     value = units * a.steps / elapsed
     # algorithmic FLOPs of this rank's share: every image's trunk convs + the 2048->512 projection
-    img_flops = sum(c_ * (sum(W.resnet_conv_flops("resnet50", h, w).values()) + 2 * 2048 * 512)
-                    for (h, w, c_) in [(h, w, max(0, min(s0 + c, ghi) - max(s0, glo)))
-                                       for (h, w, c), s0 in zip(groups, np.cumsum([0] + [g[2] for g in groups]))])
-    img_flops += sum(sum(W.resnet_conv_flops("resnet50", h, w).values()) + 2 * 2048 * 512 for (h, w) in qsizes[qlo:qhi])
+    img_flops = sum(st["flops"] for st in sets)
     rk = {}
-    ms, n = cls["conv_gemm"]
-    if n:
-        sec = ms / 1e3 / a.steps
+    conv_ms = acct["conv_ms"] + acct["qphase_ms"]
+    if acct["conv_n"]:
+        sec = conv_ms / 1e3 / a.steps
         dt = a.conv_math if a.conv_math in SPLIT_MATH else "fp32"
         ach = img_flops / sec / 1e12
         rk["conv_gemm"] = {"bound": "mfma", "achieved": round(ach, 2), "peak": PEAK_TFLOPS[dt], "unit": "TFLOP/s",
-                           "frac": round(ach / PEAK_TFLOPS[dt], 4), "dtype": "fp32", "ms_per_step": round(ms / a.steps, 3),
-                           "launches_per_step": n / a.steps, "algorithmic_flop_per_launch": img_flops / max(1.0, n / a.steps),
-                           "algorithmic_bytes_per_launch": None, "traffic": None}
+                           "frac": round(ach / PEAK_TFLOPS[dt], 4), "dtype": "fp32",
+                           "ms_per_step": round(conv_ms / a.steps, 3),
+                           "gallery_conv_kernel_ms_per_step": round(acct["conv_ms"] / a.steps, 3),
+                           "query_phase_wall_ms_per_step": round(acct["qphase_ms"] / a.steps, 3),
+                           "timing": "gallery phases: summed per-launch HIP events (one stream); query phases "
+                                     "(8 concurrent streams): whole phase wall time on the main stream",
+                           "gallery_launches_per_step": acct["conv_n"] / a.steps,
+                           "algorithmic_flop_per_step": img_flops, "algorithmic_bytes_per_launch": None,
+                           "traffic": None}
         if dt in SPLIT_MATH:
             rk["conv_gemm"]["math"] = SPLIT_MATH[dt][1]
-            rk["conv_gemm"]["mfma_flop_per_launch"] = SPLIT_MATH[dt][0] * img_flops / max(1.0, n / a.steps)
-    for name in ("select", "elementwise", "cosine_seed"):
-        ms, n = cls[name]
-        rk[name] = {"ms_per_step": round(ms / a.steps, 3), "launches_per_step": n / a.steps}
+            rk["conv_gemm"]["mfma_flop_per_step"] = SPLIT_MATH[dt][0] * img_flops
+            if dt == "h2":
+                rk["conv_gemm"]["frac_of_bf16x3_ceiling"] = round(ach / PEAK_TFLOPS["s3"], 4)
     roof = dict(rk.get("conv_gemm", {}))
     roof["kernel"] = "conv_gemm"
+    desc = " + ".join(f"{st['name']} ({st['n_g']} gallery + {st['n_q']} query images)" for st in sets)
     res = {"metric": METRIC, "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps,
            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 3), "higher_is_better": True,
            "scaling": "strong", "vs_baseline": None, "dtype": "fp32",
            "data": "synthetic: uint8 images at ROxford5k's post-thumbnail(1024) sizes (768x1024 / 1024x768 / 683x1024 / "
-                   "1024x683) and random 200-768 x 200-1024 query crops, torch.Generator(1234); synthetic "
-                   "ROxford5k-shaped gnd (mAP is pipeline parity, not accuracy); seeded weights",
-           "config": {"workload": f"C2: resnet50-GeM 512-d fp32 (Table-1 GeMModel), {n_g} gallery + {n_q} query "
-                                  f"images at imsize 1024, full ranks + revisited mAP",
-                      "global_batch": units, "gallery_rows": n_g, "queries": n_q, "dim": 512,
+                   "1024x683, the same mix for RParis6k) and random 200-768 x 200-1024 query crops, "
+                   "torch.Generator(1234); synthetic revisitop-shaped gnd (mAP is pipeline parity, not accuracy); "
+                   "seeded weights",
+           "config": {"workload": f"C2: resnet50-GeM 512-d fp32 (Table-1 GeMModel), {desc} at imsize 1024, "
+                                  f"full ranks + revisited mAP per dataset",
+                      "global_batch": units, "datasets": [st["name"] for st in sets],
+                      "gallery_rows": [st["n_g"] for st in sets], "queries": [st["n_q"] for st in sets], "dim": 512,
                       "gallery_batch": a.c2_batch, "parallelism": f"image-dp{world}", "conv_math": a.conv_math},
-           "map_easy_medium_hard": list(maps) if maps is not None else None,
+           "map_easy_medium_hard": {k: list(v) for k, v in maps.items()} if maps else None,
            "phases_ms_synchronised_step": phases,
            "roofline": roof, "roofline_by_kernel": rk}
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         t = time.time()
-        res["cpu_baseline"] = cpu_baseline_c2(n_g, n_q)
+        res["cpu_baseline"] = cpu_baseline_c2([(st["n_g"], st["n_q"]) for st in sets])
         log(f"cpu baseline {time.time() - t:.1f}s")
     if rank == 0:
         print(json.dumps(res), flush=True)
@@ -425,7 +471,7 @@ def main():
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--arch", default="resnet101")
     ap.add_argument("--workload", choices=("c2", "c3", "c4", "c5"), default="c3",
-                    help="c2: ResNet50-GeM 512-d fp32 over a ROxford5k-shaped set at imsize 1024 (full ranks + mAP); "
+                    help="c2: ResNet50-GeM 512-d fp32 over ROxford5k- + RParis6k-shaped sets at imsize 1024 (full ranks + mAP); "
                          "c3: ResNet101-GeM 2048-d + PCA-w, fp32 (BASELINE metric config); "
                          "c4: ViT-B/16 CLS 512-d, bf16 GEMMs + bf16 cosine; "
                          "c5: c3 extractor at 3 scales + fp8 cosine + alpha-QE re-rank (sharded: neighbour rows fetched from their shards)")
@@ -443,8 +489,10 @@ def main():
                     help="ranker workspace budget per rank (bounded candidate buffers, overflowed queries re-run; "
                          "0 = the worst-case size, ~Q*N*8 bytes)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--c2-gallery", type=int, default=C2_GALLERY)
-    ap.add_argument("--c2-queries", type=int, default=C2_QUERIES)
+    ap.add_argument("--c2-dataset", choices=("both", "roxford5k", "rparis6k"), default="both",
+                    help="C2 sets per step (BASELINE C2: full ROxford5k + RParis6k)")
+    ap.add_argument("--c2-gallery", type=int, default=0, help="override every C2 set's gallery size (0: revisitop's)")
+    ap.add_argument("--c2-queries", type=int, default=0, help="override every C2 set's query count (0: 70)")
     ap.add_argument("--c2-batch", type=int, default=C2_BATCH, help="same-size gallery images per extractor call")
     ap.add_argument("--c2-qstreams", type=int, default=8, help="HIP streams for the batch-1 query crops (1: serial)")
     a = ap.parse_args()
@@ -533,10 +581,11 @@ def main():
 
     def step():
         desc = embed()
-        if a.workload == "c5" and sharded is not None:
-            # sharded alpha-QE: neighbour rows fetched from their owning shards (bit-identical to 1 GPU)
-            s2, i2, _ = sharded.alpha_qe_search(desc, a.k, n=2, alpha=3.0, counts=counts)
-            return s2, i2
+        if sharded is not None:
+            # C3 / C4: sharded search; C5: + alpha-QE with neighbour rows fetched
+            # from their owning shards (bit-identical to 1 GPU); tests/test_distributed_gloo.py
+            # drives this same sharded_step at world 2 and 4
+            return sharded_step(sharded, desc, a.workload, a.k, counts, n=2, alpha=3.0)
         if a.workload == "c5":
             q_lp, q_sc = ops.quantize_rows(desc, a.dtype)
             s1, i1 = ops.cosine_topk_lp(q_lp, q_sc, gal_lp, gal_sc, a.k, a.dtype, idx_offset=lo, workspace=ws,

@@ -307,6 +307,25 @@ int rr_conv2d_h2(rr_handle_t h, const float* x, const unsigned* x_amax, int b,
                  int kw, int stride, int pad, const float* residual, int relu,
                  float* y, unsigned* y_amax, void* stream);
 
+/* The output of a stage-entry bottleneck block on the f16x2 core, its 1x1
+ * conv3 and its 1x1 strided downsample projection as ONE GEMM over
+ * K = planes + cin:
+ *   out = ReLU(y . W3^T + x[:, ::stride, ::stride] . Wd^T + bias)
+ * (torchvision Bottleneck / the reference's ResBlock sum,
+ * networks/backbone.py:327-346), so the projected identity is never written
+ * or read back.  y: conv2's output [b][oh][ow][planes] with its max-|x|
+ * record y_amax; x: the block input [b][hx][wx][cin] with x_amax;
+ * (oh - 1) * stride < hx, (ow - 1) * stride < wx.  w2 / w_iscale:
+ * rr_split2_f16 of the concatenated rows [W3 | Wd] [cout][planes + cin];
+ * bias = the two folded biases' sum.  planes % 32 == 0, cin % 32 == 0,
+ * cout % 256 == 0.  out_amax as rr_conv2d_h2's y_amax.                      */
+int rr_bottleneck_out_h2(rr_handle_t h, const float* y, const unsigned* y_amax,
+                         int b, int oh, int ow, int planes, const float* x,
+                         const unsigned* x_amax, int hx, int wx, int cin,
+                         int stride, const void* w2, const float* w_iscale,
+                         const float* bias, int cout, float* out,
+                         unsigned* out_amax, void* stream);
+
 /* fp16 2-way split of the rows of w [rows][k] (done once per weight tensor):
  * row n is scaled by 2^e_n, its max |w| then in [2^14, 2^15), and split into
  * planes [2][rows][kpad] (fp16 bit patterns, zero past k; kpad >= k, a

@@ -59,6 +59,8 @@ SIGNATURES = {
     "rr_split3_bf16": (_i, [_vp, _vp, _ll, _vp, _vp]),
     "rr_conv2d_h2": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp]),
     "rr_split2_f16": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
+    "rr_bottleneck_out_h2": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _vp,
+                                  _vp, _vp]),
     "rr_amax_f32": (_i, [_vp, _vp, _ll, _vp, _vp]),
     "rr_resize_bilinear": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _f, _f, _vp, _vp]),
     "rr_maxpool2d": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),

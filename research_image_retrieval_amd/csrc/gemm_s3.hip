@@ -671,8 +671,9 @@ __device__ __forceinline__ int s3_opaque(int v) {
   return v;
 }
 
-template <int EPI, int SP = 3>
+template <int EPI, int SP = 3, int SEG2 = 0>
 __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_n, int ntiles) {
+  static_assert(!SEG2 || SP == 2, "two-segment A: f16x2 only");
   static_assert(SP == 3 || (EPI & EP_SCALE), "f16x2: scaled epilogue");
   typedef typename S3Frag<SP>::T frag_t;
   constexpr int NP = SP;
@@ -687,6 +688,10 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
   __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STG];
   uint32_t a_amax_w = 0;
   if constexpr (SP == 2) a_amax_w = amax_load_slot(g.a_amax);
+  if constexpr (SEG2) {  // one split scale for both segments: the larger max
+    const uint32_t w2 = amax_load_slot(g.a2_amax);
+    a_amax_w = w2 > a_amax_w ? w2 : a_amax_w;
+  }
   float a_sc = 1.f, a_isc = 1.f, am = 0.f;
 
   // round stagger: every block is resident from the start, so half of them
@@ -730,6 +735,18 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
     const int m = min(m0 + t / SL, g.M - 1);
     a_ptr = g.A + (long long)m * g.lda + (t % SL) * 8;
   };
+  // SEG2: from k-tile K1 / BK on, the row's pointer moves to its sampled
+  // pixel of A2 (minus K1, so a_ptr + a_kt * BK stays the element address)
+  auto a_seg2 = [&](int tl) {
+    int m0, n0;
+    tile_origin(tl, m0, n0);
+    const int t = s3_opaque(tid);
+    const int m = min(m0 + t / SL, g.M - 1);
+    const int ohw = g.OH * g.OW;
+    const int b = m / ohw, r = m - b * ohw, oh = r / g.OW, ow = r - oh * g.OW;
+    const long long pix = ((long long)b * g.H2 + (long long)oh * g.s2) * g.W2 + (long long)ow * g.s2;
+    a_ptr = g.A2 + pix * g.lda2 + (t % SL) * 8 - g.K1;
+  };
   a_tile(0);
   f32x4 ra2[2][2];
   auto load_a = [&](int rb) {
@@ -737,6 +754,8 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
     if (++a_kt == nk) {
       a_kt = 0;
       a_tile(++a_tl);
+    } else if (SEG2 && a_kt * BK == g.K1) {
+      a_seg2(a_tl);
     }
   };
   u32x4 pk[NP];
@@ -1022,7 +1041,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
   }
 }
 
-template <int EPI, int SP = 3>
+template <int EPI, int SP = 3, int SEG2 = 0>
 static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   const long long tiles_m = (g.M + 127) / 128, tiles_n = g.N / 256;
   const long long ntiles = tiles_m * tiles_n;
@@ -1034,7 +1053,8 @@ static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
   const int grid = ntiles <= slots ? (int)ntiles : slots;
   g.stagger_blocks = grid;
   g.stagger_sleeps = ntiles > 2LL * grid ? stagger : 0;
-  hipLaunchKernelGGL((gemm_s3p_kernel<EPI, SP>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
+  hipLaunchKernelGGL((gemm_s3p_kernel<EPI, SP, SEG2>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n,
+                     (int)ntiles);
   return hipGetLastError();
 }
 
@@ -1198,6 +1218,25 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
     case 7: return launch_s3_ep<8, 1, 1, 2, 16, AM, 4, 0, 2>(g, s, n_cu, st);
     default: return launch_s3_ep<4, 2, 2, 2, 32, AM, 1, 0, 2>(g, s, n_cu, st);
   }
+}
+
+int launch_gemm_h2_seg2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int timer_cls) {
+  if (g.M < 0 || g.N <= 0 || g.K <= 0 || g.K1 <= 0 || g.K1 >= g.K || (g.K % 32) || (g.K1 % 32) || (g.N % 256))
+    return set_error(h, RR_EINVAL, "gemm_h2_seg2: K1, K - K1 multiples of 32 and N % 256 == 0");
+  if ((g.lda & 3) || (g.lda2 & 3) || ((uintptr_t)g.A & 15) || ((uintptr_t)g.A2 & 15) || g.OH <= 0 || g.OW <= 0 ||
+      g.s2 <= 0 || (long long)(g.OH - 1) * g.s2 >= g.H2 || (long long)(g.OW - 1) * g.s2 >= g.W2)
+    return set_error(h, RR_EINVAL, "gemm_h2_seg2: bad A / A2 layout");
+  if (g.col_scale == nullptr || g.a_amax == nullptr || g.a2_amax == nullptr || g.residual != nullptr ||
+      g.relu != 1 || g.out_bf16 || (g.ldb & 7) || (g.b_plane & 7) || ((uintptr_t)g.B & 15) ||
+      ((uintptr_t)g.col_scale & 15))
+    return set_error(h, RR_EINVAL, "gemm_h2_seg2: ReLU epilogue, scales and both max-|x| records");
+  if (g.M == 0) return RR_OK;
+  hipError_t e;
+  {
+    TimedLaunch tl(h, timer_cls, s);
+    e = launch_s3p_t<H2_EP | EP_RELU, 2, 1>(g, s, device_cu_count(h), h->tune.s3_stagger >= 0 ? h->tune.s3_stagger : 0);
+  }
+  return check_hip(h, e, "gemm_h2_seg2 launch");
 }
 
 int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls, int sp) {

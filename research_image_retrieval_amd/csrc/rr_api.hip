@@ -493,6 +493,51 @@ int rr_conv2d_h2(rr_handle_t h, const float* x, const unsigned* x_amax, int b, i
   return launch_gemm_s3(h, dense ? A_DENSE : (cin == 4 ? A_CONV_C4 : A_CONV), g, (hipStream_t)stream, kTimeGemm, 2);
 }
 
+int rr_bottleneck_out_h2(rr_handle_t h, const float* y, const unsigned* y_amax, int b, int oh, int ow, int planes,
+                         const float* x, const unsigned* x_amax, int hx, int wx, int cin, int stride, const void* w2,
+                         const float* w_iscale, const float* bias, int cout, float* out, unsigned* out_amax,
+                         void* stream) {
+  RR_ENTRY(h);
+  if (!y || !y_amax || !x || !x_amax || !w2 || !w_iscale || !out || b < 0 || oh <= 0 || ow <= 0 || planes <= 0 ||
+      hx <= 0 || wx <= 0 || cin <= 0 || stride <= 0 || cout <= 0)
+    return set_error(h, RR_EINVAL, "rr_bottleneck_out_h2: bad argument");
+  if ((planes % 32) || (cin % 32) || (cout % 256))
+    return set_error(h, RR_EINVAL, "rr_bottleneck_out_h2: planes % 32, cin % 32 and cout % 256 must be 0");
+  if ((long long)(oh - 1) * stride >= hx || (long long)(ow - 1) * stride >= wx)
+    return set_error(h, RR_EINVAL, "rr_bottleneck_out_h2: the strided samples leave x");
+  const long long M = (long long)b * oh * ow;
+  if (M > 0x7fffffffLL || (long long)b * hx * wx > 0x7fffffffLL)
+    return set_error(h, RR_EINVAL, "rr_bottleneck_out_h2: too many pixels");
+  if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || ((uintptr_t)w2 & 15) || ((uintptr_t)w_iscale & 15))
+    return set_error(h, RR_EINVAL, "rr_bottleneck_out_h2: y/x/w2/w_iscale must be 16-byte aligned");
+  GemmArgs g;
+  g.A = y;
+  g.lda = planes;
+  g.M = (int)M;
+  g.K = planes + cin;
+  g.K1 = planes;
+  g.A2 = x;
+  g.lda2 = cin;
+  g.H2 = hx;
+  g.W2 = wx;
+  g.s2 = stride;
+  g.OH = oh;
+  g.OW = ow;
+  g.B = reinterpret_cast<const float*>(w2);
+  g.ldb = g.K;
+  g.b_plane = (long long)cout * g.K;
+  g.N = cout;
+  g.C = out;
+  g.ldc = cout;
+  g.bias = bias;
+  g.relu = 1;
+  g.col_scale = w_iscale;
+  g.a_amax = y_amax;
+  g.a2_amax = x_amax;
+  g.c_amax = out_amax;
+  return launch_gemm_h2_seg2(h, g, (hipStream_t)stream, kTimeGemm);
+}
+
 int rr_split2_f16(rr_handle_t h, const float* w, int rows, int k, int kpad, void* planes, float* iscale,
                   void* stream) {
   RR_ENTRY(h);

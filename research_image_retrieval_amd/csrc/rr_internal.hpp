@@ -203,6 +203,15 @@ struct GemmArgs {
   // resident blocks), every other XCD-slot one sleeps stagger_sleeps x ~2k
   // cycles before starting, so later rounds run half the CUs out of phase
   int stagger_blocks = 0, stagger_sleeps = 0;
+  // two-segment dense A (gemm_s3p_kernel SEG2; the stage-entry bottleneck's
+  // conv3 and downsample projection as one GEMM over K = K1 + K2): k < K1
+  // reads row m of A (lda); k >= K1 reads channel k - K1 of A2 at the pixel
+  // output pixel m (of the OH x OW map) samples at stride s2 from the H2 x W2
+  // NHWC map A2 (lda2 channels); a2_amax: A2's max-|x| record
+  const float* A2 = nullptr;
+  long long lda2 = 0;
+  int K1 = 0, H2 = 0, W2 = 0, s2 = 1;
+  const uint32_t* a2_amax = nullptr;
 };
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,
@@ -213,6 +222,8 @@ int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStre
 // [3][N][ldb] from launch_split3; sp = 2: B = fp16 planes [2][N][ldb] +
 // col_scale from launch_split2h, A scaled by its a_amax
 int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls, int sp = 3);
+// f16x2 two-segment GEMM (GemmArgs A2 / K1): the persistent tile, N % 256 == 0
+int launch_gemm_h2_seg2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int timer_cls);
 // fp16 2-way split of the rows of w [rows][k] into planes [2][rows][kpad]
 // (zero-padded) at a per-row power-of-two scale, iscale[row] = its inverse
 int launch_split2h(rr_handle_s* h, const float* w, int rows, int k, int kpad, uint16_t* planes, float* iscale,

@@ -48,6 +48,26 @@ def _host_staged(group):
     return dist.get_backend(group) == "gloo"
 
 
+def _to_comm(t, group):
+    """The tensor a collective of `group` can move (host copy under gloo)."""
+    return t.cpu() if _host_staged(group) else t
+
+
+# device->host reads the sharded path made (size exchanges); with every
+# rank's query count known (`counts`) search / gather_rows make none
+HOST_READS = [0]
+
+
+def _exchange_sizes(n_rows, group, device):
+    """Every rank's first dim: one small all-gather and one device->host read."""
+    world = dist.get_world_size(group)
+    n = torch.tensor([n_rows], dtype=torch.int64, device=device)
+    parts = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(parts, n, group=group)
+    HOST_READS[0] += 1
+    return torch.cat(parts).tolist()
+
+
 def _all_gather_var(t, group, sizes=None):
     """all_gather of tensors whose first dim may differ across ranks.  With
     `sizes` (every rank's first dim, known to all ranks, e.g. a fixed batch)
@@ -55,13 +75,9 @@ def _all_gather_var(t, group, sizes=None):
     and one device->host read."""
     world = dist.get_world_size(group)
     dev = t.device
-    if _host_staged(group):
-        t = t.cpu()
+    t = _to_comm(t, group)
     if sizes is None:
-        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
-        parts = [torch.zeros_like(n) for _ in range(world)]
-        dist.all_gather(parts, n, group=group)
-        sizes = torch.cat(parts).tolist()
+        sizes = _exchange_sizes(t.shape[0], group, t.device)
     else:
         sizes = [int(x) for x in sizes]
         if len(sizes) != world or sizes[dist.get_rank(group)] != t.shape[0]:
@@ -133,9 +149,15 @@ class ShardedGallery:
     def gather_rows(self, idx, counts=None):
         """Rows g[idx] of the global gallery for this rank's queries: idx
         [B_r, n] int64 (global rows; < 0 = padding -> a zero row) -> [B_r, n, D]
-        fp32, each row an exact copy from the shard that owns it (one
-        variable-split all-to-all).  counts: every rank's B_r when known (no
-        size exchange); the split sizes then cost one device->host read."""
+        fp32, each row an exact copy from the shard that owns it.
+
+        Fixed-size exchange, no data-dependent split sizes: every rank sends
+        each requester r a [B_r * n, D] block holding the rows it owns in
+        their request slots (zeros elsewhere), and the requester picks every
+        slot from its owner's block.  With counts (every rank's B_r) nothing
+        here reads the device from the host; without, one size exchange.
+        Bytes per rank: Q * n * D * 4 out and W * B_r * n * D * 4 in (W times
+        the owned rows alone, which would need their counts on the host)."""
         group = self.group
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
@@ -143,29 +165,21 @@ class ShardedGallery:
         b, n = idx.shape
         d = self.shard.shape[1]
         ids, sizes = _all_gather_var(idx.contiguous(), group, counts)
-        # every rank's requests, requesting-rank-major, (query, neighbour) order within
+        # every rank's requests, requester-major, (query, neighbour) order within
         req = torch.cat([x.reshape(-1).to(dev) for x in ids]) if ids else idx.new_empty((0,)).to(dev)
-        seg = torch.cat([torch.full((sz * n,), r, dtype=torch.int64, device=dev) for r, sz in enumerate(sizes)])
-        # padding slots (idx < 0: fewer gallery rows than neighbours) have no owner
         mine = (req >= 0) & (self._owner(req.clamp_min(0)) == rank)
-        skey = torch.where(mine, seg, torch.full_like(seg, world))  # rows to send, grouped by requester
-        send_order = torch.argsort(skey, stable=True)
+        if self.shard.shape[0] > 0:
+            rows = self.shard.index_select(0, (req - self.offset).clamp(0, self.shard.shape[0] - 1))
+            sendbuf = torch.where(mine[:, None], rows, torch.zeros((), dtype=rows.dtype, device=dev))
+        else:
+            sendbuf = self.shard.new_zeros((req.shape[0], d))
+        recvbuf = _to_comm(self.shard.new_empty((world * b * n, d)), group)
+        dist.all_to_all_single(recvbuf, _to_comm(sendbuf.contiguous(), group), [b * n] * world,
+                               [sz * n for sz in sizes], group=group)
+        blocks = torch.cat([recvbuf.to(dev).view(world, b * n, d), self.shard.new_zeros((1, b * n, d))])
         flat = idx.reshape(-1).to(dev)
         own = torch.where(flat >= 0, self._owner(flat.clamp_min(0)), torch.full_like(flat, world))
-        recv_order = torch.argsort(own, stable=True)  # own slots grouped by owner rank
-        ones = torch.ones_like(skey)
-        counts2 = torch.stack([torch.zeros(world + 1, dtype=torch.int64, device=dev).scatter_add_(0, skey, ones),
-                               torch.zeros(world + 1, dtype=torch.int64, device=dev).scatter_add_(
-                                   0, own, torch.ones_like(own))]).cpu()  # the one host sync
-        send_counts, recv_counts = counts2[0, :world].tolist(), counts2[1, :world].tolist()
-        n_send, n_recv = sum(send_counts), sum(recv_counts)
-        sendbuf = self.shard.index_select(0, req[send_order[:n_send]] - self.offset)
-        recvbuf = self.shard.new_empty((n_recv, d))
-        if _host_staged(group):
-            sendbuf, recvbuf = sendbuf.cpu(), recvbuf.cpu()
-        dist.all_to_all_single(recvbuf, sendbuf.contiguous(), recv_counts, send_counts, group=group)
-        out = self.shard.new_zeros((b * n, d))  # padding slots stay zero (and get weight 0)
-        out.index_copy_(0, recv_order[:n_recv], recvbuf.to(dev))
+        out = blocks[own, torch.arange(b * n, device=dev)]  # padding slots pick the zero block
         return out.view(b, n, d)
 
     def alpha_qe_search(self, queries, k=100, n=2, alpha=3.0, expand=None, counts=None):
@@ -195,8 +209,10 @@ class ShardedGallery:
     def search(self, queries, k, counts=None):
         """queries [B_r, D] (this rank's) -> (scores [B_r,k], global idx [B_r,k]).
         counts: every rank's B_r, when all ranks know them (a fixed batch):
-        then the search has no host sync (the merge and the collectives stay
-        on the stream); without, one size all-gather + one host read."""
+        then the collectives and the merge make no host sync; without, one
+        size all-gather + one host read.  With max_workspace_bytes set, the
+        local ranker reads its 4-byte overflow count once per call
+        (ops._recover_overflow), which syncs the stream."""
         group = self.group
         world = dist.get_world_size(group)
         rank = dist.get_rank(group)
@@ -207,11 +223,21 @@ class ShardedGallery:
         # (B_r * W * k * 12 bytes in per rank instead of Q * W * k * 12)
         mine = sizes[rank]
         dev = s.device
-        if _host_staged(group):
-            s, i = s.cpu(), i.cpu()
+        s, i = _to_comm(s, group), _to_comm(i, group)
         rs = s.new_empty((world * mine, k))
         ri = i.new_empty((world * mine, k))
         dist.all_to_all_single(rs, s.contiguous(), [mine] * world, sizes, group=group)
         dist.all_to_all_single(ri, i.contiguous(), [mine] * world, sizes, group=group)
         rs, ri = rs.to(dev), ri.to(dev)
         return self._merge_parts(rs.view(world, mine, k).contiguous(), ri.view(world, mine, k).contiguous(), k)
+
+
+def sharded_step(sharded, desc, workload, k, counts, n=2, alpha=3.0, expand=None):
+    """The rank step of bench.py's sharded workloads after embedding: C3 / C4
+    rank this rank's descriptors against the whole row-sharded gallery; C5
+    ranks, alpha-QE-expands with the top-n neighbour rows fetched from their
+    owning shards, and ranks again.  -> (scores [B_r,k], global idx [B_r,k])."""
+    if workload == "c5":
+        s2, i2, _ = sharded.alpha_qe_search(desc, k, n=n, alpha=alpha, expand=expand, counts=counts)
+        return s2, i2
+    return sharded.search(desc, k, counts)

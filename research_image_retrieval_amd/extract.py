@@ -3,7 +3,8 @@ on librr.
 
 Same contract: ``extract_vectors(net, loader, ms=[1], device, print_freq)``
 returns a CPU float32 [N, net.outputdim] in loader order, with the reference's
-single-scale small-image upsampling (:24-26) and multi-scale averaging
+single-scale small-image upsampling (:24-26; a single scale ms=[s] is NOT
+applied, as the reference's len(ms) == 1 branch ignores it) and multi-scale averaging
 (:30-46: bilinear rescale, scales whose result is < 36 px dropped, sum /
 (len(ms) - drop), L2 renormalisation).  Differences, all deliberate:
   * loaders may be BATCHED (the reference requires batch size 1);
@@ -58,10 +59,10 @@ def extract_vectors(net, loader, ms=(1,), device=torch.device("cuda"), print_fre
         x = _nhwc(batch, device)
         b, h, w = x.shape[0], x.shape[1], x.shape[2]
         if len(ms) == 1:
+            # as the reference's single-scale branch (:22-27): ms[0] itself is
+            # never applied, only images below 36 px are upsampled
             if h < MIN_SIDE or w < MIN_SIDE:
                 x = _rescale(x, max(UPSAMPLE_TO / h, UPSAMPLE_TO / w))
-            elif ms[0] != 1:
-                x = _rescale(x, ms[0])
             v = _forward(net, x)
         else:
             acc = None

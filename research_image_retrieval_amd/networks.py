@@ -64,6 +64,14 @@ class ResNet:
             self.stem_s3 = ops.split3_stem(self.convs["conv1"][0])
         elif conv_math == "h2":
             self.convs_h2 = {k: ops.H2Conv(w) for k, (w, _) in self.convs.items()}
+            # each stage's first block: conv3 + downsample as one GEMM (ops.H2Bottleneck)
+            self.fuse_downsample = True
+            self.bneck_h2 = {}
+            for li in range(len(self.layers)):
+                p = f"layer{li + 1}.0"
+                (w3, b3), (wd, bd) = self.convs[p + ".conv3"], self.convs[p + ".downsample.0"]
+                if w3.shape[0] % 256 == 0:
+                    self.bneck_h2[p] = ops.H2Bottleneck(w3, b3, wd, bd)
 
     def _conv(self, x, name, stride, pad, relu, residual=None):
         w, b = self.convs[name]
@@ -78,7 +86,9 @@ class ResNet:
         """The trunk on the f16x2 core: every conv reads its input's max-|x|
         record and writes its output's (one zeroed [2 + 3 blocks, 64] tensor per
         forward); the max-pool output reuses the stem's record (every stem
-        output lies in some 3x3/2 window, so the max is the same)."""
+        output lies in some 3x3/2 window, so the max is the same).  A stage's
+        first block runs conv3 and its downsample projection as one GEMM
+        (ops.bottleneck_out_h2), so the projected identity never reaches HBM."""
         cv, h2 = self.convs, self.convs_h2
         rec = ops.amax_records(2 + 3 * sum(self.layers), x.device)
         ops.amax_f32(x, rec[0])
@@ -90,10 +100,15 @@ class ResNet:
                 p = f"layer{li + 1}.{bi}"
                 s1, s2 = W.block_strides(2 if (bi == 0 and li > 0) else 1, self.stride_on)
                 d = f"{p}.downsample.0"
-                idn = ops.conv2d_h2(x, xa, h2[d], cv[d][1], s1 * s2, 0, None, False) if bi == 0 else x
+                fused = bi == 0 and self.fuse_downsample and p in self.bneck_h2
+                idn = ops.conv2d_h2(x, xa, h2[d], cv[d][1], s1 * s2, 0, None, False) if bi == 0 and not fused else x
                 y = ops.conv2d_h2(x, xa, h2[f"{p}.conv1"], cv[f"{p}.conv1"][1], s1, 0, None, True, rec[r])
                 y = ops.conv2d_h2(y, rec[r], h2[f"{p}.conv2"], cv[f"{p}.conv2"][1], s2, 1, None, True, rec[r + 1])
-                x = ops.conv2d_h2(y, rec[r + 1], h2[f"{p}.conv3"], cv[f"{p}.conv3"][1], 1, 0, idn, True, rec[r + 2])
+                if fused:
+                    x = ops.bottleneck_out_h2(y, rec[r + 1], x, xa, self.bneck_h2[p], s1 * s2, rec[r + 2])
+                else:
+                    x = ops.conv2d_h2(y, rec[r + 1], h2[f"{p}.conv3"], cv[f"{p}.conv3"][1], 1, 0, idn, True,
+                                      rec[r + 2])
                 xa, r = rec[r + 2], r + 3
             if li == 2:
                 x3 = x

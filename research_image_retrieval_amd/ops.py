@@ -274,6 +274,43 @@ def conv2d_h2(x, x_amax, wc, bias, stride=1, pad=0, residual=None, relu=False, y
     return y
 
 
+class H2Bottleneck:
+    """Weights of a stage-entry bottleneck's conv3 + downsample projection as
+    one f16x2 GEMM (rr_bottleneck_out_h2): rows [W3 | Wd] split together,
+    bias = b3 + bd."""
+
+    def __init__(self, w3, b3, wd, bd):
+        w3, wd = _f32(w3.contiguous(), "H2Bottleneck w3"), _f32(wd.contiguous(), "H2Bottleneck wd")
+        cout, planes = w3.shape[0], w3.numel() // w3.shape[0]
+        cin = wd.numel() // wd.shape[0]
+        if wd.shape[0] != cout or tuple(w3.shape[1:3]) != (1, 1) or tuple(wd.shape[1:3]) != (1, 1):
+            raise ValueError("H2Bottleneck: 1x1 conv3 and downsample with the same Cout")
+        self.planes, self.cin, self.cout = planes, cin, cout
+        self.planes2, self.iscale = split2_f16(torch.cat([w3.reshape(cout, planes), wd.reshape(cout, cin)], 1))
+        self.bias = (b3.double() + bd.double()).float().contiguous() if b3 is not None else bd.contiguous()
+
+
+def bottleneck_out_h2(y, y_amax, x, x_amax, wb, stride, out_amax=None):
+    """ReLU(conv3(y) + downsample(x)) of a stage-entry bottleneck as one f16x2
+    GEMM (rr_bottleneck_out_h2): y [B,OH,OW,planes], x [B,H,W,cin]."""
+    _f32(y, "bottleneck_out_h2 y")
+    _f32(x, "bottleneck_out_h2 x")
+    if not isinstance(wb, H2Bottleneck):
+        raise TypeError("bottleneck_out_h2: wb must be an ops.H2Bottleneck")
+    b, oh, ow, planes = y.shape
+    bx, hx, wx, cin = x.shape
+    if planes != wb.planes or cin != wb.cin or bx != b:
+        raise ValueError("bottleneck_out_h2: shape mismatch")
+    dev = _dev(y)
+    out = torch.empty((b, oh, ow, wb.cout), dtype=torch.float32, device=y.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_bottleneck_out_h2(hd, _ptr(y), _ptr(y_amax), b, oh, ow, planes, _ptr(x), _ptr(x_amax),
+                                               hx, wx, cin, int(stride), _ptr(wb.planes2), _ptr(wb.iscale),
+                                               _ptr(wb.bias), wb.cout, _ptr(out), _ptr(out_amax), _stream(dev)),
+               hd, "rr_bottleneck_out_h2")
+    return out
+
+
 def resize_bilinear(x_nhwc, out_h, out_w, scale_factor=None):
     """NHWC bilinear resize, align_corners=False.  With ``scale_factor`` the
     source index uses 1/scale_factor, as F.interpolate(scale_factor=s) does."""

@@ -82,6 +82,20 @@ def trunk_fixture():
     np.savez_compressed(os.path.join(HERE, "resnet_dolg.npz"), **out)
 
 
+def extract_fixture():
+    """(vi) extract_vectors on a tiny networks-style extractor (utils/helpfunc.py:18-48):
+    single scale ms=[1], single scale ms=[0.5] (the reference's len(ms) == 1
+    branch never rescales by ms[0]), and three scales."""
+    from utils.helpfunc import extract_vectors
+    tn = I.TinyNetRef(41)
+    imgs = I.tiny_images(42)
+    v1 = extract_vectors(tn, imgs, ms=[1], device=torch.device("cpu"))
+    v05 = extract_vectors(tn, imgs, ms=[0.5], device=torch.device("cpu"))
+    v3 = extract_vectors(tn, imgs, ms=[1, 1 / np.sqrt(2), 1 / 2], device=torch.device("cpu"))
+    np.savez_compressed(os.path.join(HERE, "extract.npz"), net_seed=41, img_seed=42, v1=v1.numpy(), v3=v3.numpy(),
+                        v05=v05.numpy())
+
+
 def main():
     _stub_torchvision()
     sys.path.insert(0, REF)
@@ -90,6 +104,9 @@ def main():
         return
     if "--only-trunk" in sys.argv:
         trunk_fixture()
+        return
+    if "--only-extract" in sys.argv:
+        extract_fixture()
         return
     loader_fixture()
     trunk_fixture()
@@ -177,12 +194,7 @@ def main():
                         medium_map=mAP, medium_aps=aps, medium_pr=pr, medium_prs=prs, medium_map_nokeeps=mAP2,
                         medium_aps_nokeeps=aps2)
 
-    # (vi) multi-scale extract_vectors on a tiny networks-style extractor (utils/helpfunc.py:18-48)
-    tn = I.TinyNetRef(41)
-    imgs = I.tiny_images(42)
-    v1 = extract_vectors(tn, imgs, ms=[1], device=torch.device("cpu"))
-    v3 = extract_vectors(tn, imgs, ms=[1, 1 / np.sqrt(2), 1 / 2], device=torch.device("cpu"))
-    np.savez_compressed(os.path.join(HERE, "extract.npz"), net_seed=41, img_seed=42, v1=v1.numpy(), v3=v3.numpy())
+    extract_fixture()
 
     # (vii) CLIP ViT (networks/model.py:206-243): tiny config and ViT-B/16, seeded weights
     out = {}

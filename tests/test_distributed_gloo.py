@@ -129,3 +129,56 @@ def test_sharded_alpha_qe_world3_matches_single():
         assert np.array_equal(o[3][:, 0], np.broadcast_to(g[0], o[3][:, 0].shape))
         assert not o[3][:, 1].any()
         assert np.array_equal(o[3][:, 2], np.broadcast_to(g[-1], o[3][:, 2].shape))
+
+
+def _step_worker(rank, world, port, q_all, g_all, k, batch, out):
+    """bench.py's sharded rank step (distributed.sharded_step) for C3 and C5
+    with every rank's query count known, as bench runs it (fixed batch)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from research_image_retrieval_amd import distributed as D
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    lo, hi = D.shard_bounds(g_all.shape[0], world, rank)
+    sg = D.ShardedGallery(g_all[lo:hi].contiguous(), lo, local_topk=_local_topk, merge=_merge)
+    counts = [batch] * world
+    sg._bounds()  # the shard bounds are all-gathered once per gallery, before the timed steps
+    desc = q_all[rank * batch:(rank + 1) * batch].contiguous()
+    reads0 = D.HOST_READS[0]
+    res = {w: D.sharded_step(sg, desc, w, k, counts, n=2, alpha=3.0, expand=_expand) for w in ("c3", "c5")}
+    # exact copies through the fixed-size exchange, -0.0 included
+    rows = sg.gather_rows(torch.tensor([[3, g_all.shape[0] - 1]] * batch, dtype=torch.int64), counts)
+    assert D.HOST_READS[0] == reads0, "the counted sharded step read the device from the host"
+    out[rank] = {w: (s.numpy(), i.numpy()) for w, (s, i) in res.items()}, rows.numpy()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_bench_sharded_step_world2_world4_matches_single():
+    """bench.py's C3 and C5 sharded choreography at world 2 and 4 (gloo, the
+    oracle as the local kernels): equal to the single-process pipeline bit
+    for bit, and no host read anywhere in the counted step."""
+    import oracle
+    rs = np.random.RandomState(5)
+    batch, k, dim = 3, 12, 32
+    g = rs.standard_normal((997, dim)).astype(np.float32)
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    g[3, :4] = -0.0
+    for world in (2, 4):
+        q = rs.standard_normal((batch * world, dim)).astype(np.float32)
+        q /= np.linalg.norm(q, axis=1, keepdims=True)
+        g[900] = q[0] * 0.95 + g[900] * 0.05  # a close neighbour on the last shard
+        mgr = mp.Manager()
+        out = mgr.dict()
+        mp.start_processes(_step_worker, args=(world, _free_port(), torch.from_numpy(q), torch.from_numpy(g), k,
+                                               batch, out), nprocs=world, join=True, start_method="spawn")
+        s1, i1 = oracle.cosine_topk(q, g, k)
+        q2 = oracle.alpha_qe(q, g, i1, s1, 2, 3.0)
+        s2, i2 = oracle.cosine_topk(q2, g, k)
+        got = [out[r] for r in range(world)]
+        for w, (s_ref, i_ref) in (("c3", (s1, i1)), ("c5", (s2, i2))):
+            np.testing.assert_array_equal(np.concatenate([o[0][w][1] for o in got]), i_ref)
+            np.testing.assert_array_equal(np.concatenate([o[0][w][0] for o in got]), s_ref)
+        for o in got:
+            assert np.array_equal(o[1][:, 0].view(np.int32), np.broadcast_to(g[3], o[1][:, 0].shape).view(np.int32))
+            assert np.array_equal(o[1][:, 1], np.broadcast_to(g[-1], o[1][:, 1].shape))

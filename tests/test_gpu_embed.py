@@ -107,6 +107,30 @@ def test_extract_vectors_multiscale_vs_reference_fixture(cuda):
     assert np.isnan(v3[~ok]).all()  # all scales dropped -> NaN, as the reference
 
 
+def test_extract_vectors_single_scale_ignores_ms_vs_reference_fixture(cuda):
+    """ms=[0.5]: the reference's len(ms) == 1 branch never rescales by ms[0]
+    (utils/helpfunc.py:22-27), so its output equals ms=[1] (fixture v05)."""
+    fx = np.load(os.path.join(GOLD, "extract.npz"))
+    net = TinyNetGPU(int(fx["net_seed"]), cuda)
+    imgs = I.tiny_images(int(fx["img_seed"]))
+    v05 = extract_vectors(net, imgs, ms=[0.5], device=cuda, print_freq=0).numpy()
+    v1 = extract_vectors(net, imgs, ms=[1], device=cuda, print_freq=0).numpy()
+    np.testing.assert_allclose(v05, fx["v05"], rtol=0, atol=2e-6)
+    assert np.array_equal(v05, v1)
+
+
+def test_gempooling_p25_vs_reference_fixture(cuda):
+    """models.GeMPooling(p=2.5) (models/gem_pooling.py:12-23) on the GPU vs the
+    reference's own output (gem.npz gempool_p25)."""
+    from research_image_retrieval_amd.models import GeMPooling
+    fx = np.load(os.path.join(GOLD, "gem.npz"))
+    x = torch.from_numpy(fx["x"]).permute(0, 2, 3, 1).contiguous()  # NCHW fixture -> NHWC
+    got = GeMPooling(p=2.5)(x.to(cuda)).cpu().numpy()
+    ref = fx["gempool_p25"]
+    print("GeMPooling(p=2.5) vs reference max|err|", np.abs(got.reshape(ref.shape) - ref).max())
+    np.testing.assert_allclose(got.reshape(ref.shape), ref, rtol=2e-6, atol=2e-6)
+
+
 @pytest.mark.parametrize("tag", ["rank_a", "rank_b"])
 def test_ranker_vs_reference_fixture(cuda, tag):
     fx = np.load(os.path.join(GOLD, tag + ".npz"))

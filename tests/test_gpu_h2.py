@@ -237,3 +237,56 @@ def test_resnet_h2_descriptors_vs_float64(cuda):
     e_f32 = (got["f32"] - ref).abs().max().item()
     print(f"R50-GeM descriptors vs float64: h2 {e_h2:.3g}  f32 {e_f32:.3g}")
     assert e_h2 < DESC_TOL and e_h2 <= 2.0 * e_f32
+
+
+@pytest.mark.parametrize("b,hx,cin,planes,stride", [(3, 56, 64, 64, 1), (2, 56, 256, 128, 2), (2, 27, 512, 256, 2),
+                                                    (5, 7, 1024, 512, 2)])
+def test_bottleneck_out_h2_vs_float64(cuda, b, hx, cin, planes, stride):
+    """A stage-entry block's conv3 + strided downsample projection as one
+    f16x2 GEMM (rr_bottleneck_out_h2) vs float64 of the reference's sum
+    ReLU(bn3(conv3(y)) + bn_d(conv_d(x))) (networks/backbone.py:327-346),
+    next to the two-launch exact-fp32 path; odd map sizes included."""
+    g = torch.Generator().manual_seed(b * hx + cin)
+    oh = (hx - 1) // stride + 1
+    cout = 4 * planes
+    y = torch.relu(torch.randn(b, oh, oh, planes, generator=g))
+    x = torch.relu(torch.randn(b, hx, hx, cin, generator=g))
+    w3 = torch.randn(cout, 1, 1, planes, generator=g) / planes ** 0.5
+    wd = torch.randn(cout, 1, 1, cin, generator=g) / cin ** 0.5
+    b3, bd = torch.randn(cout, generator=g) * 0.1, torch.randn(cout, generator=g) * 0.1
+    xs = x[:, ::stride, ::stride].double()
+    ref = y.double() @ w3.reshape(cout, planes).double().t() + b3.double() + xs @ wd.reshape(cout, cin).double().t() \
+        + bd.double()
+    ref = torch.relu(ref)
+    scale = y.double() @ w3.reshape(cout, planes).double().abs().t() + xs @ wd.reshape(cout, cin).double().abs().t()
+    rec = ops.amax_records(3, cuda)
+    yd, xd = y.to(cuda), x.to(cuda)
+    ops.amax_f32(yd, rec[0])
+    ops.amax_f32(xd, rec[1])
+    wb = ops.H2Bottleneck(w3.to(cuda), b3.to(cuda), wd.to(cuda), bd.to(cuda))
+    out = ops.bottleneck_out_h2(yd, rec[0], xd, rec[1], wb, stride, rec[2]).cpu()
+    idn = ops.conv2d(xd, wd.to(cuda), bd.to(cuda), stride, 0, None, False)
+    out_f32 = ops.conv2d(yd, w3.to(cuda), b3.to(cuda), 1, 0, idn, True).cpu()
+    live = ref > 0
+    e = _rel_err(out[live], ref[live], scale[live])
+    ef32 = _rel_err(out_f32[live], ref[live], scale[live])
+    print(f"bottleneck {b}x{hx}x{cin}/{stride} planes {planes}: h2 max {e[0]:.3g} mean {e[1]:.3g} | "
+          f"f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
+    assert e[0] <= max(ef32[0], 1e-7) * 1.5 and e[1] <= ef32[1] * 1.05 + 1e-9
+    assert ops.amax_value(rec[2]) == float(out.abs().max())
+
+
+def test_resnet_h2_fused_downsample_matches_unfused(cuda):
+    """The trunk with the stage-entry conv3 + projection fused equals the
+    unfused f16x2 trunk to fp32 accuracy (only the sum's rounding order
+    differs) and both stay within the trunk tolerance of each other."""
+    from research_image_retrieval_amd.networks import ResNet
+    rs = np.random.RandomState(9)
+    x = torch.from_numpy(rs.standard_normal((2, 96, 80, 3)).astype(np.float32)).to(cuda)
+    net = ResNet("resnet50", seed=3, device=cuda)
+    a = net.forward(x)
+    net.fuse_downsample = False
+    b = net.forward(x)
+    d = (a - b).abs().max().item()
+    print("fused vs unfused trunk max|diff|", d, "max|y|", a.abs().max().item())
+    assert d < 2e-6
