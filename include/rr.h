@@ -44,6 +44,15 @@ extern "C" {
 
 typedef struct rr_handle_s* rr_handle_t;
 
+/* ABI revision of this header.  Bumped when an existing entry changes its
+ * arguments under the same name (a caller built against an older header would
+ * pass shifted arguments): 2 = rr_alpha_qe gained n_rows (round 2); 3 = the
+ * f16x2 entries rr_conv2d_h2 / rr_bottleneck_out_h2 / rr_split2_f16 /
+ * rr_amax_f32 were added (no existing entry changed).  Bindings compare
+ * rr_abi_version() with the RR_ABI_VERSION they were written against.     */
+#define RR_ABI_VERSION 3
+int rr_abi_version(void);
+
 /* ---- handle ------------------------------------------------------------ */
 const char* rr_version(void);
 int rr_create(int device, rr_handle_t* out);

@@ -16,6 +16,8 @@ LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(_HERE, "librr.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_EWORKSPACE, RR_EOVERFLOW = 0, -1, -2, -3, -4
+ABI_VERSION = 3  # RR_ABI_VERSION of include/rr.h these signatures follow
+AMAX_SLOTS = 64  # RR_AMAX_SLOTS
 
 # timing classes (rr_timing_enable / rr_timing_collect)
 TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM, TIME_COSINE_SEED, TIME_ATTN = 0, 1, 2, 3, 4, 5
@@ -34,6 +36,7 @@ _sz = ctypes.c_size_t
 # name -> (restype, argtypes): exactly the symbols include/rr.h declares
 SIGNATURES = {
     "rr_version": (ctypes.c_char_p, []),
+    "rr_abi_version": (_i, []),
     "rr_create": (_i, [_i, ctypes.POINTER(_vp)]),
     "rr_destroy": (_i, [_vp]),
     "rr_last_error": (ctypes.c_char_p, [_vp]),
@@ -119,6 +122,9 @@ def lib():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
+            if not os.environ.get("RR_LIB_PATH") and L.rr_abi_version() != ABI_VERSION:
+                raise RRError(f"librr.so ABI {L.rr_abi_version()} != {ABI_VERSION} this binding was written "
+                              f"against: rebuild it with `make -C {CSRC}`")
             _lib = L
     return _lib
 

@@ -231,11 +231,12 @@ int rr_cosine_topk_prefilter(rr_handle_t h, const float* queries, int nq, const 
   float* eps2 = (float*)(ws + L.off_eps);
   uint16_t* qb = (uint16_t*)(ws + L.off_qb);
   unsigned long long* cand = (unsigned long long*)(ws + L.off_cand);
+  // the overflow count is zeroed on every call (rr.h), the empty gallery included
+  if (int rc = check_hip(h, hipMemsetAsync(ovf, 0, 4, s), "memset")) return rc;
   if (n == 0) {
     if (int rc = check_hip(h, hipMemsetAsync(cnt, 0, (size_t)nq * 4, s), "memset")) return rc;
     return launch_select_final(h, cand, L.cap, cnt, nq, k, idx_offset, out_scores, out_idx, ovf, s);
   }
-  if (int rc = check_hip(h, hipMemsetAsync(ovf, 0, 4, s), "memset")) return rc;
   if (int rc = rr_quantize_rows(h, queries, nq, d, DT_BF16, qb, nullptr, s)) return rc;
   {
     TimedLaunch tl(h, kTimeElem, s);

@@ -76,7 +76,9 @@ using namespace rr;
 
 extern "C" {
 
-const char* rr_version(void) { return "librr 0.1.0 (gfx950, fp32 MFMA)"; }
+const char* rr_version(void) { return "librr 0.3.0 (gfx950: fp32 / f16x2 / bf16x3 / bf16 / fp8 MFMA)"; }
+
+int rr_abi_version(void) { return RR_ABI_VERSION; }
 
 int rr_create(int device, rr_handle_t* out) {
   if (!out) return RR_EINVAL;
@@ -235,11 +237,12 @@ static int cosine_topk_impl(rr_handle_t h, const void* queries, const float* q_s
   int* cnt = (int*)(ws + L.off_cnt);
   int* ovf = (int*)(ws + L.off_ovf);
   unsigned long long* cand = (unsigned long long*)(ws + L.off_cand);
+  // the overflow count is zeroed on every call (rr.h), the empty gallery included
+  if (int rc = check_hip(h, hipMemsetAsync(ovf, 0, 4, s), "memset")) return rc;
   if (n == 0) {  // nothing to rank: all padding
     if (int rc = check_hip(h, hipMemsetAsync(cnt, 0, (size_t)nq * 4, s), "memset")) return rc;
     return launch_select_final(h, cand, L.cap, cnt, nq, k, idx_offset, out_scores, out_idx, ovf, s);
   }
-  if (int rc = check_hip(h, hipMemsetAsync(ovf, 0, 4, s), "memset")) return rc;
   // 1. exact scores of the first s gallery rows (query-major)
   GemmArgs g;
   g.A = (const float*)gallery;
