@@ -100,7 +100,7 @@ __device__ __forceinline__ int h2_exp(float amax) {
 // fixed at compile time and (BI == 1) one column per thread, so the loop is
 // the arithmetic, a row bound and an address step; FL = -1: the flags read
 // from g per element.
-template <int FL, int P, int ITERS, int NT, int C4, int BN, int BI>
+template <int FL, int P, int ITERS, int NT, int C4, int CS, int BI>
 __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const float* ct, const f32x4 (&bias_v)[BI],
                                            const f32x4 (&res)[ITERS], int tid, int mb, int n0, const f32x4 (&sc_v)[BI],
                                            float& am) {
@@ -125,7 +125,7 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
       for (int u = it; u < it + GR && u < ITERS; ++u) {
         const int idx = tid + u * NT;
         const int row = idx / C4, c4 = idx - row * C4;
-        cv[u] = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
+        cv[u] = *reinterpret_cast<const f32x4*>(ct + row * CS + c4 * 4);
       }
     }
     int m, n;
@@ -179,7 +179,17 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
   constexpr int NT = 64 * WM * WN;
   constexpr int WTM = 32 * FM, WTN = 32 * FN;
   constexpr int BM = WTM * WM, BN = WTN * WN;
-  constexpr int P = (BM * BN + CAPF - 1) / CAPF;
+  // staging row stride: padded so the accumulator writes hit distinct banks
+  // (16x16 map: lanes 16 apart are 4 rows apart -> +4 floats per row; 32x32
+  // map: lanes 32 apart are 4 rows apart -> +8); the row-contiguous 16-B
+  // reads of store_slab stay conflict-free and aligned either way
+  // (tiles whose padded slabs would not tile the waves keep unpadded rows)
+  constexpr int CSP = BN + (MF16 ? 4 : 8);
+  constexpr int PP0 = (BM * CSP + CAPF - 1) / CAPF;
+  constexpr int PP = PP0 <= 1 ? 1 : (PP0 <= 2 ? 2 : (PP0 <= 4 ? 4 : 8));  // a divisor of WM
+  constexpr bool PAD = PP <= WM && BM / PP * CSP <= CAPF;
+  constexpr int CS = PAD ? CSP : BN;
+  constexpr int P = PAD ? PP : (BM * BN + CAPF - 1) / CAPF;
   constexpr int SLAB = BM / P;
   constexpr int C4 = BN / 4;
   constexpr int ITERS = SLAB * C4 / NT;
@@ -188,7 +198,7 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
   const bool vec_ok = ((g.N & 3) == 0) && ((g.ldc & 3) == 0);
-  float* ct = lds;  // [SLAB][BN] row-major
+  float* ct = lds;  // [SLAB][CS] row-major
   // The bias columns, loaded before any store: a load issued after a store
   // may alias it, so the compiler waits vmcnt(0) for it — and vmcnt counts
   // stores too — turning every row chunk into a store round trip (32 per
@@ -238,7 +248,7 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
           for (int r = 0; r < 16; ++r) {
             const int row = wm * WTM + acc_row<MF16>(i, r, lane) - p * SLAB;
             const int col = wn * WTN + acc_col<MF16>(j, r, lane);
-            ct[row * BN + col] = acc[i][j][r];
+            ct[row * CS + col] = acc[i][j][r];
           }
     }
     __syncthreads();
@@ -267,13 +277,13 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) asm volatile("" : "+v"(res[it]));
       }
-      store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, BN, BI>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0, sc_v, am);
+      store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, CS, BI>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0, sc_v, am);
     } else {
       for (int idx = tid; idx < SLAB * C4; idx += NT) {
         const int row = idx / C4, c4 = idx - row * C4;
         const int m = m0 + rbase + row, n = n0 + c4 * 4;
         if (m >= g.M || n >= g.N) continue;
-        const f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * BN + c4 * 4);
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * CS + c4 * 4);
         const long long o = (long long)m * g.ldc + n;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {

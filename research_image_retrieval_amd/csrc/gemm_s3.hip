@@ -174,7 +174,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   static_assert(BK == 16 || BK == 32, "BK");
   // f16x2 at one block per CU: room for the whole fp32 C tile, so the
   // epilogue stages it in one slab (two planes leave the stages smaller)
-  constexpr int LDS_U16 = (SP == 2 && MINB == 1 && BM * BN > BUF) ? 2 * BM * BN : 2 * BUF;
+  // (rows padded by 4 / 8 floats, epilogue_store)
+  constexpr int CT_F = BM * (BN + (MF16 ? 4 : 8));
+  constexpr int LDS_U16 = (SP == 2 && MINB == 1 && CT_F > BUF) ? 2 * CT_F : 2 * BUF;
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
 
   // the A operand's split scale (f16x2): its max-|x| record is loaded first,
@@ -680,8 +682,10 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
   constexpr int WM = 2, FM = 2, FN = 2, BK = 32, NT = 512, NW = 8;
   constexpr int WTM = 64, WTN = 64, BM = 128, BN = 256, SL = BK / 8;
   constexpr int A_EL = NP * BM * BK, BUF = A_EL + NP * BN * BK;
-  // stage stride: a stage also stages one 64-row slab of C (64 KB) in the epilogue
-  constexpr int STG = BUF > 64 * BN * 2 ? BUF : 64 * BN * 2;
+  // stage stride: a stage also stages one 64-row slab of C in the epilogue
+  // (rows padded by 4 floats: the 16x16 accumulator writes hit distinct banks)
+  constexpr int CS = BN + 4;
+  constexpr int STG = BUF > 64 * CS * 2 ? BUF : 64 * CS * 2;
   constexpr int B_INS = NP * BN / (64 / SL) / NW;  // LDS-DMA instructions per wave per k-tile (6 / 4)
   constexpr int A_LD = 2;                          // A loads per thread per k-tile
   static_assert(B_INS * NW * (64 / SL) == NP * BN, "B staging must tile the block");
@@ -926,14 +930,14 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
           }
       }
     };
-    float* ct = reinterpret_cast<float*>(lds + buf * STG);  // [2 bands x 32 rows][BN]
+    float* ct = reinterpret_cast<float*>(lds + buf * STG);  // [2 bands x 32 rows][CS]
     const int le = te & 63;
     auto stage = [&](int sl) {
-      float* cw = ct + (wm * 32) * BN + wn * WTN;
+      float* cw = ct + (wm * 32) * CS + wn * WTN;
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) cw[acc_row<true>(0, r, le) * BN + acc_col<true>(j, r, le)] = acc[sl][j][r];
+        for (int r = 0; r < 16; ++r) cw[acc_row<true>(0, r, le) * CS + acc_col<true>(j, r, le)] = acc[sl][j][r];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -947,7 +951,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
       }
 #pragma unroll
       for (int q = 0; q < 2; ++q)
-        store_slab<EPI, 2, HITERS, NT, C4, BN, 1>(g, g.C, ct + q * 32 * BN, bias_v, res[sl][q], te,
+        store_slab<EPI, 2, HITERS, NT, C4, CS, 1>(g, g.C, ct + q * 32 * CS, bias_v, res[sl][q], te,
                                                   m0 + q * 64 + sl * 32, n0, sc_v, am);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every LDS read of the slab done

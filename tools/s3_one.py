@@ -1,5 +1,5 @@
-"""Run one conv shape on the split-bf16 core repeatedly (rocprofv3 counter
-passes).  usage: s3_one.py B H W Cin Cout K stride pad [res] [reps]"""
+"""Run one conv shape on a split core repeatedly (rocprofv3 counter passes).
+usage: s3_one.py B H W Cin Cout K stride pad [res] [reps]   (RR_CORE=h2|s3, default h2)"""
 import os
 import sys
 
@@ -14,18 +14,25 @@ reps = int(sys.argv[10]) if len(sys.argv) > 10 else 20
 dev = torch.device("cuda:0")
 x = torch.relu(torch.randn(b, h, w, cin, device=dev))
 wt = torch.randn(cout, k, k, cin, device=dev) * 0.01
-w3 = ops.split3_bf16(wt)
 bias = torch.randn(cout, device=dev)
 oh, ow = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
 r = torch.randn(b, oh, ow, cout, device=dev) if res else None
+if os.environ.get("RR_CORE", "h2") == "h2":
+    wc = ops.H2Conv(wt)
+    rec = ops.amax_records(2, dev)
+    ops.amax_f32(x, rec[0])
+    run = lambda: ops.conv2d_h2(x, rec[0], wc, bias, s, p, r, True, rec[1])  # noqa: E731
+else:
+    w3 = ops.split3_bf16(wt)
+    run = lambda: ops.conv2d_s3(x, w3, bias, s, p, r, True)  # noqa: E731
 for _ in range(3):
-    ops.conv2d_s3(x, w3, bias, s, p, r, True)
+    run()
 torch.cuda.synchronize()
 st = torch.cuda.Event(enable_timing=True)
 en = torch.cuda.Event(enable_timing=True)
 st.record()
 for _ in range(reps):
-    ops.conv2d_s3(x, w3, bias, s, p, r, True)
+    run()
 en.record()
 torch.cuda.synchronize()
 ms = st.elapsed_time(en) / reps

@@ -98,6 +98,7 @@ def main(src, tag):
             traffic[c] = {"kernels": [r["kernel"] for r in rs], "hbm_read_bytes_per_launch": rb, "hbm_write_bytes_per_launch": wb,
                           "hbm_bytes_per_launch": rb + wb, "source": f"profiles/{tag}_kernel_summary.json"}
     traffic["workload"] = os.environ.get("RR_PROFILE_WORKLOAD", "c3")
+    traffic["conv_math"] = os.environ.get("RR_PROFILE_CONV_MATH", "h2")  # bench.py's default --conv-math
     traffic["batch"] = int(os.environ.get("RR_PROFILE_BATCH", "1280"))  # bench.py's default --batch
     with open(os.path.join(dst, "traffic.json"), "w") as f:
         json.dump(traffic, f, indent=1)
