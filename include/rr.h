@@ -84,7 +84,7 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     otherwise as 3), 6 (bf16 filter sweeps with K % 64 == 0:
  *                     gallery rows in VGPRs, query panel in LDS, sweep_v.hip;
  *                     otherwise the pick)
- *   RR_TUNE_S3_CFG:   split cores (bf16x3 and f16x2), 1..8 (gemm_s3.hip tile table)
+ *   RR_TUNE_S3_CFG:   split cores (bf16x3 and f16x2), 1..9 (gemm_s3.hip tile table)
  *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of
  *                     ~1 us for every other resident block (-1 = the library's pick)
  * Any other key or value: RR_EINVAL. */

@@ -146,14 +146,58 @@ __device__ __forceinline__ void s3_load1x2(const f32x4* p0, const f32x4* p1, f32
 // a fresh definition of v after the preceding (volatile) wait: nothing that
 // reads v can be scheduled above it
 __device__ __forceinline__ void s3_launder(f32x4& v) { asm volatile("" : "+v"(v)); }
+// a fresh, opaque copy of v: address math built from it cannot be folded or
+// hoisted (see its uses)
+__device__ __forceinline__ int s3_opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
+// Diagnostic build only (-DRR_S3_PHASES=1, tools/phase_build.sh): per-wave
+// s_memtime deltas of the k-loop phases of the f16x2 kernels, summed over
+// every wave into s3_phase_sum[kernel][phase] (rr_debug_phases reads them).
+// Phases: 0 issue loads, 1 first MFMA part, 2 mid wait, 3 split + second
+// MFMA part, 4 end wait, 5 barrier, 6 epilogue, 7 prologue.  The timers cost
+// a few % and are compiled out of the product library.
+#ifndef RR_S3_PHASES
+#define RR_S3_PHASES 0
+#endif
+#if RR_S3_PHASES
+__device__ unsigned long long s3_phase_sum[2][8];
+struct S3Phases {
+  unsigned long long t, acc[8];
+  __device__ __forceinline__ S3Phases() {
+    t = __builtin_amdgcn_s_memtime();
+    for (int i = 0; i < 8; ++i) acc[i] = 0;
+  }
+  __device__ __forceinline__ void mark(int i) {
+    const unsigned long long n = __builtin_amdgcn_s_memtime();
+    acc[i] += n - t;
+    t = n;
+  }
+  __device__ __forceinline__ void flush(int kernel) {
+    if ((threadIdx.x & 63) == 0)
+      for (int i = 0; i < 8; ++i) atomicAdd(&s3_phase_sum[kernel][i], acc[i]);
+  }
+};
+#define RR_PH_DECL S3Phases ph_;
+#define RR_PH(i) ph_.mark(i)
+#define RR_PH_FLUSH(k) ph_.flush(k)
+#else
+#define RR_PH_DECL
+#define RR_PH(i) ((void)0)
+#define RR_PH_FLUSH(k) ((void)0)
+#endif
 
 // MF16 (BK = 32): each 32x32 tile is four v_mfma_f32_16x16x32_bf16
 // tiles (one 32-deep k-step per k-tile instead of two 16-deep ones; the
 // 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
 // 'DVFS give-back' item 7).  The k-tile's MFMAs go in two parts around the A
 // split: a0b0 + a1b1 + a0b1 + a1b0 (planes 0-1), then a0b2 + a2b0 (plane 2).
-template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0, int EPI = -1, int SP = 3>
+template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0, int EPI = -1, int SP = 3,
+          int NSTG = 2>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
+  static_assert(NSTG == 2 || (NSTG == 3 && MF16 && SP == 2), "three LDS stages: the f16x2 16x16x32 tile");
   static_assert(!MF16 || BK == 32, "MF16: BK 32");
   static_assert(SP == 2 || SP == 3, "split kind");
   static_assert(SP == 3 || (EPI >= 0 && (EPI & EP_SCALE)), "f16x2: scaled epilogue");
@@ -176,7 +220,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   // epilogue stages it in one slab (two planes leave the stages smaller)
   // (rows padded by 4 / 8 floats, epilogue_store)
   constexpr int CT_F = BM * (BN + (MF16 ? 4 : 8));
-  constexpr int LDS_U16 = (SP == 2 && MINB == 1 && CT_F > BUF) ? 2 * CT_F : 2 * BUF;
+  constexpr int LDS_U16 = (SP == 2 && MINB == 1 && 2 * CT_F > NSTG * BUF) ? 2 * CT_F : NSTG * BUF;
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
 
   // the A operand's split scale (f16x2): its max-|x| record is loaded first,
@@ -431,7 +475,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   // plane p fragments of one 32-deep k-tile: lane group lg holds k = 8lg..8lg+7
   // (16-B slot lg) of row l16 of each 16-row half
   auto rd_mf = [&](int cur, int p) {
-    const uint16_t* la = lds + cur * BUF;
+    // three stages: the stage offset (up to 96 KB) does not fit the 16-bit
+    // ds_read offset, so each stage would need its own address registers;
+    // an opaque per-call base keeps one set
+    const uint16_t* la = lds + (NSTG == 3 ? s3_opaque(cur * BUF) : cur * BUF);
     const uint16_t* lb = la + A_EL;
 #pragma unroll
     for (int i = 0; i < FM; ++i)
@@ -512,10 +559,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
           }
     }
   };
-  auto mf_rest = [&](int cur, int nxt) {
+  // rbn: the register buffer holding the next A k-tile; stn: the stage it goes to
+  auto mf_rest = [&](int cur, int rbn, int stn) {
     if constexpr (MF16) {
-      split_a(nxt);
-      write_a(nxt);  // the other stage is free since the last barrier
+      split_a(rbn);
+      write_a(stn);  // that stage is free since the last barrier
       // f16x2: the conv A loader's state leaves no room to hold the plane-0
       // fragments across the split (2 registers spilled): re-read them
       if constexpr (SP == 2 && (MF_REREAD || AMODE != A_DENSE)) rd_mf(cur, 0);
@@ -572,59 +620,113 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         s3_launder(ra2[rb][i][1]);
       }
     };
-    load_a(0, 0);
-    glds_b(0, 0);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_INS) : "memory");  // A(0) landed
-    launder_a(0);
-    if constexpr (SP == 2) {
-      // uniform: the exponent and both powers of two stay in scalar registers
-      const int e = __builtin_amdgcn_readfirstlane(h2_exp(amax_reduce(a_amax_w)));
-      a_sc = __int_as_float((127 + e) << 23);
-      a_isc = __int_as_float((127 - e) << 23);
-    }
-    store_a(0, 0);
-    load_a(nk > 1 ? 1 : 0, 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B(0) landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    auto iter = [&](int kt, int cur) __attribute__((always_inline)) {
-      glds_b(min(kt + 1, nk - 1), cur ^ 1);
-      load_a(min(kt + 2, nk - 1), cur);
-      if constexpr (MF16 && AMODE == A_DENSE && SP == 3) {
-        mf_dense0(cur);
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
-        launder_a(cur ^ 1);
-        split_a(cur ^ 1);
-        mf_dense1(cur);
-        write_a(cur ^ 1);
-      } else if constexpr (MF16) {
-        mf_lo1(cur);
-        // A(kt+1) landed (the B DMA of kt+1 and the A loads of kt+2 may not
-        // have): split and stored among the remaining MFMAs of tile kt
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
-        launder_a(cur ^ 1);
-        mf_rest(cur, cur ^ 1);
-      } else {
-        compute_st(cur, 0);
-        // A(kt+1) landed: its split overlaps the remaining MFMAs of tile kt
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
-        launder_a(cur ^ 1);
-        split_a(cur ^ 1);
+    if constexpr (NSTG == 3) {
+      // Three LDS stages (config 9): the B DMA of k-tile kt+2 and the A
+      // loads of kt+2 go out at the start of iteration kt, so B has two
+      // iterations to land instead of one; A(kt+1) is split into stage
+      // (kt+1) % 3 among the MFMAs as before.  Its counted wait also covers
+      // B(kt+1) (issued before it), so the iteration ends on the barrier
+      // alone.  Unrolled by six: stage (kt % 3) and register buffer (kt % 2)
+      // indices are constants.
+      load_a(0, 0);
+      glds_b(0, 0);
+      glds_b(nk > 1 ? 1 : 0, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * B_INS) : "memory");  // A(0) landed
+      launder_a(0);
+      {
+        const int e = __builtin_amdgcn_readfirstlane(h2_exp(amax_reduce(a_amax_w)));
+        a_sc = __int_as_float((127 + e) << 23);
+        a_isc = __int_as_float((127 - e) << 23);
       }
-      if constexpr (!MF16) {
-#pragma unroll
-        for (int st = 1; st < BK / 16; ++st) compute_st(cur, st);
-        write_a(cur ^ 1);
-      }
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of kt+1 landed
+      store_a(0, 0);
+      load_a(nk > 1 ? 1 : 0, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // B(0) landed
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
-    };
-    for (int kt = 0; kt < nk; kt += 2) {
-      iter(kt, 0);
-      if (kt + 1 < nk) iter(kt + 1, 1);
+      auto iter3 = [&](int kt, int cur, int rb) __attribute__((always_inline)) {
+        glds_b(min(kt + 2, nk - 1), (cur + 2) % 3);
+        load_a(min(kt + 2, nk - 1), rb);
+        mf_lo1(cur);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(kt+1), B(kt+1) landed
+        launder_a(rb ^ 1);
+        mf_rest(cur, rb ^ 1, (cur + 1) % 3);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      };
+      for (int kt = 0; kt < nk; kt += 6) {
+        iter3(kt, 0, 0);
+        if (kt + 1 < nk) iter3(kt + 1, 1, 1);
+        if (kt + 2 < nk) iter3(kt + 2, 2, 0);
+        if (kt + 3 < nk) iter3(kt + 3, 0, 1);
+        if (kt + 4 < nk) iter3(kt + 4, 1, 0);
+        if (kt + 5 < nk) iter3(kt + 5, 2, 1);
+      }
+    } else {
+      RR_PH_DECL
+      load_a(0, 0);
+      glds_b(0, 0);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_INS) : "memory");  // A(0) landed
+      launder_a(0);
+      if constexpr (SP == 2) {
+        // uniform: the exponent and both powers of two stay in scalar registers
+        const int e = __builtin_amdgcn_readfirstlane(h2_exp(amax_reduce(a_amax_w)));
+        a_sc = __int_as_float((127 + e) << 23);
+        a_isc = __int_as_float((127 - e) << 23);
+      }
+      store_a(0, 0);
+      load_a(nk > 1 ? 1 : 0, 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B(0) landed
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      auto iter = [&](int kt, int cur) __attribute__((always_inline)) {
+        glds_b(min(kt + 1, nk - 1), cur ^ 1);
+        load_a(min(kt + 2, nk - 1), cur);
+        if constexpr (MF16 && AMODE == A_DENSE && SP == 3) {
+          mf_dense0(cur);
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
+          launder_a(cur ^ 1);
+          split_a(cur ^ 1);
+          mf_dense1(cur);
+          write_a(cur ^ 1);
+        } else if constexpr (MF16) {
+          RR_PH(0);
+          mf_lo1(cur);
+          RR_PH(1);
+          // A(kt+1) landed (the B DMA of kt+1 and the A loads of kt+2 may not
+          // have): split and stored among the remaining MFMAs of tile kt
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
+          launder_a(cur ^ 1);
+          RR_PH(2);
+          mf_rest(cur, cur ^ 1, cur ^ 1);
+          RR_PH(3);
+        } else {
+          compute_st(cur, 0);
+          // A(kt+1) landed: its split overlaps the remaining MFMAs of tile kt
+          asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
+          launder_a(cur ^ 1);
+          split_a(cur ^ 1);
+        }
+        if constexpr (!MF16) {
+  #pragma unroll
+          for (int st = 1; st < BK / 16; ++st) compute_st(cur, st);
+          write_a(cur ^ 1);
+        }
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of kt+1 landed
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        RR_PH(4);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+        RR_PH(5);
+      };
+      RR_PH(7);
+      for (int kt = 0; kt < nk; kt += 2) {
+        iter(kt, 0);
+        if (kt + 1 < nk) iter(kt + 1, 1);
+      }
+      if constexpr (SP == 2 && MF16) RR_PH_FLUSH(0);
     }
     // the clamped tail loads are still in flight: keep both buffers live
     // until they have landed, so no later value is allocated to them
@@ -665,13 +767,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 // 64-row slabs of 64 KB), with every bias / residual load issued before the
 // staging.  Same per-accumulator k order and epilogue arithmetic as config 4:
 // the results are bit-identical to it.
-// a fresh, opaque copy of v: per-thread address math built from it inside a
-// tile loop's epilogue / loader switch cannot be hoisted out of the loop (its
-// results would then be live through the whole k-loop and spill it)
-__device__ __forceinline__ int s3_opaque(int v) {
-  asm volatile("" : "+v"(v));
-  return v;
-}
+// (s3_opaque: per-thread address math built from it inside a tile loop's
+// epilogue / loader switch cannot be hoisted out of the loop -- its results
+// would then be live through the whole k-loop and spill it)
 
 template <int EPI, int SP = 3, int SEG2 = 0>
 __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_n, int ntiles) {
@@ -913,10 +1011,21 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
     const int te = s3_opaque(tid);
     const int c40 = te % C4, r0 = te / C4;
     f32x4 bias_v[1] = {f32x4{0.f, 0.f, 0.f, 0.f}}, sc_v[1];
-    if ((EPI & EP_BIAS) && g.bias != nullptr) bias_v[0] = *reinterpret_cast<const f32x4*>(g.bias + n0 + c40 * 4);
-    if constexpr ((EPI & EP_SCALE) != 0) sc_v[0] = *reinterpret_cast<const f32x4*>(g.col_scale + n0 + c40 * 4) * a_isc;
-    asm volatile("" : "+v"(bias_v[0]));
-    if constexpr ((EPI & EP_SCALE) != 0) asm volatile("" : "+v"(sc_v[0]));
+    // the bias / column scales load after slab 0's residual rows go out and
+    // are waited for (redefined by an empty asm) only after slab 0 is staged:
+    // waited for up front, as before, they cost a full memory round trip (a
+    // vmcnt(0), the next tile's prefetch included) ahead of the residual loads
+    auto load_bias = [&]() {
+      if ((EPI & EP_BIAS) && g.bias != nullptr) bias_v[0] = *reinterpret_cast<const f32x4*>(g.bias + n0 + c40 * 4);
+      if constexpr ((EPI & EP_SCALE) != 0) sc_v[0] = *reinterpret_cast<const f32x4*>(g.col_scale + n0 + c40 * 4);
+    };
+    auto launder_bias = [&]() {
+      asm volatile("" : "+v"(bias_v[0]));
+      if constexpr ((EPI & EP_SCALE) != 0) {
+        asm volatile("" : "+v"(sc_v[0]));
+        sc_v[0] *= a_isc;
+      }
+    };
     f32x4 res[2][2][HITERS];  // [slab][band][row chunk]
     auto load_res = [&](int sl) {
       if constexpr ((EPI & EP_RES) != 0) {
@@ -958,9 +1067,11 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
       asm volatile("" ::: "memory");
     };
     load_res(0);
+    load_bias();
     stage(0);
     load_res(1);
     if constexpr ((EPI & EP_RES) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    launder_bias();
     store(0);
     stage(1);
     store(1);  // its barrier also frees `buf` for the next k-tiles
@@ -986,6 +1097,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
   int c_kt = 0, c_tl = 0;
+  RR_PH_DECL
   // iteration j (stage cur = j & 1 holds k-tile j, register buffer cur ^ 1
   // holds A(j+1)): B DMA of j+1, A loads of j+2, the k-tile's MFMAs with the
   // split of A(j+1) among them (the dense-A order of config 4), then — after
@@ -997,6 +1109,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
   auto iter = [&](int cur) __attribute__((always_inline)) {
     glds_b(cur ^ 1);
     load_a(cur);
+    RR_PH(0);
     rd_mf(cur, 0);
     rd_mf(cur, 1);
     if constexpr (SP == 3) {
@@ -1011,8 +1124,10 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
       // f16x2: the plane-1 products, then a0b0 with the split of A(j+1) two
       // VALU per MFMA gap (same per-accumulator order as config 4)
       mf_lo1();
+      RR_PH(1);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
       launder_a(cur ^ 1);
+      RR_PH(2);
       split_a(cur ^ 1);
       mf_hi();
 #pragma unroll
@@ -1022,15 +1137,20 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
       }
     }
     write_a(cur ^ 1);
+    RR_PH(3);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of j+1 landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    RR_PH(4);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    RR_PH(5);
     if (++c_kt == nk) {
       c_kt = 0;
       epilogue(c_tl++, cur);
+      RR_PH(6);
     }
   };
+  RR_PH(7);
   for (int j = 0; j < J; j += 2) {
     iter(0);
     if (j + 1 < J) iter(1);
@@ -1043,6 +1163,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
   if constexpr ((EPI & EP_AMAX) != 0) {
     if (g.c_amax != nullptr) amax_publish(g.c_amax, am, bid * NW + wave);
   }
+  if constexpr (SP == 2) RR_PH_FLUSH(1);
 }
 
 template <int EPI, int SP = 3, int SEG2 = 0>
@@ -1095,7 +1216,8 @@ static hipError_t launch_s3p(const GemmArgs& g, hipStream_t s, int n_cu, int st)
   }
 }
 
-template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int EPI = -1, int SP = 3>
+template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int EPI = -1, int SP = 3,
+          int NSTG = 2>
 static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
@@ -1106,7 +1228,7 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
   constexpr int PER_CU = (MINB * 4) / (WM * WN) > 1 ? (MINB * 4) / (WM * WN) : 1;
   g.stagger_blocks = n_cu * PER_CU;
   g.stagger_sleeps = nblk > 2LL * n_cu * PER_CU ? stagger : 0;  // only grids of several rounds
-  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16, EPI, SP>), dim3((unsigned)nblk),
+  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16, EPI, SP, NSTG>), dim3((unsigned)nblk),
                      dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
@@ -1124,6 +1246,8 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //      stem 2-7 % faster than 6, profiles/r02f_s3_cfg7.txt)
 //   8: config 4 as a persistent k-stream (gemm_s3p_kernel): dense A, N % 256
 //      == 0 — the picked tile for the 1x1 layers it serves
+//   9: config 4 with three LDS stages (f16x2 only, 144 KB): the B DMA two
+//      k-tiles ahead
 // (all others on v_mfma_f32_32x32x16_{bf16,f16}).  The f16x2 split is built
 // for the picked configs 3, 4, 7 and 8 (a forced 1, 2, 5 or 6 runs the pick).
 // Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the fastest
@@ -1152,6 +1276,7 @@ static int pick_s3(const GemmArgs& g, int forced) {
 }
 // f16x2: config 1 (no f16x2 build) -> 3 where it tiles no worse than 7
 static int pick_h2(const GemmArgs& g, int forced) {
+  if (forced == 9) return (g.N % 256) == 0 ? 9 : pick_h2(g, 0);
   int cfg = pick_s3(g, forced);
   if (cfg == 3 || cfg == 4 || cfg == 7 || cfg == 8) return cfg;
   cfg = pick_s3(g, 0);
@@ -1162,15 +1287,15 @@ static int pick_h2(const GemmArgs& g, int forced) {
 // The picked configs (3, 4, 7) with the ResNet's epilogues compiled in:
 // conv + BN + ReLU, + residual + ReLU, projection conv + BN (f16x2: the four
 // residual / ReLU combinations of H2_EP).
-template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int SP = 3>
+template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int SP = 3, int NSTG = 2>
 static hipError_t launch_s3_ep(const GemmArgs& g, hipStream_t s, int n_cu, int st) {
   if constexpr (SP == 2) {
     switch (ep_flags(g) & (EP_RES | EP_RELU)) {
-      case EP_RELU: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RELU, 2>(g, s, n_cu, st);
+      case EP_RELU: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RELU, 2, NSTG>(g, s, n_cu, st);
       case EP_RES | EP_RELU:
-        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RES | EP_RELU, 2>(g, s, n_cu, st);
-      case EP_RES: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RES, 2>(g, s, n_cu, st);
-      default: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP, 2>(g, s, n_cu, st);
+        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RES | EP_RELU, 2, NSTG>(g, s, n_cu, st);
+      case EP_RES: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RES, 2, NSTG>(g, s, n_cu, st);
+      default: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP, 2, NSTG>(g, s, n_cu, st);
     }
   } else {
     switch (ep_flags(g)) {
@@ -1219,6 +1344,7 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
   }
   switch (cfg) {
     case 4: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1, 2>(g, s, n_cu, st);
+    case 9: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1, 2, 3>(g, s, n_cu, st);
     case 7: return launch_s3_ep<8, 1, 1, 2, 16, AM, 4, 0, 2>(g, s, n_cu, st);
     default: return launch_s3_ep<4, 2, 2, 2, 32, AM, 1, 0, 2>(g, s, n_cu, st);
   }
@@ -1364,4 +1490,17 @@ int launch_amax(rr_handle_s* h, const float* x, long long n, uint32_t* slots, hi
   return check_hip(h, hipGetLastError(), "amax launch");
 }
 
+#if RR_S3_PHASES
+// diagnostic build: read and clear the phase sums ([2][8] cycles)
+int debug_phases(unsigned long long* out) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(s3_phase_sum), sizeof(s3_phase_sum)) != hipSuccess) return RR_EHIP;
+  unsigned long long z[2][8] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(s3_phase_sum), z, sizeof(z)) == hipSuccess ? RR_OK : RR_EHIP;
+}
+#endif
+
 }  // namespace rr
+
+#if RR_S3_PHASES
+extern "C" int rr_debug_phases(unsigned long long* out) { return rr::debug_phases(out); }
+#endif

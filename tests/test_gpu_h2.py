@@ -176,7 +176,7 @@ TILE_SHAPES = [  # shapes that reach each f16x2 config's edges: ragged M, N = 64
 ]
 
 
-@pytest.mark.parametrize("cfg", [3, 4, 7, 8])
+@pytest.mark.parametrize("cfg", [3, 4, 7, 8, 9])
 @pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res", TILE_SHAPES)
 def test_conv2d_h2_tile_configs(cuda, cfg, b, h, w, cin, cout, k, s, p, res):
     """Every f16x2 tile config forced on every shape: fp32-grade vs float64
@@ -192,14 +192,21 @@ def test_conv2d_h2_tile_configs(cuda, cfg, b, h, w, cin, cout, k, s, p, res):
 
 
 def test_h2_persistent_tile_bit_identical(cuda):
-    """Config 8 (persistent k-stream) and config 4 keep the same
-    per-accumulator k order and epilogue arithmetic: identical bits."""
+    """Config 8 (persistent k-stream), config 9 (three LDS stages) and config
+    4 keep the same per-accumulator k order and epilogue arithmetic:
+    identical bits (1x1 with residual; 3x3 for config 9)."""
     x, wt, bias, r, _, _ = _conv_case(cuda, 3, 29, 31, 256, 1024, 1, 1, 0, True, seed=5)
     outs = {}
-    for cfg in (4, 8):
+    for cfg in (4, 8, 9):
         with ops.tuning(0, s3_cfg=cfg):
             outs[cfg] = _run_h2(cuda, x, wt, bias, r, 1, 0)[0].cpu()
-    assert torch.equal(outs[4], outs[8])
+    assert torch.equal(outs[4], outs[8]) and torch.equal(outs[4], outs[9])
+    x, wt, bias, r, _, _ = _conv_case(cuda, 2, 15, 13, 256, 256, 3, 1, 1, False, seed=6)
+    y9 = {}
+    for cfg in (4, 9):
+        with ops.tuning(0, s3_cfg=cfg):
+            y9[cfg] = _run_h2(cuda, x, wt, bias, None, 1, 1)[0].cpu()
+    assert torch.equal(y9[4], y9[9])
 
 
 def test_conv2d_h2_nonfinite_inputs(cuda):
