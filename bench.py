@@ -690,19 +690,23 @@ def main():
         flop_seed *= 2
     else:
         conv_flops_img = sum(W.resnet_conv_flops(a.arch, 224, 224).values()) + 2 * 2 * 2048 * 2048  # + whiten, PCA-w
-    conv_bytes_step, conv_floor_ms = None, None
+    conv_bytes_step, conv_floor_ms, floor_parts = None, None, None
     if a.workload in ("c3", "c5"):
         # per-layer algorithmic bytes (weights.resnet_conv_bytes) and the layer-wise
         # roofline floor sum_l max(FLOP_l / peak, bytes_l / HBM peak) of the conv class
         pk = PEAK_TFLOPS[a.conv_math if a.conv_math in SPLIT_MATH else "fp32"] * 1e12
         conv_bytes_step, floor = 0.0, 0.0
+        floor_parts = {"mfma": 0.0, "hbm": 0.0}  # the floor's time in MFMA-bound / HBM-bound layers
         for sc in (scales if a.workload == "c5" else (1.0,)):
             hh = int(224.0 * sc)
             fl_l = W.resnet_conv_flops(a.arch, hh, hh)
-            by_l = W.resnet_conv_bytes(a.arch, hh, hh, a.batch, weight_bytes=WEIGHT_BYTES[a.conv_math])
+            by_l = W.resnet_conv_bytes(a.arch, hh, hh, a.batch, weight_bytes=WEIGHT_BYTES[a.conv_math],
+                                       fused=a.conv_math == "h2")
             for name in fl_l:
                 conv_bytes_step += by_l[name]
-                floor += max(fl_l[name] * a.batch / pk, by_l[name] / (PEAK_HBM_GBS * 1e9))
+                t_f, t_b = fl_l[name] * a.batch / pk, by_l[name] / (PEAK_HBM_GBS * 1e9)
+                floor += max(t_f, t_b)
+                floor_parts["mfma" if t_f >= t_b else "hbm"] += max(t_f, t_b)
             lin_by = 2 * (2 * a.batch * 2048 * 4 + 2048 * 2048 * 4)  # whiten + PCA-w (exact-fp32 core)
             conv_bytes_step += lin_by
             floor += max(2 * 2 * 2048 * 2048 * a.batch / (PEAK_TFLOPS["fp32"] * 1e12), lin_by / (PEAK_HBM_GBS * 1e9))
@@ -736,7 +740,13 @@ def main():
         peak = PEAK_TFLOPS[dt]
         t_mfma = fl_step / (peak * 1e12)
         t_hbm = by_step / (PEAK_HBM_GBS * 1e9) if by_step else 0.0
-        if t_hbm > t_mfma:
+        if name == "conv_gemm" and floor_parts is not None:
+            # a class of layers with their own bounds: the bound of the layers that
+            # hold most of its roofline floor (not of the class's summed bytes vs FLOPs)
+            hbm_bound = floor_parts["hbm"] > floor_parts["mfma"]
+        else:
+            hbm_bound = t_hbm > t_mfma
+        if hbm_bound:
             ach = by_step / sec / 1e9
             e = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
                  "frac": round(ach / PEAK_HBM_GBS, 4)}
@@ -761,6 +771,7 @@ def main():
         if name == "conv_gemm" and conv_floor_ms is not None:
             e["layer_roofline_floor_ms_per_step"] = round(conv_floor_ms, 3)
             e["frac_of_layer_floor"] = round(conv_floor_ms / (ms / a.steps), 4)
+            e["layer_floor_split_ms"] = {k: round(v * 1e3, 3) for k, v in floor_parts.items()}
         rk[name] = e
     for name in ("select", "elementwise"):
         ms, n = cls[name]

@@ -47,8 +47,8 @@ typedef struct rr_handle_s* rr_handle_t;
 /* ABI revision of this header.  Bumped when an existing entry changes its
  * arguments under the same name (a caller built against an older header would
  * pass shifted arguments): 2 = rr_alpha_qe gained n_rows (round 2); 3 = the
- * f16x2 entries rr_conv2d_h2 / rr_bottleneck_out_h2 / rr_split2_f16 /
- * rr_amax_f32 were added (no existing entry changed).  Bindings compare
+ * f16x2 entries rr_conv2d_h2 / rr_bottleneck_out_h2 / rr_stem_pool_h2 /
+ * rr_split2_f16 / rr_amax_f32 were added (no existing entry changed).  Bindings compare
  * rr_abi_version() with the RR_ABI_VERSION they were written against.     */
 #define RR_ABI_VERSION 3
 int rr_abi_version(void);
@@ -336,6 +336,23 @@ int rr_bottleneck_out_h2(rr_handle_t h, const float* y, const unsigned* y_amax,
                          int stride, const void* w2, const float* w_iscale,
                          const float* bias, int cout, float* out,
                          unsigned* out_amax, void* stream);
+
+/* The ResNet stem on the f16x2 core with its max-pool fused: NHWC4 conv
+ * (cin == 4, as rr_conv2d_h2) + bias + ReLU, then the 3x3 stride-2 padding-1
+ * max-pool, written only pooled: y_pool [b][ph][pw][64] with
+ * ph = (oh - 1) / 2 + 1, pw likewise (oh, ow the conv's output size).  Each
+ * tile computes a 17 x 15 patch of conv outputs and pools its 8 x 7 windows
+ * from LDS: the stem's 112 x 112 x 64 map never reaches HBM.  The max is taken
+ * over the raw accumulators and scaled once (scale > 0, bias add and ReLU are
+ * monotone): the same bits as rr_conv2d_h2 followed by the max-pool, for
+ * finite inputs.  y_amax (optional, zeroed): max |y_pool|, which equals the
+ * conv output's (every conv output lies in some window).  cout == 64.
+ * Replaces networks/backbone.py:103-109's conv1 / bn1 / relu / maxpool.     */
+int rr_stem_pool_h2(rr_handle_t h, const float* x, const unsigned* x_amax,
+                    int b, int hgt, int wid, const void* w2,
+                    const float* w_iscale, const float* bias, int cout, int kh,
+                    int kw, int stride, int pad, float* y_pool,
+                    unsigned* y_amax, void* stream);
 
 /* fp16 2-way split of the rows of w [rows][k] (done once per weight tensor):
  * row n is scaled by 2^e_n, its max |w| then in [2^14, 2^15), and split into

@@ -62,6 +62,7 @@ SIGNATURES = {
     "rr_split3_bf16": (_i, [_vp, _vp, _ll, _vp, _vp]),
     "rr_conv2d_h2": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp]),
     "rr_split2_f16": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
+    "rr_stem_pool_h2": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
     "rr_bottleneck_out_h2": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _vp,
                                   _vp, _vp]),
     "rr_amax_f32": (_i, [_vp, _vp, _ll, _vp, _vp]),

@@ -143,7 +143,7 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.lp_cfg = value;
       return RR_OK;
     case RR_TUNE_S3_CFG:
-      if (value < 0 || value > 9) break;
+      if (value < 0 || value > 10) break;
       h->tune.s3_cfg = value;
       return RR_OK;
     case RR_TUNE_S3_STAGGER:
@@ -494,6 +494,53 @@ int rr_conv2d_h2(rr_handle_t h, const float* x, const unsigned* x_amax, int b, i
   const bool dense = kh == 1 && kw == 1 && stride == 1 && pad == 0 && cin != 4;
   if (dense) g.lda = cin;
   return launch_gemm_s3(h, dense ? A_DENSE : (cin == 4 ? A_CONV_C4 : A_CONV), g, (hipStream_t)stream, kTimeGemm, 2);
+}
+
+int rr_stem_pool_h2(rr_handle_t h, const float* x, const unsigned* x_amax, int b, int hgt, int wid, const void* w2,
+                    const float* w_iscale, const float* bias, int cout, int kh, int kw, int stride, int pad,
+                    float* y_pool, unsigned* y_amax, void* stream) {
+  RR_ENTRY(h);
+  if (!x || !x_amax || !w2 || !w_iscale || !y_pool || b < 0 || hgt <= 0 || wid <= 0 || kh <= 0 || kw <= 0 ||
+      stride <= 0 || pad < 0)
+    return set_error(h, RR_EINVAL, "rr_stem_pool_h2: bad argument");
+  if (cout != 64) return set_error(h, RR_EINVAL, "rr_stem_pool_h2: cout must be 64");
+  const int oh = (hgt + 2 * pad - kh) / stride + 1, ow = (wid + 2 * pad - kw) / stride + 1;
+  if (oh <= 0 || ow <= 0) return set_error(h, RR_EINVAL, "rr_stem_pool_h2: empty output");
+  const int ph = (oh - 1) / 2 + 1, pw = (ow - 1) / 2 + 1;  // 3x3 / 2, padding 1
+  if ((long long)b * oh * ow > 0x7fffffffLL || (long long)b * ph * pw * cout > (1LL << 40))
+    return set_error(h, RR_EINVAL, "rr_stem_pool_h2: too many output pixels");
+  if (((uintptr_t)x & 15) || ((uintptr_t)w2 & 15) || ((uintptr_t)w_iscale & 15) || ((uintptr_t)y_pool & 15) ||
+      (bias && ((uintptr_t)bias & 15)))
+    return set_error(h, RR_EINVAL, "rr_stem_pool_h2: x/w2/w_iscale/bias/y_pool must be 16-byte aligned");
+  GemmArgs g;
+  g.A = x;
+  g.M = (int)((long long)b * oh * ow);
+  g.K = (kh * kw * 4 + 31) / 32 * 32;  // NHWC4 planes zero-padded to a multiple of 32
+  g.H = hgt;
+  g.W = wid;
+  g.Cin = 4;
+  g.OH = oh;
+  g.OW = ow;
+  g.KH = kh;
+  g.KW = kw;
+  g.stride = stride;
+  g.pad = pad;
+  g.B = reinterpret_cast<const float*>(w2);
+  g.ldb = g.K;
+  g.b_plane = (long long)cout * g.K;
+  g.N = cout;
+  g.ldc = cout;
+  g.bias = bias;
+  g.relu = 1;
+  g.col_scale = w_iscale;
+  g.a_amax = x_amax;
+  g.c_amax = y_amax;
+  g.pool_out = y_pool;
+  g.POH = ph;
+  g.POW = pw;
+  g.pool_tr = (ph + 7) / 8;
+  g.pool_tc = (pw + 6) / 7;
+  return launch_stem_pool_h2(h, g, (hipStream_t)stream, kTimeGemm);
 }
 
 int rr_bottleneck_out_h2(rr_handle_t h, const float* y, const unsigned* y_amax, int b, int oh, int ow, int planes,

@@ -212,6 +212,12 @@ struct GemmArgs {
   long long lda2 = 0;
   int K1 = 0, H2 = 0, W2 = 0, s2 = 1;
   const uint32_t* a2_amax = nullptr;
+  // stem conv + 3x3/2 pad-1 max-pool (gemm_s3_kernel POOL; rr_stem_pool_h2):
+  // tile t = (image, pr, pc) covers the 17 x 15 conv outputs from
+  // (16 pr - 1, 14 pc - 1), whose windows give pooled rows 8 pr .. +7 and
+  // columns 7 pc .. +6 of the POH x POW pooled map pool_out (NHWC, N channels)
+  float* pool_out = nullptr;
+  int POH = 0, POW = 0, pool_tr = 0, pool_tc = 0;
 };
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,
@@ -224,6 +230,8 @@ int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStre
 int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls, int sp = 3);
 // f16x2 two-segment GEMM (GemmArgs A2 / K1): the persistent tile, N % 256 == 0
 int launch_gemm_h2_seg2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int timer_cls);
+// f16x2 NHWC4 stem conv + ReLU + 3x3/2 pad-1 max-pool (GemmArgs pool_*), N == 64
+int launch_stem_pool_h2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int timer_cls);
 // fp16 2-way split of the rows of w [rows][k] into planes [2][rows][kpad]
 // (zero-padded) at a per-row power-of-two scale, iscale[row] = its inverse
 int launch_split2h(rr_handle_s* h, const float* w, int rows, int k, int kpad, uint16_t* planes, float* iscale,

@@ -66,6 +66,8 @@ class ResNet:
             self.convs_h2 = {k: ops.H2Conv(w) for k, (w, _) in self.convs.items()}
             # each stage's first block: conv3 + downsample as one GEMM (ops.H2Bottleneck)
             self.fuse_downsample = True
+            # the stem conv + ReLU + max-pool as one launch (ops.stem_pool_h2)
+            self.fuse_stem_pool = True
             self.bneck_h2 = {}
             for li in range(len(self.layers)):
                 p = f"layer{li + 1}.0"
@@ -86,14 +88,19 @@ class ResNet:
         """The trunk on the f16x2 core: every conv reads its input's max-|x|
         record and writes its output's (one zeroed [2 + 3 blocks, 64] tensor per
         forward); the max-pool output reuses the stem's record (every stem
-        output lies in some 3x3/2 window, so the max is the same).  A stage's
+        output lies in some 3x3/2 window, so the max is the same); the stem,
+        its ReLU and the max-pool run as one launch (ops.stem_pool_h2), so the
+        stem's full-resolution map never reaches HBM.  A stage's
         first block runs conv3 and its downsample projection as one GEMM
         (ops.bottleneck_out_h2), so the projected identity never reaches HBM."""
         cv, h2 = self.convs, self.convs_h2
         rec = ops.amax_records(2 + 3 * sum(self.layers), x.device)
         ops.amax_f32(x, rec[0])
-        x = ops.conv2d_h2(x, rec[0], h2["conv1"], cv["conv1"][1], 2, 3, None, True, rec[1])
-        x = ops.maxpool2d(x, 3, 2, 1)
+        if self.fuse_stem_pool and h2["conv1"].cout == 64:
+            x = ops.stem_pool_h2(x, rec[0], h2["conv1"], cv["conv1"][1], 2, 3, rec[1])
+        else:
+            x = ops.conv2d_h2(x, rec[0], h2["conv1"], cv["conv1"][1], 2, 3, None, True, rec[1])
+            x = ops.maxpool2d(x, 3, 2, 1)
         xa, r, x3 = rec[1], 2, None
         for li, nb in enumerate(self.layers):
             for bi in range(nb):

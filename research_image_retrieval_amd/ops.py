@@ -274,6 +274,29 @@ def conv2d_h2(x, x_amax, wc, bias, stride=1, pad=0, residual=None, relu=False, y
     return y
 
 
+def stem_pool_h2(x, x_amax, wc, bias, stride=2, pad=3, y_amax=None):
+    """The NHWC4 stem conv + bias + ReLU with the 3x3/2 padding-1 max-pool
+    fused (rr_stem_pool_h2): [B,H,W,4] -> pooled [B,PH,PW,64], the same bits
+    as conv2d_h2(..., relu=True) followed by maxpool2d for finite inputs."""
+    _f32(x, "stem_pool_h2 x")
+    if not isinstance(wc, H2Conv) or wc.cin != 4 or wc.cout != 64:
+        raise TypeError("stem_pool_h2: wc must be an ops.H2Conv with Cin 4 and Cout 64")
+    dev = _dev(x)
+    b, h, wd, cin = x.shape
+    if cin != 4:
+        raise ValueError("stem_pool_h2: x must be NHWC4")
+    oh = (h + 2 * pad - wc.kh) // stride + 1
+    ow = (wd + 2 * pad - wc.kw) // stride + 1
+    y = torch.empty((b, (oh - 1) // 2 + 1, (ow - 1) // 2 + 1, 64), dtype=torch.float32, device=x.device)
+    if bias is not None:
+        _f32(bias, "stem_pool_h2 bias")
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_stem_pool_h2(hd, _ptr(x), _ptr(x_amax), b, h, wd, _ptr(wc.planes), _ptr(wc.iscale),
+                                          _ptr(bias), 64, wc.kh, wc.kw, stride, pad, _ptr(y), _ptr(y_amax),
+                                          _stream(dev)), hd, "rr_stem_pool_h2")
+    return y
+
+
 class H2Bottleneck:
     """Weights of a stage-entry bottleneck's conv3 + downsample projection as
     one f16x2 GEMM (rr_bottleneck_out_h2): rows [W3 | Wd] split together,

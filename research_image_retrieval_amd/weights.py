@@ -229,20 +229,26 @@ def resnet_conv_flops(arch, h, w, stride_on="3x3"):
     return flops
 
 
-def resnet_conv_bytes(arch, h, w, batch, stride_on="3x3", weight_bytes=6):
+def resnet_conv_bytes(arch, h, w, batch, stride_on="3x3", weight_bytes=6, fused=False):
     """Algorithmic HBM bytes of every trunk conv launch for `batch` h x w
     images (the same layer walk as resnet_conv_flops): the fp32 NHWC input map
     read once (the stem's NHWC4 image: 4 channels), the fp32 output written
     once, the block's fp32 identity read once by the residual conv3, and the
     weights once per launch (`weight_bytes` per parameter: 6 = the split-bf16
-    core's three bf16 planes, 4 = fp32)."""
+    core's three bf16 planes, 4 = fp32 or the f16x2 core's two fp16 planes).
+    fused (the f16x2 trunk, networks.ResNet._forward_h2): the stem writes only
+    its max-pooled map (rr_stem_pool_h2), and a stage's first block computes
+    conv3 and the downsample projection as one GEMM (rr_bottleneck_out_h2),
+    which reads the block input at the sampled pixels and writes no projected
+    identity (its bytes are split between the two names)."""
     def out(x, k, s, p):
         return (x + 2 * p - k) // s + 1
 
     by = {}
     H, Wd = out(h, 7, 2, 3), out(w, 7, 2, 3)
-    by["conv1"] = batch * (h * w * 4 + H * Wd * 64) * 4 + 64 * 7 * 7 * 4 * weight_bytes
-    H, Wd = out(H, 3, 2, 1), out(Wd, 3, 2, 1)
+    Hp, Wp = out(H, 3, 2, 1), out(Wd, 3, 2, 1)
+    by["conv1"] = batch * (h * w * 4 + (Hp * Wp if fused else H * Wd) * 64) * 4 + 64 * 7 * 7 * 4 * weight_bytes
+    H, Wd = Hp, Wp
     inplanes = 64
     for li, nb in enumerate(RESNET_LAYERS[arch]):
         planes = 64 * 2 ** li
@@ -253,11 +259,15 @@ def resnet_conv_bytes(arch, h, w, batch, stride_on="3x3", weight_bytes=6):
             H1, W1 = out(H, 1, s1, 0), out(Wd, 1, s1, 0)
             Ho, Wo = out(H1, 3, s2, 1), out(W1, 3, s2, 1)
             x_in = H * Wd * inplanes
-            if bi == 0:
-                by[p + ".downsample.0"] = batch * (x_in + Ho * Wo * planes * 4) * 4 + planes * 4 * inplanes * weight_bytes
+            wd_by = planes * 4 * inplanes * weight_bytes
+            if bi == 0 and fused:
+                by[p + ".downsample.0"] = batch * Ho * Wo * inplanes * 4 + wd_by
+            elif bi == 0:
+                by[p + ".downsample.0"] = batch * (x_in + Ho * Wo * planes * 4) * 4 + wd_by
             by[p + ".conv1"] = batch * (x_in + H1 * W1 * planes) * 4 + planes * inplanes * weight_bytes
             by[p + ".conv2"] = batch * (H1 * W1 * planes + Ho * Wo * planes) * 4 + planes * planes * 9 * weight_bytes
-            by[p + ".conv3"] = batch * (Ho * Wo * planes + 2 * Ho * Wo * planes * 4) * 4 + \
+            n_res = 0 if (bi == 0 and fused) else 1  # the identity map read by the residual epilogue
+            by[p + ".conv3"] = batch * (Ho * Wo * planes + (1 + n_res) * Ho * Wo * planes * 4) * 4 + \
                 planes * 4 * planes * weight_bytes
             H, Wd, inplanes = Ho, Wo, planes * 4
     return by

@@ -297,3 +297,37 @@ def test_resnet_h2_fused_downsample_matches_unfused(cuda):
     d = (a - b).abs().max().item()
     print("fused vs unfused trunk max|diff|", d, "max|y|", a.abs().max().item())
     assert d < 2e-6
+
+
+@pytest.mark.parametrize("b,h,w", [(2, 224, 224), (3, 37, 53), (1, 9, 7), (2, 64, 72)])
+def test_stem_pool_h2_bit_identical(cuda, b, h, w):
+    """The stem with its max-pool fused (rr_stem_pool_h2) writes the same bits
+    as the f16x2 stem conv + ReLU followed by the max-pool, on map sizes whose
+    pooled grid leaves ragged 8 x 7 tiles; its max-|x| record equals the conv
+    output's (networks/backbone.py:103-109)."""
+    g = torch.Generator().manual_seed(b * h + w)
+    x4 = F.pad(torch.randn(b, h, w, 3, generator=g) * 1.5, (0, 1)).contiguous().to(cuda)
+    wt = F.pad(torch.randn(64, 7, 7, 3, generator=g) * (2.0 / 147) ** 0.5, (0, 1)).contiguous().to(cuda)
+    bias = (torch.randn(64, generator=g) * 0.1).to(cuda)
+    wc = ops.H2Conv(wt)
+    rec = ops.amax_records(3, cuda)
+    ops.amax_f32(x4, rec[0])
+    y = ops.conv2d_h2(x4, rec[0], wc, bias, 2, 3, None, True, rec[1])
+    ref = ops.maxpool2d(y, 3, 2, 1)
+    got = ops.stem_pool_h2(x4, rec[0], wc, bias, 2, 3, rec[2])
+    assert got.shape == ref.shape
+    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
+    assert ops.amax_value(rec[2]) == ops.amax_value(rec[1])
+
+
+def test_resnet_h2_fused_stem_pool_bit_identical(cuda):
+    """The trunk with the fused stem + max-pool equals the unfused trunk bit
+    for bit (same pooled values, same max-|x| record)."""
+    from research_image_retrieval_amd.networks import ResNet
+    rs = np.random.RandomState(11)
+    x = torch.from_numpy(rs.standard_normal((2, 70, 90, 3)).astype(np.float32)).to(cuda)
+    net = ResNet("resnet50", seed=3, device=cuda)
+    a = net.forward(x)
+    net.fuse_stem_pool = False
+    b = net.forward(x)
+    assert torch.equal(a.view(torch.int32), b.view(torch.int32))
