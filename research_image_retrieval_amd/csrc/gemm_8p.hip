@@ -27,6 +27,18 @@
 // read from P5 on; P8 waits vmcnt(4) (up to P6: tile 2j+2 complete), read from
 // the next P1.  The counted waits never drain to 0 inside the loop, so the
 // DMA stays in flight across the raw barriers.
+//
+// fp8 (OCP e4m3, DT_FP8; the C5 sweep): the same 128-B rows hold 128 k.  A
+// wave's 64x32 piece of a quadrant is two 32x32 tiles on the block-scaled
+// v_mfma_scale_f32_32x32x64_f8f6f4 with unit E8M0 scales (the rows' fp32
+// scales are applied to the accumulator in the epilogue, as gemm_f32.hip's
+// fp8 tiles do), two 64-deep k-steps per k-tile: 4 MFMAs per phase, each
+// twice the cycles of the bf16 32x32x16 at 4x the k, so the phase is as long
+// as the bf16 phase over the same LDS bytes.  Lane half h holds the 32 bytes
+// of 16-B slots 4 step + 2h, +1 (gemm_f32.hip's fp8 reads); A and B use the
+// same lane -> k map, so each dot product covers every k once.  (The
+// 16x16x128 form of this tile left the compiler copying its accumulators and
+// spilling, 68-128 B per lane, which broke the counted waits.)
 #include "gemm_epilogue.hpp"
 #include "rr_internal.hpp"
 
@@ -38,8 +50,10 @@ constexpr int P8_HALF = 128 * 128;  // bytes per half-tile (128 rows x 128 B)
 
 __device__ __forceinline__ int swz8(int row, int slot) { return slot ^ ((row >> 1) & 7); }
 
-template <int EM>
+template <int EM, int DT>
 __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g, int tiles_n) {
+  constexpr bool F8 = DT == DT_FP8;
+  constexpr int EPR = F8 ? 128 : 64;  // elements per 128-B row (k per k-tile)
   __shared__ __attribute__((aligned(16))) unsigned char lds[8 * P8_HALF];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -52,11 +66,11 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g, int tiles_n
   const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
   const int tn = wgid % tiles_n, tm = wgid / tiles_n;
   const int m0 = tm * 256, n0 = tn * 256;
-  const int nk = g.K / 64;  // even (K % 128 == 0, checked on the host)
+  const int nk = g.K / EPR;  // even (K % (2 EPR) == 0, checked on the host)
 
   // LDS-DMA sources: instruction i of wave w fills rows (i*8 + w)*8 .. +7 of a
   // half, lane l -> row + l/8, physical slot l%8 (logical slot swz8 of it)
-  const uint16_t* src[4][2];
+  const unsigned char* src[4][2];
 #pragma unroll
   for (int h = 0; h < 4; ++h)
 #pragma unroll
@@ -65,56 +79,88 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g, int tiles_n
       const bool isa = h < 2;
       const int row = (isa ? m0 : n0) + (h & 1) * 128 + r;
       const int lim = (isa ? g.M : g.N) - 1;
-      const uint16_t* base = reinterpret_cast<const uint16_t*>(isa ? g.A : g.B);
-      src[h][i] = base + (long long)min(row, lim) * (isa ? g.lda : g.ldb) + swz8(r, lane & 7) * 8;
+      const unsigned char* base = reinterpret_cast<const unsigned char*>(isa ? g.A : g.B);
+      src[h][i] = base + ((long long)min(row, lim) * (isa ? g.lda : g.ldb)) * (F8 ? 1 : 2) + swz8(r, lane & 7) * 16;
     }
   auto stage = [&](int h, int kt, int buf) {
     const int t = min(kt, nk - 1);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
       __builtin_amdgcn_global_load_lds(
-          (const void*)(src[h][i] + (long long)t * 64),
+          (const void*)(src[h][i] + (long long)t * 128),
           (__attribute__((address_space(3))) void*)(lds + (buf * 4 + h) * P8_HALF + (i * 8 + wave) * 8 * 128), 16, 0, 0);
   };
 
-  f32x4 acc[4][4][2];
+  f32x4 acc[F8 ? 1 : 4][4][2];  // bf16: [quadrant][16-row group][16-col group]
+  f32x16 acc8[F8 ? 4 : 1][2];    // fp8: [quadrant][32-row tile]
 #pragma unroll
-  for (int q = 0; q < 4; ++q)
+  for (int q = 0; q < (F8 ? 1 : 4); ++q)
 #pragma unroll
     for (int a = 0; a < 4; ++a)
 #pragma unroll
       for (int b = 0; b < 2; ++b) acc[q][a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[4][2], fb[2][2];
+#pragma unroll
+  for (int q = 0; q < (F8 ? 4 : 1); ++q)
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc8[q][i][r] = 0.f;
+  const int l32 = lane & 31, lh = lane >> 5;
+  // fragments, 8 registers each.  bf16: fa[mg] / fb[ng] = 16-B slots lg (k-step
+  // 0) and 4 + lg (k-step 1) of row l16 of a 16-row group; fp8: fa[2 i + st] /
+  // fb[st] = the 32 bytes of k-step st of row l32 of 32-row tile i
+  i32x8 fa[4], fb[2];
+  auto rd32 = [&](const unsigned char* base, int row, int s0, int s1) {
+    const i32x4 x = *reinterpret_cast<const i32x4*>(base + row * 128 + swz8(row, s0) * 16);
+    const i32x4 y = *reinterpret_cast<const i32x4*>(base + row * 128 + swz8(row, s1) * 16);
+    return __builtin_shufflevector(x, y, 0, 1, 2, 3, 4, 5, 6, 7);
+  };
 
   auto read_a = [&](int buf, int ha) {
     const unsigned char* base = lds + (buf * 4 + ha) * P8_HALF;
+    if constexpr (F8) {
 #pragma unroll
-    for (int mg = 0; mg < 4; ++mg) {
-      const int row = wr * 64 + mg * 16 + l16;
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        fa[mg][s] = *reinterpret_cast<const bf16x8*>(base + row * 128 + swz8(row, 4 * s + lg) * 16);
+        for (int st = 0; st < 2; ++st) fa[2 * i + st] = rd32(base, wr * 64 + i * 32 + l32, 4 * st + 2 * lh, 4 * st + 2 * lh + 1);
+    } else {
+#pragma unroll
+      for (int mg = 0; mg < 4; ++mg) fa[mg] = rd32(base, wr * 64 + mg * 16 + l16, lg, 4 + lg);
     }
   };
   auto read_b = [&](int buf, int hb) {
     const unsigned char* base = lds + (buf * 4 + 2 + hb) * P8_HALF;
+    if constexpr (F8) {
 #pragma unroll
-    for (int ng = 0; ng < 2; ++ng) {
-      const int row = wc * 32 + ng * 16 + l16;
+      for (int st = 0; st < 2; ++st) fb[st] = rd32(base, wc * 32 + l32, 4 * st + 2 * lh, 4 * st + 2 * lh + 1);
+    } else {
 #pragma unroll
-      for (int s = 0; s < 2; ++s)
-        fb[ng][s] = *reinterpret_cast<const bf16x8*>(base + row * 128 + swz8(row, 4 * s + lg) * 16);
+      for (int ng = 0; ng < 2; ++ng) fb[ng] = rd32(base, wc * 32 + ng * 16 + l16, lg, 4 + lg);
     }
+  };
+  auto half_bf = [](const i32x8& v, int s) {
+    const i32x4 h = s ? __builtin_shufflevector(v, v, 4, 5, 6, 7) : __builtin_shufflevector(v, v, 0, 1, 2, 3);
+    return __builtin_bit_cast(bf16x8, h);
   };
   auto mfma_q = [&](int q) {
     __builtin_amdgcn_s_setprio(1);
+    if constexpr (F8) {
 #pragma unroll
-    for (int s = 0; s < 2; ++s)
+      for (int st = 0; st < 2; ++st)
 #pragma unroll
-      for (int mg = 0; mg < 4; ++mg)
+        for (int i = 0; i < 2; ++i)
+          acc8[q][i] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(fa[2 * i + st], fb[st], acc8[q][i], 0, 0, 0, 127,
+                                                                       0, 127);
+    } else {
 #pragma unroll
-        for (int ng = 0; ng < 2; ++ng)
-          acc[q][mg][ng] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[mg][s], fb[ng][s], acc[q][mg][ng], 0, 0, 0);
+      for (int s = 0; s < 2; ++s)
+#pragma unroll
+        for (int mg = 0; mg < 4; ++mg)
+#pragma unroll
+          for (int ng = 0; ng < 2; ++ng)
+            acc[q][mg][ng] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(half_bf(fa[mg], s), half_bf(fb[ng], s),
+                                                                     acc[q][mg][ng], 0, 0, 0);
+    }
     __builtin_amdgcn_s_setprio(0);
   };
   auto sync_mid = [&]() {
@@ -193,6 +239,62 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g, int tiles_n
 
   // acc[q][mg][ng][e]: row = qa*128 + wr*64 + mg*16 + 4*lg + e, col = qb*128 + wc*32 + ng*16 + l16
   constexpr int QA[4] = {0, 0, 1, 1}, QB[4] = {0, 1, 1, 0};
+  if constexpr (F8) {
+    // acc8[q][i][r]: row = qa*128 + wr*64 + 32 i + (r & 3) + 8 (r >> 2) + 4 lh,
+    // col = qb*128 + wc*32 + l32; the rows' fp32 scales first (gemm_f32.hip's
+    // fp8 order: acc * s_a * s_b), one quadrant at a time (all at once spilled)
+    const bool scaled = g.scale_a != nullptr || g.scale_b != nullptr;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int n = n0 + QB[q] * 128 + wc * 32 + l32;
+      const bool nok = n < g.N;
+      if (scaled) {
+        const float sb = (g.scale_b != nullptr && nok) ? g.scale_b[n] : 1.f;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + QA[q] * 128 + wr * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const float sa = (g.scale_a != nullptr && m < g.M) ? g.scale_a[m] : 1.f;
+            acc8[q][i][r] = acc8[q][i][r] * sa * sb;
+          }
+      }
+      if constexpr (EM == E_FILTER) {
+        const float t = nok ? g.tau[n] : __builtin_inff();
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int m = m0 + QA[q] * 128 + wr * 64 + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lh;
+            const float v = acc8[q][i][r];
+            if (nok && m < g.M && !(v <= t)) {
+              const int pos = atomicAdd(g.cnt + n, 1);
+              if (pos < g.cap) g.cand[(long long)n * g.cap + pos] = make_key(v, (uint32_t)(g.row_offset + m));
+            }
+          }
+      } else if constexpr (EM == E_SCORES_T) {
+        if (nok) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+              const int mb = m0 + QA[q] * 128 + wr * 64 + 32 * i + 8 * b + 4 * lh;
+              float* dst = g.C + (long long)n * g.ldc + mb;
+              if (mb + 3 < g.M) {
+                *reinterpret_cast<f32x4*>(dst) =
+                    f32x4{acc8[q][i][4 * b], acc8[q][i][4 * b + 1], acc8[q][i][4 * b + 2], acc8[q][i][4 * b + 3]};
+              } else {
+#pragma unroll
+                for (int e = 0; e < 4; ++e)
+                  if (mb + e < g.M) dst[e] = acc8[q][i][4 * b + e];
+              }
+            }
+        }
+      }
+      asm volatile("" ::: "memory");
+    }
+    return;
+  }
   if constexpr (EM == E_FILTER) {
 #pragma unroll
     for (int q = 0; q < 4; ++q)
@@ -238,22 +340,29 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g, int tiles_n
 
 }  // namespace
 
-// Host side: dense bf16 A and B, K % 128 == 0 (whole k-tile pairs), 16-B
-// aligned rows (checked by launch_gemm), no split-K / symmetric / scales.
-bool gemm_8p_eligible(const GemmArgs& g) {
-  return (g.K % 128) == 0 && g.k_split == 0 && !g.sym && g.scale_a == nullptr && g.scale_b == nullptr &&
+// Host side: dense A and B, K a multiple of two k-tiles (bf16 128, fp8 256),
+// 16-B aligned rows (checked by launch_gemm), no split-K / symmetric; row
+// scales only for fp8.
+bool gemm_8p_eligible(const GemmArgs& g, int dt) {
+  const int ktp = dt == DT_FP8 ? 256 : 128;
+  return (dt == DT_BF16 || dt == DT_FP8) && (g.K % ktp) == 0 && g.k_split == 0 && !g.sym &&
+         (dt == DT_FP8 || (g.scale_a == nullptr && g.scale_b == nullptr)) &&
          (((uintptr_t)g.A | (uintptr_t)g.B) & 15) == 0;
 }
 
-hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s) {
+hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s, int dt) {
   const long long tiles_m = (g.M + 255) / 256, tiles_n = (g.N + 255) / 256;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  if (emode == E_FILTER)
-    hipLaunchKernelGGL(gemm_8p_kernel<E_FILTER>, dim3((unsigned)nblk), dim3(512), 0, s, g, (int)tiles_n);
+  if (emode == E_FILTER && dt == DT_FP8)
+    hipLaunchKernelGGL((gemm_8p_kernel<E_FILTER, DT_FP8>), dim3((unsigned)nblk), dim3(512), 0, s, g, (int)tiles_n);
+  else if (emode == E_SCORES_T && dt == DT_FP8)
+    hipLaunchKernelGGL((gemm_8p_kernel<E_SCORES_T, DT_FP8>), dim3((unsigned)nblk), dim3(512), 0, s, g, (int)tiles_n);
+  else if (emode == E_FILTER)
+    hipLaunchKernelGGL((gemm_8p_kernel<E_FILTER, DT_BF16>), dim3((unsigned)nblk), dim3(512), 0, s, g, (int)tiles_n);
   else if (emode == E_SCORES_T)
-    hipLaunchKernelGGL(gemm_8p_kernel<E_SCORES_T>, dim3((unsigned)nblk), dim3(512), 0, s, g, (int)tiles_n);
+    hipLaunchKernelGGL((gemm_8p_kernel<E_SCORES_T, DT_BF16>), dim3((unsigned)nblk), dim3(512), 0, s, g, (int)tiles_n);
   else
     return hipErrorInvalidValue;  // stored C: the 256x256 tile of gemm_f32.hip (config 3)
   return hipGetLastError();

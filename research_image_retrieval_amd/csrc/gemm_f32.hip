@@ -809,8 +809,8 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
   int cfg = pick_lp(g, EM, DT == DT_BF16, tu);
   if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles
   if (cfg == 5) {
-    if constexpr (DT == DT_BF16) {
-      if (gemm_8p_eligible(g)) return launch_gemm_8p(g, EM, s);
+    if constexpr (DT != DT_F32 && EM != E_STORE) {
+      if (gemm_8p_eligible(g, DT)) return launch_gemm_8p(g, EM, s, DT);
     }
     cfg = 3;
   }

@@ -594,7 +594,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       write_a(stn);  // that stage is free since the last barrier
       // f16x2: the conv A loader's state leaves no room to hold the plane-0
       // fragments across the split (2 registers spilled): re-read them
-      if constexpr (SP == 2 && (MF_REREAD || AMODE != A_DENSE)) rd_mf(cur, 0);
+      // (ACC1 leaves the registers to hold them)
+      if constexpr (SP == 2 && !ACC1 && (MF_REREAD || AMODE != A_DENSE)) rd_mf(cur, 0);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1329,8 +1330,13 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //      == 0 — the picked tile for the 1x1 layers it serves
 //   9: config 4 with three LDS stages (f16x2 only, 144 KB): the B DMA two
 //      k-tiles ahead
+//  10: config 4 with one accumulator set (f16x2 only, ACC1: the plane-1
+//      products accumulate with a0b0; error vs float64 still at the exact-fp32
+//      core's, profiles/r03j_acc1_ab.txt; 196 instead of 254 VGPRs)
+//  11: 128x128, 4 waves of 64x64, BK 32, 2/CU (64 KB), 16x16x32, ACC1 (f16x2
+//      only): the picked tile for N == 128
 // (all others on v_mfma_f32_32x32x16_{bf16,f16}).  The f16x2 split is built
-// for the picked configs 3, 4, 7 and 8 (a forced 1, 2, 5 or 6 runs the pick).
+// for configs 3, 4, 7, 8, 9, 10 and 11 (a forced 1, 2, 5 or 6 runs the pick).
 // Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the fastest
 // wherever N >= 128 (1.1-1.3x config 1 per FLOP); 4 on 16x16x32 runs every
 // N % 256 == 0 layer 3-14 % faster than 3 (the 16x16 shape holds a higher
@@ -1359,6 +1365,10 @@ static int pick_s3(const GemmArgs& g, int forced) {
 static int pick_h2(const GemmArgs& g, int forced) {
   if (forced == 9) return (g.N % 256) == 0 ? 9 : pick_h2(g, 0);
   if (forced == 10) return (g.N % 256) == 0 ? 10 : pick_h2(g, 0);
+  if (forced == 11) return (g.N % 128) == 0 ? 11 : pick_h2(g, 0);
+  // N == 128: two 128x128 blocks per CU (config 11) run the R101 N = 128
+  // layers 4-7 % faster than the 256x128 tile (profiles/r03l_h2_cfg_sweep.txt)
+  if (forced == 0 && g.N == 128) return 11;
   int cfg = pick_s3(g, forced);
   if (cfg == 3 || cfg == 4 || cfg == 7 || cfg == 8) return cfg;
   cfg = pick_s3(g, 0);
@@ -1432,6 +1442,7 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
     case 4: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1, 2>(g, s, n_cu, st);
     case 9: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1, 2, 3>(g, s, n_cu, st);
     case 10: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1, 2, 2, 1>(g, s, n_cu, st);
+    case 11: return launch_s3_ep<2, 2, 2, 2, 32, AM, 2, 1, 2, 2, 1>(g, s, n_cu, st);
     case 7: return launch_s3_ep<8, 1, 1, 2, 16, AM, 4, 0, 2>(g, s, n_cu, st);
     default: return launch_s3_ep<4, 2, 2, 2, 32, AM, 1, 0, 2>(g, s, n_cu, st);
   }

@@ -242,9 +242,10 @@ int launch_amax(rr_handle_s* h, const float* x, long long n, uint32_t* slots, hi
 // bf16 filter sweep with the gallery in VGPRs (sweep_v.hip): dense A/B, K % 64 == 0
 bool sweep_v_eligible(const GemmArgs& g);
 hipError_t launch_sweep_v(const GemmArgs& g, hipStream_t s);
-// bf16 256x256 8-phase pipeline (gemm_8p.hip): dense A/B, K % 128 == 0
-bool gemm_8p_eligible(const GemmArgs& g);
-hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s);
+// 256x256 8-phase pipeline (gemm_8p.hip), bf16 or fp8 (16x16x128 block-scaled
+// MFMA): dense A/B, K a multiple of two k-tiles
+bool gemm_8p_eligible(const GemmArgs& g, int dt);
+hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s, int dt);
 int launch_split3(rr_handle_s* h, const float* x, long long n, uint16_t* planes, hipStream_t s);
 
 // ---- top-k kernels (topk.hip) -------------------------------------------

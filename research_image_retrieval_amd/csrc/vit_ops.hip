@@ -173,16 +173,29 @@ __global__ __launch_bounds__(64 * NC) void attention_kernel(const float* __restr
   const long long ld = 3LL * width;
   const float* base = qkv + (long long)b * L * ld;
   const int tid = threadIdx.x;
-  // stage K and V
-  for (int idx = tid; idx < LP * (HD / 4); idx += 64 * NC) {
-    const int row = idx / (HD / 4), s4 = idx - row * (HD / 4);
-    f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
-    if (row < L) {
-      kv = *reinterpret_cast<const f32x4*>(base + (long long)row * ld + width + h * HD + s4 * 4);
-      vv = *reinterpret_cast<const f32x4*>(base + (long long)row * ld + 2 * width + h * HD + s4 * 4);
+  // stage K and V: every thread's NIT = 8 groups, all loads issued before the
+  // first LDS store (as attention_bf16_kernel)
+  constexpr int NIT = LP * (HD / 4) / (64 * NC);
+  static_assert(NIT * 64 * NC == LP * (HD / 4), "staging groups must tile the block");
+  {
+    f32x4 kv[NIT], vv[NIT];
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * 64 * NC;
+      const int row = idx / (HD / 4), s4 = idx - row * (HD / 4);
+      kv[it] = vv[it] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (row < L) {
+        kv[it] = *reinterpret_cast<const f32x4*>(base + (long long)row * ld + width + h * HD + s4 * 4);
+        vv[it] = *reinterpret_cast<const f32x4*>(base + (long long)row * ld + 2 * width + h * HD + s4 * 4);
+      }
     }
-    *reinterpret_cast<f32x4*>(Ks + row * HD + ((s4 ^ (row & 15)) * 4)) = kv;
-    *reinterpret_cast<f32x4*>(Vs + row * HD + s4 * 4) = vv;
+#pragma unroll
+    for (int it = 0; it < NIT; ++it) {
+      const int idx = tid + it * 64 * NC;
+      const int row = idx / (HD / 4), s4 = idx - row * (HD / 4);
+      *reinterpret_cast<f32x4*>(Ks + row * HD + ((s4 ^ (row & 15)) * 4)) = kv[it];
+      *reinterpret_cast<f32x4*>(Vs + row * HD + s4 * 4) = vv[it];
+    }
   }
   const int wave = tid >> 6, lane = tid & 63;
   const int lr = lane & 31, lh = lane >> 5;
@@ -316,19 +329,33 @@ __global__ __launch_bounds__(64 * NC, 2) void attention_bf16_kernel(const InT* _
   const long long ld = 3LL * width;
   const InT* base = qkv + (long long)b * L * ld;
   const int tid = threadIdx.x;
-  for (int idx = tid; idx < LP * (HD / 4); idx += 64 * NC) {
+  // K / V staging: every thread handles exactly NIT = LP * 16 / (64 NC) = 8
+  // four-element groups.  All 2 NIT loads are issued before the first LDS
+  // store (one HBM round trip per block instead of NIT serialised ones: the
+  // loop form waited for each iteration's loads before its stores)
+  constexpr int NIT = LP * (HD / 4) / (64 * NC);
+  static_assert(NIT * 64 * NC == LP * (HD / 4), "staging groups must tile the block");
+  f32x4 kv[NIT], vv[NIT];
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int idx = tid + it * 64 * NC;
     const int row = idx / (HD / 4), s4 = idx - row * (HD / 4);
-    f32x4 kv = {0.f, 0.f, 0.f, 0.f}, vv = {0.f, 0.f, 0.f, 0.f};
+    kv[it] = vv[it] = f32x4{0.f, 0.f, 0.f, 0.f};
     if (row < L) {
-      kv = ld4f(base + (long long)row * ld + width + h * HD + s4 * 4);
-      vv = ld4f(base + (long long)row * ld + 2 * width + h * HD + s4 * 4);
+      kv[it] = ld4f(base + (long long)row * ld + width + h * HD + s4 * 4);
+      vv[it] = ld4f(base + (long long)row * ld + 2 * width + h * HD + s4 * 4);
     }
+  }
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int idx = tid + it * 64 * NC;
+    const int row = idx / (HD / 4), s4 = idx - row * (HD / 4);
     typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-    const bf16x4 kb = {(__bf16)kv[0], (__bf16)kv[1], (__bf16)kv[2], (__bf16)kv[3]};
+    const bf16x4 kb = {(__bf16)kv[it][0], (__bf16)kv[it][1], (__bf16)kv[it][2], (__bf16)kv[it][3]};
     *reinterpret_cast<bf16x4*>(Ks + row * HD + (((s4 >> 1) ^ ((row >> 1) & 7)) * 8) + (s4 & 1) * 4) = kb;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      const __bf16 v = (__bf16)vv[e];
+      const __bf16 v = (__bf16)vv[it][e];
       Vt[(s4 * 4 + e) * VS + row] = __builtin_bit_cast(uint16_t, v);
     }
   }

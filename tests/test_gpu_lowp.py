@@ -67,19 +67,23 @@ def test_lowp_cosine_recall_at_100(cuda, dtype, min_recall):
     assert (i[:6, 0] == i_ref[:6, 0]).all()  # planted near-duplicates stay first
 
 
+@pytest.mark.parametrize("lp_cfg", [0, 5])
 @pytest.mark.parametrize("dtype", ["bf16", "fp8"])
-def test_lowp_topk_many_queries_vs_dequantised(cuda, dtype):
+def test_lowp_topk_many_queries_vs_dequantised(cuda, dtype, lp_cfg):
     """>= 1024 queries over 200 k rows: the filter sweep runs on the 8-wave
-    256x256 tile (16x16x32 bf16 / block-scaled fp8 MFMA).  The returned scores
-    are the fp32 dot products of the dequantised rows, and the returned lists
-    are the top-100 of those scores (torch on the same dequantised rows)."""
+    256x256 tile (16x16x32 bf16 / block-scaled fp8 MFMA), or forced (lp_cfg 5)
+    on the 8-phase 256x256 pipeline of gemm_8p.hip (bf16, and fp8 on the
+    32x32x64 block-scaled MFMA).  The returned scores are the fp32 dot
+    products of the dequantised rows, and the returned lists are the top-100
+    of those scores (torch on the same dequantised rows)."""
     g = torch.Generator(device=cuda).manual_seed(11)
     n, d, q, k = 200_000, 512, 1100, 100
     gal = torch.nn.functional.normalize(torch.randn(n, d, device=cuda, generator=g), dim=1)
     qs_ = torch.nn.functional.normalize(torch.randn(q, d, device=cuda, generator=g), dim=1)
     gl, gs = ops.quantize_rows(gal, dtype)
     ql, qs = ops.quantize_rows(qs_, dtype)
-    s, i = ops.cosine_topk_lp(ql, qs, gl, gs, k, dtype)
+    with ops.tuning(0, lp_cfg=lp_cfg):
+        s, i = ops.cosine_topk_lp(ql, qs, gl, gs, k, dtype)
     if dtype == "bf16":
         gd, qd = gl.float(), ql.float()
     else:
