@@ -431,7 +431,7 @@ def run_c2(a, world, rank, dev):
         res["cpu_baseline"] = cpu_baseline_c2([(st["n_g"], st["n_q"]) for st in sets])
         log(f"cpu baseline {time.time() - t:.1f}s")
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res, default=_json_scalar), flush=True)
     if DIST_ON:
         dist.barrier()
         dist.destroy_process_group()
@@ -452,6 +452,13 @@ def load_traffic():
         except (OSError, ValueError):
             return None
     return None
+
+
+def _json_scalar(o):
+    """numpy scalars (dataset sizes, FLOP counts) in the JSON line."""
+    if hasattr(o, "item"):
+        return o.item()
+    raise TypeError(f"not JSON serializable: {type(o).__name__}")
 
 
 def main():
@@ -812,7 +819,7 @@ def main():
         res["cpu_baseline"] = cpu_baseline(a.arch, a.gallery, a.dim, a.k)
         log(f"cpu baseline {time.time() - t:.1f}s")
     if rank == 0:
-        print(json.dumps(res), flush=True)
+        print(json.dumps(res, default=_json_scalar), flush=True)
     if DIST_ON:
         dist.barrier()
         dist.destroy_process_group()

@@ -208,7 +208,7 @@ struct S3Phases {
 template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0, int EPI = -1, int SP = 3,
           int NSTG = 2, int POOL = 0, int ACC1 = 0>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
-  static_assert(!ACC1 || (SP == 2 && MF16), "one accumulator: the f16x2 16x16x32 tile");
+  static_assert(!ACC1 || SP == 2, "one accumulator: the f16x2 split");
   static_assert(!POOL || (AMODE == A_CONV_C4 && WM * 32 * FM == 256 && SP == 2), "stem + max-pool: 256-row NHWC4 tile");
   static_assert(NSTG == 2 || (NSTG == 3 && MF16 && SP == 2), "three LDS stages: the f16x2 16x16x32 tile");
   static_assert(!MF16 || BK == 32, "MF16: BK 32");
@@ -234,7 +234,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   // (rows padded by 4 / 8 floats, epilogue_store)
   constexpr int CT_F = BM * (BN + (MF16 ? 4 : 8));
   // (the fused stem + max-pool stages its whole C tile at any MINB)
-  constexpr int LDS_U16 = (SP == 2 && (MINB == 1 || POOL) && 2 * CT_F > NSTG * BUF) ? 2 * CT_F : NSTG * BUF;
+  constexpr int LDS_U16 =
+      (SP == 2 && (MINB == 1 || POOL) && 2 * CT_F > NSTG * BUF && 2 * CT_F <= 80 * 1024) ? 2 * CT_F : NSTG * BUF;
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
 
   // the A operand's split scale (f16x2): its max-|x| record is loaded first,
@@ -435,7 +436,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   };
 
   f32x16 hi[FM][FN];
-  f32x16 lo[FM][FN];
+  f32x16 lo[ACC1 ? 1 : FM][ACC1 ? 1 : FN];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -443,7 +444,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         hi[i][j][r] = 0.f;
-        lo[i][j][r] = 0.f;
+        if constexpr (!ACC1) lo[i][j][r] = 0.f;
       }
 
   auto compute_st = [&](int cur, int st) {
@@ -472,7 +473,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
-          f32x16& L = lo[i][j];
+          f32x16& L = ACC1 ? hi[i][j] : lo[ACC1 ? 0 : i][ACC1 ? 0 : j];
           if constexpr (SP == 3) {
             L = s3_mf32<SP>(a[1][i], b[1][j], L);
             L = s3_mf32<SP>(a[0][i], b[NP - 1][j], L);
@@ -779,7 +780,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < FN; ++j) hi[i][j] += lo[i][j];
+      for (int j = 0; j < FN; ++j)
+        if constexpr (!ACC1) hi[i][j] += lo[i][j];
   }
   if constexpr (POOL) {
     // stage the raw 256 x 64 accumulator tile, then every pooled output of
@@ -1335,6 +1337,10 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //      core's, profiles/r03j_acc1_ab.txt; 196 instead of 254 VGPRs)
 //  11: 128x128, 4 waves of 64x64, BK 32, 2/CU (64 KB), 16x16x32, ACC1 (f16x2
 //      only): the picked tile for N == 128
+//  12: 256x256, 8 waves of 128x64, BK 32, 1/CU (128 KB), 32x32x16, ACC1 (f16x2
+//      only; 254 VGPRs — two accumulator sets do not fit this tile): half the
+//      operand bytes per FLOP of config 4, the picked tile for N % 256 == 0
+//      except the K < 256 residual expansions
 // (all others on v_mfma_f32_32x32x16_{bf16,f16}).  The f16x2 split is built
 // for configs 3, 4, 7, 8, 9, 10 and 11 (a forced 1, 2, 5 or 6 runs the pick).
 // Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the fastest
@@ -1366,6 +1372,7 @@ static int pick_h2(const GemmArgs& g, int forced) {
   if (forced == 9) return (g.N % 256) == 0 ? 9 : pick_h2(g, 0);
   if (forced == 10) return (g.N % 256) == 0 ? 10 : pick_h2(g, 0);
   if (forced == 11) return (g.N % 128) == 0 ? 11 : pick_h2(g, 0);
+  if (forced == 12) return (g.N % 256) == 0 ? 12 : pick_h2(g, 0);
   // N == 128: two 128x128 blocks per CU (config 11) run the R101 N = 128
   // layers 4-7 % faster than the 256x128 tile (profiles/r03l_h2_cfg_sweep.txt)
   if (forced == 0 && g.N == 128) return 11;
@@ -1431,7 +1438,16 @@ static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int
 template <int AM>
 static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
   int cfg = pick_h2(g, forced);
-  if (forced == 0 && AM == A_DENSE && s3_persist_ok<2>(g, AM)) cfg = 8;
+  // N % 256 == 0: the 256x256 one-accumulator tile (config 12) everywhere but
+  // the short-K residual expansions (K < 256: their epilogue dominates and the
+  // persistent k-stream, config 8, hides part of it).  Measured per R101 layer
+  // at 1280 images (profiles/r03p_h2_cfg_sweep.txt): 3x3 256@14 0.848 -> 0.794
+  // ms, 1024->256 0.432 -> 0.400, 512@7 0.778 -> 0.707, 2048->512 0.393 ->
+  // 0.350, 256->1024 (residual) 0.690 -> 0.676; 128->512 / 64->256 (residual,
+  // K 128 / 64) 17 % / 8 % slower, so those keep config 8.
+  const bool big = (g.N % 256) == 0 && (g.residual == nullptr || g.K >= 256);
+  if (forced == 0 && big) cfg = 12;
+  else if (forced == 0 && AM == A_DENSE && s3_persist_ok<2>(g, AM)) cfg = 8;
   if (cfg == 8) {
     if constexpr (AM == A_DENSE) {
       if (s3_persist_ok<2>(g, AM)) return launch_s3p<2>(g, s, n_cu, st);
@@ -1443,6 +1459,7 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
     case 9: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1, 2, 3>(g, s, n_cu, st);
     case 10: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1, 2, 2, 1>(g, s, n_cu, st);
     case 11: return launch_s3_ep<2, 2, 2, 2, 32, AM, 2, 1, 2, 2, 1>(g, s, n_cu, st);
+    case 12: return launch_s3_ep<2, 4, 4, 2, 32, AM, 1, 0, 2, 2, 1>(g, s, n_cu, st);
     case 7: return launch_s3_ep<8, 1, 1, 2, 16, AM, 4, 0, 2>(g, s, n_cu, st);
     default: return launch_s3_ep<4, 2, 2, 2, 32, AM, 1, 0, 2>(g, s, n_cu, st);
   }

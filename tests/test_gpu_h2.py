@@ -176,7 +176,7 @@ TILE_SHAPES = [  # shapes that reach each f16x2 config's edges: ragged M, N = 64
 ]
 
 
-@pytest.mark.parametrize("cfg", [3, 4, 7, 8, 9, 10, 11])
+@pytest.mark.parametrize("cfg", [3, 4, 7, 8, 9, 10, 11, 12])
 @pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res", TILE_SHAPES)
 def test_conv2d_h2_tile_configs(cuda, cfg, b, h, w, cin, cout, k, s, p, res):
     """Every f16x2 tile config forced on every shape: fp32-grade vs float64
