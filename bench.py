@@ -765,8 +765,12 @@ def main():
             e["math"] = SPLIT_MATH[dt][1] + (" (every conv incl. the stem; the whiten and PCA-w linears, 0.2% of "
                                              "the FLOPs, run on the exact-fp32 core)")
             e["mfma_flop_per_launch"] = SPLIT_MATH[dt][0] * fl_step / max(1.0, n / a.steps)
+            # the class's fp32-equivalent rate (algorithmic FLOPs / time) whichever
+            # bound is reported, against both split cores' ceilings
+            e["fp32_equiv_tflops"] = round(fl_step / sec / 1e12, 2)
+            e["frac_of_split_ceiling"] = round(fl_step / sec / 1e12 / PEAK_TFLOPS[dt], 4)
             if dt == "h2":  # the previous core's ceiling, for comparison across rounds
-                e["frac_of_bf16x3_ceiling"] = round(e["achieved"] / PEAK_TFLOPS["s3"], 4) if e["unit"] == "TFLOP/s" else None
+                e["frac_of_bf16x3_ceiling"] = round(fl_step / sec / 1e12 / PEAK_TFLOPS["s3"], 4)
         e.update({"dtype": "fp32" if dt in SPLIT_MATH else dt, "ms_per_step": round(ms / a.steps, 3),
                   "launches_per_step": n / a.steps,
                   "algorithmic_flop_per_launch": fl_step / max(1.0, n / a.steps),

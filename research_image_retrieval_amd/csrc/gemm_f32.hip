@@ -803,8 +803,8 @@ template <int EM, int DT>
 static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s::Tuning& tu) {
   constexpr int EPR = DT == DT_BF16 ? 64 : 128;  // elements per 128-B k-tile row
   constexpr int MF = DT == DT_BF16 ? 1 : 0;
-  if constexpr (EM == E_FILTER && DT == DT_BF16) {
-    if (tu.lp_cfg == 6 && sweep_v_eligible(g)) return launch_sweep_v(g, s);
+  if constexpr (EM == E_FILTER && DT != DT_F32) {
+    if (tu.lp_cfg == 6 && sweep_v_eligible(g, DT)) return launch_sweep_v(g, s, DT);
   }
   int cfg = pick_lp(g, EM, DT == DT_BF16, tu);
   if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles

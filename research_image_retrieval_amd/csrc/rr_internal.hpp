@@ -16,7 +16,7 @@ struct rr_handle_s {
   struct Tuning {
     int gemm_cfg = 0;  // fp32 core: 22, 41 or 88
     int gemm_bk = 0;   // fp32 core k-tile depth: 16 or 32
-    int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 / fp8 sweeps), 6 = gallery-in-VGPR bf16 filter sweep (sweep_v.hip)
+    int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 / fp8 sweeps), 6 = gallery-in-VGPR bf16 / fp8 filter sweep (sweep_v.hip)
     int s3_cfg = 0;    // split cores: 1..11 (gemm_s3.hip tile table; 9-11 f16x2 only)
     int s3_stagger = -1;  // split-bf16 core round stagger in ~1 us sleeps (-1: the library's pick)
   } tune;
@@ -239,9 +239,10 @@ int launch_split2h(rr_handle_s* h, const float* w, int rows, int k, int kpad, ui
 // max |x| over x[n] into the RR_AMAX_SLOTS words at slots (atomic max)
 int launch_amax(rr_handle_s* h, const float* x, long long n, uint32_t* slots, hipStream_t s);
 
-// bf16 filter sweep with the gallery in VGPRs (sweep_v.hip): dense A/B, K % 64 == 0
-bool sweep_v_eligible(const GemmArgs& g);
-hipError_t launch_sweep_v(const GemmArgs& g, hipStream_t s);
+// bf16 / fp8 filter sweep with the gallery in VGPRs (sweep_v.hip): dense A/B,
+// K % 32 (bf16) or % 128 (fp8) == 0, unscaled bf16 rows
+bool sweep_v_eligible(const GemmArgs& g, int dt);
+hipError_t launch_sweep_v(const GemmArgs& g, hipStream_t s, int dt);
 // 256x256 8-phase pipeline (gemm_8p.hip), bf16 or fp8 (16x16x128 block-scaled
 // MFMA): dense A/B, K a multiple of two k-tiles
 bool gemm_8p_eligible(const GemmArgs& g, int dt);

@@ -145,6 +145,23 @@ def test_prefilter_query_panels_of_256(cuda, nq):
     assert i[3, 0] == 77_777
 
 
+@pytest.mark.parametrize("nq,n,d", [(1280, 70_001, 2048), (300, 50_000, 256), (17, 9_999, 512)])
+def test_prefilter_gallery_in_vgpr_sweep(cuda, nq, n, d):
+    """The gallery-in-VGPR bf16 filter sweep (sweep_v.hip, lp_cfg 6: 256x256
+    blocks, query panel in LDS) inside the prefilter ranker: bit-identical to
+    the exhaustive fp32 ranker on ragged gallery tiles, padded query panels
+    and a planted exact match."""
+    rs = np.random.RandomState(nq + n)
+    g = rs.standard_normal((n, d)).astype(np.float32)
+    q = rs.standard_normal((nq, d)).astype(np.float32)
+    g[n - 1] = q[nq - 1]
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    with ops.tuning(cuda.index, lp_cfg=6):
+        s, i = _prefilter_vs_exhaustive(cuda, q, g, 100)
+    assert i[nq - 1, 0] == n - 1
+
+
 def test_prefilter_bitexact_ties_and_clusters(cuda):
     """Exact ties (duplicate rows on both sides of the seed boundary), planted
     near-duplicates, and a dense cluster where thousands of rows score within
