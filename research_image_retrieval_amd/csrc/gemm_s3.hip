@@ -1276,6 +1276,247 @@ static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
 // in; residual and ReLU select the instance
 constexpr int H2_EP = EP_SCALE | EP_AMAX | EP_BIAS;
 
+// ---- Halo-staged A for stride-1 3x3 convolutions (config 13, f16x2) -------
+// The implicit-GEMM A loader of gemm_s3_kernel fetches every input pixel once
+// per filter tap: nine fetches of each activation on a 3x3 conv.  Every tile
+// here on this chip is bound by the bytes each CU fetches per MFMA cycle
+// (the per-CU fill rate), and on the 3x3 256@14 layer the A operand
+// is half of them: per output, 4 K / Nt B of A plus 4 K / Mt B of B planes =
+// 36 + 36 B at the 256x256 tile.  Here a 256-row tile (256 consecutive output
+// pixels in NHWC raster order) loads, per 32-channel slice of Cin, the raster
+// range of input pixels its nine taps can touch — 256 + 2 (W + 1) rows, one
+// fetch each — splits it once into the two fp16 planes of an LDS halo buffer,
+// and runs the slice's nine k-tiles (one per tap) on it: output row r reads
+// halo row r + kh W + kw, or a zero row when the tap falls outside its image
+// (padding) or r is past M.  A fetch per output drops to (256 + 2W + 2) / 256
+// x 4 Cin / Nt (4.5 B at 256@14), the split VALU to one per slice instead of
+// one per k-tile.  k order: slice-major, tap-minor (k-tile (c, t) = weight
+// columns t Cin + 32 c ..); B planes by LDS-DMA one k-tile ahead as config 12;
+// 256x256 tile, 8 waves of 128x64 on v_mfma_f32_32x32x16_f16, one accumulator
+// set (ACC1, config 12's arithmetic per product); the next slice's halo goes
+// to the other buffer one 128-row pass per k-tile during the slice's first
+// four.  W <= 15 (halo <= 288 rows; the 14x14 and 7x7 layers).
+constexpr int HALO_HR = 288;  // halo rows; row HALO_HR of each plane is zero
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int tiles_n) {
+  constexpr int NP = 2, WM = 2, FM = 4, FN = 2, BK = 32, NT = 512, NW = 8;
+  constexpr int WTM = 128, WTN = 64, BM = 256, BN = 256, SL = BK / 8;
+  constexpr int HRA = HALO_HR + 1;                  // rows per A plane (+ the zero row)
+  constexpr int A_EL = NP * HRA * BK;               // u16 per halo buffer
+  constexpr int B_EL = NP * BN * BK;                // u16 per B stage
+  constexpr int B_RPI = 64 / SL;                    // plane rows per LDS-DMA wave instruction
+  constexpr int B_INS = NP * BN / B_RPI / NW;       // LDS-DMA instructions per wave per k-tile (4)
+  constexpr int A_PASS = (HALO_HR + NT / SL - 1) / (NT / SL);  // 128-row passes over the halo (3)
+  constexpr int LDS_U16 = 2 * A_EL + 2 * B_EL;
+  static_assert(B_INS * NW * B_RPI == NP * BN, "B staging must tile the block");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
+  typedef f16x8 frag_t;
+
+  const uint32_t a_amax_w = amax_load_slot(g.a_amax);
+  float a_sc = 1.f, a_isc = 1.f;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tn = wgid % tiles_n, tm = wgid / tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int W = g.W, H = g.H, KW = g.KW, ntap = g.KH * g.KW;
+  const int nch = g.Cin / BK, nk = nch * ntap;
+  const int hoff = g.pad * W + g.pad;  // halo row 0 = input raster index m0 - hoff
+
+  // ---- halo loader: thread -> (row t / 4 + 128 pass, 16-B slot pair t % 4);
+  // one 128-row pass at a time (8 registers), so the halo of the next slice
+  // never holds more than one pass beside the accumulators ----
+  const int a_slot = tid % SL, a_row = tid / SL;
+  f32x4 ra[2];
+  auto load_pass = [&](int c, int p) {
+    const int hr = a_row + p * (NT / SL);
+    const long long q = (long long)m0 - hoff + hr;
+    const bool ok = hr < HALO_HR && q >= 0 && q < g.M;
+    const f32x4* src = ok ? reinterpret_cast<const f32x4*>(g.A + q * g.Cin + c * BK + a_slot * 8) : s3_zero_page();
+    s3_load2<1>(src, ra);
+  };
+  auto launder_pass = [&]() {
+    s3_launder(ra[0]);
+    s3_launder(ra[1]);
+  };
+  auto store_pass = [&](int buf, int p) {
+    const int hr = a_row + p * (NT / SL);
+    u32x4 p0, p1;
+    split2h8(ra, a_sc, p0, p1);
+    if (hr < HALO_HR) {
+      uint16_t* la = lds + buf * A_EL;
+      const int off = hr * BK + pswz<BK, 2>(hr, a_slot) * 8;
+      *reinterpret_cast<u32x4*>(la + off) = p0;
+      *reinterpret_cast<u32x4*>(la + HRA * BK + off) = p1;
+    }
+  };
+
+  // ---- B planes: LDS-DMA, instruction i of a wave fills plane rows
+  // (i NW + wave) B_RPI .. (N % 256 == 0: every row real): plane i / 2, rows
+  // 128 (i & 1) + 16 wave + lane / 4 ----
+  const int b_r = wave * B_RPI + lane / SL;
+  const uint16_t* b_src =
+      reinterpret_cast<const uint16_t*>(g.B) + (long long)(n0 + b_r) * g.ldb + pswz<BK, 2>(b_r, lane % SL) * 8;
+  static_assert(B_INS == 4 && NW * B_RPI == BN / 2, "B DMA map: two instructions per plane");
+  auto glds_b = [&](int kt, int buf) {
+    const int c = kt / ntap, t = kt - c * ntap;
+    const long long koff = (long long)t * g.Cin + c * BK;
+    uint16_t* lb = lds + 2 * A_EL + buf * B_EL;
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i)
+      __builtin_amdgcn_global_load_lds(
+          (const void*)(b_src + (i >> 1) * g.b_plane + (long long)(i & 1) * (BN / 2) * g.ldb + koff),
+          (__attribute__((address_space(3))) void*)(lb + (i * NW + wave) * B_RPI * BK), 16, 0, 0);
+  };
+
+  // ---- the lanes' fragment rows: a 9-bit mask of the taps that stay inside
+  // the row's image (bit kh KW + kw), empty past M ----
+  int tmask[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = m0 + wm * WTM + i * 32 + lr;
+    const int rem = m % (H * W), oh = rem / W, ow = rem - oh * W;
+    int mk = 0;
+    for (int kh = 0; kh < g.KH; ++kh)
+      for (int kw = 0; kw < KW; ++kw)
+        if ((unsigned)(oh + kh - g.pad) < (unsigned)H && (unsigned)(ow + kw - g.pad) < (unsigned)W) mk |= 1 << (kh * KW + kw);
+    tmask[i] = m < g.M ? mk : 0;
+  }
+
+  f32x16 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  // one k-tile: tap t of halo buffer hb, B stage bs; two 16-deep k-steps, each
+  // a0b0 first, then a0b1 + a1b0 (config 12's per-accumulator order)
+  auto compute = [&](int hb, int bs, int t) {
+    const int kh = t / KW, kw = t - kh * KW;
+    const uint16_t* la = lds + hb * A_EL;
+    const uint16_t* lb = lds + 2 * A_EL + bs * B_EL;
+    int ar[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) ar[i] = ((tmask[i] >> t) & 1) ? wm * WTM + i * 32 + lr + kh * W + kw : HALO_HR;
+#pragma unroll
+    for (int st = 0; st < BK / 16; ++st) {
+      frag_t a[NP][FM], b[NP][FN];
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+          a[p][i] = *reinterpret_cast<const frag_t*>(la + (p * HRA + ar[i]) * BK + pswz<BK, 2>(ar[i], 2 * st + lh) * 8);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          const int row = wn * WTN + j * 32 + lr;
+          b[p][j] = *reinterpret_cast<const frag_t*>(lb + (p * BN + row) * BK + pswz<BK, 2>(row, 2 * st + lh) * 8);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = s3_mf32<2>(a[0][i], b[0][j], acc[i][j]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) {
+          acc[i][j] = s3_mf32<2>(a[0][i], b[1][j], acc[i][j]);
+          acc[i][j] = s3_mf32<2>(a[1][i], b[0][j], acc[i][j]);
+        }
+    }
+  };
+
+  // ---- prologue: the zero rows, slice 0's halo (pass by pass), k-tile 0's B ----
+  if (tid < 16) {
+    // row HALO_HR of both planes of both buffers: 4 x 64 B, 16 B per thread
+    const int buf = tid >> 3, p = (tid >> 2) & 1, sl = tid & 3;
+    *reinterpret_cast<u32x4*>(lds + buf * A_EL + (p * HRA + HALO_HR) * BK + sl * 8) = u32x4{0u, 0u, 0u, 0u};
+  }
+  glds_b(0, 0);
+#pragma unroll
+  for (int p = 0; p < A_PASS; ++p) {
+    load_pass(0, p);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    launder_pass();
+    if (p == 0) {
+      // the record's wave max, with shuffle addresses from an opaque lane id:
+      // amax_reduce's would be shared with the epilogue's amax_publish and held
+      // (spilled) through the whole k-loop
+      uint32_t u = a_amax_w;
+      const int lo = s3_opaque(lane);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((lo ^ o) << 2, (int)u);
+        u = v > u ? v : u;
+      }
+      const int e = __builtin_amdgcn_readfirstlane(h2_exp(__uint_as_float(u)));
+      a_sc = __int_as_float((127 + e) << 23);
+      a_isc = __int_as_float((127 - e) << 23);
+    }
+    store_pass(0, p);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+
+  // ---- k-loop: k-tile kt = (slice c, tap t); B stage kt & 1, halo buffer c & 1.
+  // The next slice's halo: pass p loaded in tap p's k-tile (after its B DMA,
+  // landed by the end-of-tile wait) and split into the other buffer at the
+  // start of tap p + 1's (that buffer's last reader was slice c - 1) ----
+  static_assert(A_PASS < 9, "the halo passes must fit in one slice's taps");
+  int c = 0, t = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = c + 1 < nch;
+    glds_b(min(kt + 1, nk - 1), (kt + 1) & 1);
+    if (more && t >= 1 && t <= A_PASS) store_pass((c + 1) & 1, t - 1);
+    if (more && t < A_PASS) load_pass(c + 1, t);
+    compute(c & 1, kt & 1, t);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next B (and a halo pass)
+    launder_pass();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (++t == ntap) {
+      t = 0;
+      ++c;
+    }
+  }
+  __syncthreads();
+  epilogue_store<WM, 4, FM, FN, LDS_U16 / 2, false, EPI>(g, g.C, acc, reinterpret_cast<float*>(lds), m0, n0, a_isc);
+}
+
+// config 13 serves: f16x2, conv A, 3x3 stride 1 pad 1 (output = input size),
+// Cin % 32 == 0, N % 256 == 0, W <= 15, the ResNet's f16x2 flag sets
+static bool h2_halo_ok(const GemmArgs& g) {
+  return g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1 && g.OH == g.H && g.OW == g.W && (g.Cin % 32) == 0 &&
+         (g.N % 256) == 0 && g.W <= (HALO_HR - 256) / 2 - 1 && g.K == 9 * g.Cin && g.col_scale != nullptr &&
+         g.a_amax != nullptr;
+}
+template <int EPI>
+static hipError_t launch_h2_halo_t(const GemmArgs& g, hipStream_t s) {
+  const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / 256;
+  const long long nblk = tiles_m * tiles_n;
+  if (nblk <= 0) return hipSuccess;
+  if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(gemm_h2_halo_kernel<EPI>, dim3((unsigned)nblk), dim3(512), 0, s, g, (int)tiles_n);
+  return hipGetLastError();
+}
+static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s) {
+  switch (ep_flags(g) & (EP_RES | EP_RELU)) {
+    case EP_RELU: return launch_h2_halo_t<H2_EP | EP_RELU>(g, s);
+    case EP_RES | EP_RELU: return launch_h2_halo_t<H2_EP | EP_RES | EP_RELU>(g, s);
+    case EP_RES: return launch_h2_halo_t<H2_EP | EP_RES>(g, s);
+    default: return launch_h2_halo_t<H2_EP>(g, s);
+  }
+}
+
 // config 8 serves dense A (1x1 convs), N % 256 == 0 and the ResNet's flag
 // sets (conv + BN + ReLU, + residual + ReLU, the projection conv; f16x2: any
 // residual / ReLU combination); the rest falls back to the library's pick
@@ -1441,6 +1682,10 @@ static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int
 
 template <int AM>
 static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
+  if constexpr (AM == A_CONV) {
+    if (forced == 13 && h2_halo_ok(g)) return launch_h2_halo(g, s);
+  }
+  if (forced == 13) forced = 0;
   int cfg = pick_h2(g, forced);
   // N % 256 == 0: the 256x256 one-accumulator tile (config 12) everywhere but
   // the short-K residual expansions (K < 256: their epilogue dominates and the

@@ -186,7 +186,7 @@ TILE_SHAPES = [  # shapes that reach each f16x2 config's edges: ragged M, N = 64
 ]
 
 
-@pytest.mark.parametrize("cfg", [3, 4, 7, 8, 9, 10, 11, 12])
+@pytest.mark.parametrize("cfg", [3, 4, 7, 8, 9, 10, 11, 12, 13])
 @pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res", TILE_SHAPES)
 def test_conv2d_h2_tile_configs(cuda, cfg, b, h, w, cin, cout, k, s, p, res):
     """Every f16x2 tile config forced on every shape: fp32-grade vs float64
@@ -199,6 +199,36 @@ def test_conv2d_h2_tile_configs(cuda, cfg, b, h, w, cin, cout, k, s, p, res):
     e = _rel_err(y[live], ref[live], scale[live])
     assert e[0] < 4e-7, (cfg, e)
     assert ops.amax_value(rec[1]) == float(y.abs().max())
+
+
+HALO_SHAPES = [  # stride-1 3x3, Cin % 32 == 0, N % 256 == 0, W <= 15: config 13 serves these
+    (2, 14, 14, 256, 256, 3, 1, 1, False),
+    (3, 7, 7, 512, 512, 3, 1, 1, True),
+    (2, 15, 15, 256, 256, 3, 1, 1, True),   # the widest map the 288-row halo holds
+    (1, 13, 11, 64, 512, 3, 1, 1, False),   # odd sizes, two Cin slices
+    (5, 14, 14, 32, 256, 3, 1, 1, False),   # one Cin slice, ragged M (980 rows)
+]
+
+
+@pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res", HALO_SHAPES)
+def test_conv2d_h2_halo(cuda, b, h, w, cin, cout, k, s, p, res):
+    """Config 13 (halo-staged A: each input pixel fetched once per Cin slice,
+    taps read from the LDS halo, zero row for padding taps and rows past M):
+    the same accuracy bar as every f16x2 conv against float64 and the
+    exact-fp32 core, and the max-|y| record exact."""
+    x, wt, bias, r, ref, scale = _conv_case(cuda, b, h, w, cin, cout, k, s, p, res, seed=13)
+    with ops.tuning(0, s3_cfg=13):
+        y, rec = _run_h2(cuda, x, wt, bias, r, s, p)
+    y = y.cpu()
+    rd = r.to(cuda) if res else None
+    y_f32 = ops.conv2d(x.to(cuda), wt.to(cuda), bias.to(cuda), s, p, rd, True).cpu()
+    live = ref > 0
+    e = _rel_err(y[live], ref[live], scale[live])
+    ef32 = _rel_err(y_f32[live], ref[live], scale[live])
+    print(f"halo {b}x{h}x{w}x{cin}->{cout}: max {e[0]:.3g} mean {e[1]:.3g} | f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
+    assert e[0] <= 1.25 * max(ef32[0], 1e-7) and e[1] <= ef32[1] * 1.05 + 1e-9
+    assert ops.amax_value(rec[1]) == float(y.abs().max())
+    assert bool(torch.isfinite(y).all())
 
 
 def test_h2_persistent_tile_bit_identical(cuda):
