@@ -1295,18 +1295,24 @@ constexpr int H2_EP = EP_SCALE | EP_AMAX | EP_BIAS;
 // 256x256 tile, 8 waves of 128x64 on v_mfma_f32_32x32x16_f16, one accumulator
 // set (ACC1, config 12's arithmetic per product); the next slice's halo goes
 // to the other buffer one 128-row pass per k-tile during the slice's first
-// four.  W <= 15 (halo <= 288 rows; the 14x14 and 7x7 layers).
-constexpr int HALO_HR = 288;  // halo rows; row HALO_HR of each plane is zero
-
-template <int EPI>
+// four.  Instances (waves WM x WN of FM x FN 32x32 tiles, halo rows HR):
+//   <2, 4, 4, 2, 288>  256x256, N % 256 == 0, W <= 15 (the 14x14 / 7x7 layers)
+//   <4, 2, 2, 2, 320>  256x128, N % 128 == 0, W <= 31 (28x28, N = 128)
+//   <4, 2, 2, 1, 384>  256x64,  N % 64 == 0,  W <= 63 (56x56, N = 64), three
+//                      taps per k-step (and barrier): its 12 MFMAs per wave
+//                      and tap are too few to carry a barrier each
+// Row HR of each halo plane is the zero row.
+template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1>
 __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int tiles_n) {
-  constexpr int NP = 2, WM = 2, FM = 4, FN = 2, BK = 32, NT = 512, NW = 8;
-  constexpr int WTM = 128, WTN = 64, BM = 256, BN = 256, SL = BK / 8;
+  constexpr int NP = 2, BK = 32, NT = 512, NW = 8;
+  constexpr int WTM = 32 * FM, WTN = 32 * FN, BM = WTM * WM, BN = WTN * WN, SL = BK / 8;
+  static_assert(WM * WN == NW && BM == 256, "8 waves, 256-row tiles");
   constexpr int HRA = HALO_HR + 1;                  // rows per A plane (+ the zero row)
   constexpr int A_EL = NP * HRA * BK;               // u16 per halo buffer
-  constexpr int B_EL = NP * BN * BK;                // u16 per B stage
+  constexpr int B_TAP = NP * BN * BK;               // u16 of one tap's B planes
+  constexpr int B_EL = TPK * B_TAP;                 // u16 per B stage (TPK taps per barrier)
   constexpr int B_RPI = 64 / SL;                    // plane rows per LDS-DMA wave instruction
-  constexpr int B_INS = NP * BN / B_RPI / NW;       // LDS-DMA instructions per wave per k-tile (4)
+  constexpr int B_INS = NP * BN / B_RPI / NW;       // LDS-DMA instructions per wave per k-tile (4 / 2 / 1)
   constexpr int A_PASS = (HALO_HR + NT / SL - 1) / (NT / SL);  // 128-row passes over the halo (3)
   constexpr int LDS_U16 = 2 * A_EL + 2 * B_EL;
   static_assert(B_INS * NW * B_RPI == NP * BN, "B staging must tile the block");
@@ -1325,29 +1331,34 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   const int tn = wgid % tiles_n, tm = wgid / tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
   const int W = g.W, H = g.H, KW = g.KW, ntap = g.KH * g.KW;
-  const int nch = g.Cin / BK, nk = nch * ntap;
+  const int nch = g.Cin / BK, ngrp = ntap / TPK, nk = nch * ngrp;  // k-step kt = (slice, group of TPK taps)
   const int hoff = g.pad * W + g.pad;  // halo row 0 = input raster index m0 - hoff
 
   // ---- halo loader: thread -> (row t / 4 + 128 pass, 16-B slot pair t % 4);
   // one 128-row pass at a time (8 registers), so the halo of the next slice
   // never holds more than one pass beside the accumulators ----
+  // (TPK > 1: the narrow tiles have the registers to hold every pass at once)
   const int a_slot = tid % SL, a_row = tid / SL;
-  f32x4 ra[2];
+  constexpr int RA_N = TPK == 1 ? 1 : A_PASS;
+  f32x4 ra[RA_N][2];
   auto load_pass = [&](int c, int p) {
     const int hr = a_row + p * (NT / SL);
     const long long q = (long long)m0 - hoff + hr;
     const bool ok = hr < HALO_HR && q >= 0 && q < g.M;
     const f32x4* src = ok ? reinterpret_cast<const f32x4*>(g.A + q * g.Cin + c * BK + a_slot * 8) : s3_zero_page();
-    s3_load2<1>(src, ra);
+    s3_load2<1>(src, ra[TPK == 1 ? 0 : p]);
   };
   auto launder_pass = [&]() {
-    s3_launder(ra[0]);
-    s3_launder(ra[1]);
+#pragma unroll
+    for (int p = 0; p < RA_N; ++p) {
+      s3_launder(ra[p][0]);
+      s3_launder(ra[p][1]);
+    }
   };
   auto store_pass = [&](int buf, int p) {
     const int hr = a_row + p * (NT / SL);
     u32x4 p0, p1;
-    split2h8(ra, a_sc, p0, p1);
+    split2h8(ra[TPK == 1 ? 0 : p], a_sc, p0, p1);
     if (hr < HALO_HR) {
       uint16_t* la = lds + buf * A_EL;
       const int off = hr * BK + pswz<BK, 2>(hr, a_slot) * 8;
@@ -1357,21 +1368,38 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   };
 
   // ---- B planes: LDS-DMA, instruction i of a wave fills plane rows
-  // (i NW + wave) B_RPI .. (N % 256 == 0: every row real): plane i / 2, rows
-  // 128 (i & 1) + 16 wave + lane / 4 ----
+  // prow = (i NW + wave) B_RPI + lane / 4 of the [2][BN] stage (N % BN == 0:
+  // every row real).  256 columns: plane i / 2, rows 128 (i & 1) + prow % 128
+  // off one pointer (rows r and r + 128 share their swizzle); narrower tiles
+  // keep a pointer per instruction ----
   const int b_r = wave * B_RPI + lane / SL;
-  const uint16_t* b_src =
-      reinterpret_cast<const uint16_t*>(g.B) + (long long)(n0 + b_r) * g.ldb + pswz<BK, 2>(b_r, lane % SL) * 8;
-  static_assert(B_INS == 4 && NW * B_RPI == BN / 2, "B DMA map: two instructions per plane");
-  auto glds_b = [&](int kt, int buf) {
-    const int c = kt / ntap, t = kt - c * ntap;
-    const long long koff = (long long)t * g.Cin + c * BK;
-    uint16_t* lb = lds + 2 * A_EL + buf * B_EL;
+  const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
+  static_assert(NW * B_RPI == 128, "one DMA round = 128 plane rows");
+  const uint16_t* b_src[BN == 256 ? 1 : B_INS];
+  if constexpr (BN == 256) {
+    b_src[0] = Bp + (long long)(n0 + b_r) * g.ldb + pswz<BK, 2>(b_r, lane % SL) * 8;
+  } else {
 #pragma unroll
-    for (int i = 0; i < B_INS; ++i)
-      __builtin_amdgcn_global_load_lds(
-          (const void*)(b_src + (i >> 1) * g.b_plane + (long long)(i & 1) * (BN / 2) * g.ldb + koff),
-          (__attribute__((address_space(3))) void*)(lb + (i * NW + wave) * B_RPI * BK), 16, 0, 0);
+    for (int i = 0; i < B_INS; ++i) {
+      const int prow = i * 128 + b_r, p = prow / BN, r = prow - p * BN;
+      b_src[i] = Bp + p * g.b_plane + (long long)(n0 + r) * g.ldb + pswz<BK, 2>(r, lane % SL) * 8;
+    }
+  }
+  auto glds_b = [&](int kt, int buf) {
+    const int c = kt / ngrp, t0 = (kt - c * ngrp) * TPK;
+#pragma unroll
+    for (int u = 0; u < TPK; ++u) {
+      const long long koff = (long long)(t0 + u) * g.Cin + c * BK;
+      uint16_t* lb = lds + 2 * A_EL + buf * B_EL + u * B_TAP;
+#pragma unroll
+      for (int i = 0; i < B_INS; ++i) {
+        const uint16_t* src = BN == 256 ? b_src[0] + (i >> 1) * g.b_plane + (long long)(i & 1) * (BN / 2) * g.ldb
+                                        : b_src[BN == 256 ? 0 : i];
+        __builtin_amdgcn_global_load_lds((const void*)(src + koff),
+                                         (__attribute__((address_space(3))) void*)(lb + (i * NW + wave) * B_RPI * BK),
+                                         16, 0, 0);
+      }
+    }
   };
 
   // ---- the lanes' fragment rows: a 9-bit mask of the taps that stay inside
@@ -1398,10 +1426,10 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
 
   // one k-tile: tap t of halo buffer hb, B stage bs; two 16-deep k-steps, each
   // a0b0 first, then a0b1 + a1b0 (config 12's per-accumulator order)
-  auto compute = [&](int hb, int bs, int t) {
+  auto compute = [&](int hb, int bs, int t, int u) {
     const int kh = t / KW, kw = t - kh * KW;
     const uint16_t* la = lds + hb * A_EL;
-    const uint16_t* lb = lds + 2 * A_EL + bs * B_EL;
+    const uint16_t* lb = lds + 2 * A_EL + bs * B_EL + u * B_TAP;
     int ar[FM];
 #pragma unroll
     for (int i = 0; i < FM; ++i) ar[i] = ((tmask[i] >> t) & 1) ? wm * WTM + i * 32 + lr + kh * W + kw : HALO_HR;
@@ -1471,50 +1499,78 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   // landed by the end-of-tile wait) and split into the other buffer at the
   // start of tap p + 1's (that buffer's last reader was slice c - 1) ----
   static_assert(A_PASS < 9, "the halo passes must fit in one slice's taps");
-  int c = 0, t = 0;
+  int c = 0, tg = 0;
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = c + 1 < nch;
     glds_b(min(kt + 1, nk - 1), (kt + 1) & 1);
-    if (more && t >= 1 && t <= A_PASS) store_pass((c + 1) & 1, t - 1);
-    if (more && t < A_PASS) load_pass(c + 1, t);
-    compute(c & 1, kt & 1, t);
+    if constexpr (TPK == 1) {
+      if (more && tg >= 1 && tg <= A_PASS) store_pass((c + 1) & 1, tg - 1);
+      if (more && tg < A_PASS) load_pass(c + 1, tg);
+    } else {
+      // every pass loaded in the slice's first group, split in its second
+      if (more && tg == 1) {
+#pragma unroll
+        for (int p = 0; p < A_PASS; ++p) store_pass((c + 1) & 1, p);
+      }
+      if (more && tg == 0) {
+#pragma unroll
+        for (int p = 0; p < A_PASS; ++p) load_pass(c + 1, p);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < TPK; ++u) compute(c & 1, kt & 1, tg * TPK + u, u);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next B (and a halo pass)
     launder_pass();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (++t == ntap) {
-      t = 0;
+    if (++tg == ngrp) {
+      tg = 0;
       ++c;
     }
   }
   __syncthreads();
-  epilogue_store<WM, 4, FM, FN, LDS_U16 / 2, false, EPI>(g, g.C, acc, reinterpret_cast<float*>(lds), m0, n0, a_isc);
+  epilogue_store<WM, WN, FM, FN, LDS_U16 / 2, false, EPI>(g, g.C, acc, reinterpret_cast<float*>(lds), m0, n0, a_isc);
 }
 
 // config 13 serves: f16x2, conv A, 3x3 stride 1 pad 1 (output = input size),
-// Cin % 32 == 0, N % 256 == 0, W <= 15, the ResNet's f16x2 flag sets
-static bool h2_halo_ok(const GemmArgs& g) {
-  return g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1 && g.OH == g.H && g.OW == g.W && (g.Cin % 32) == 0 &&
-         (g.N % 256) == 0 && g.W <= (HALO_HR - 256) / 2 - 1 && g.K == 9 * g.Cin && g.col_scale != nullptr &&
-         g.a_amax != nullptr;
+// Cin % 32 == 0, N % 64 == 0 and W within the instance's halo (see above),
+// the ResNet's f16x2 flag sets.  Returns the halo rows of the instance that
+// serves g, 0 if none.
+static int h2_halo_rows(const GemmArgs& g) {
+  if (!(g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1 && g.OH == g.H && g.OW == g.W && (g.Cin % 32) == 0 &&
+        g.K == 9 * g.Cin && g.col_scale != nullptr && g.a_amax != nullptr))
+    return 0;
+  const int need = 256 + 2 * (g.W + 1);
+  if ((g.N % 256) == 0) return need <= 288 ? 288 : 0;
+  if ((g.N % 128) == 0) return need <= 320 ? 320 : 0;
+  if ((g.N % 64) == 0) return need <= 384 ? 384 : 0;
+  return 0;
 }
-template <int EPI>
+template <int EPI, int WM, int WN, int FM, int FN, int HR, int TPK>
 static hipError_t launch_h2_halo_t(const GemmArgs& g, hipStream_t s) {
-  const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / 256;
+  constexpr int BN = 32 * FN * WN;
+  const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(gemm_h2_halo_kernel<EPI>, dim3((unsigned)nblk), dim3(512), 0, s, g, (int)tiles_n);
+  hipLaunchKernelGGL((gemm_h2_halo_kernel<EPI, WM, WN, FM, FN, HR, TPK>), dim3((unsigned)nblk), dim3(512), 0, s, g,
+                     (int)tiles_n);
   return hipGetLastError();
 }
-static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s) {
+template <int WM, int WN, int FM, int FN, int HR, int TPK>
+static hipError_t launch_h2_halo_ep(const GemmArgs& g, hipStream_t s) {
   switch (ep_flags(g) & (EP_RES | EP_RELU)) {
-    case EP_RELU: return launch_h2_halo_t<H2_EP | EP_RELU>(g, s);
-    case EP_RES | EP_RELU: return launch_h2_halo_t<H2_EP | EP_RES | EP_RELU>(g, s);
-    case EP_RES: return launch_h2_halo_t<H2_EP | EP_RES>(g, s);
-    default: return launch_h2_halo_t<H2_EP>(g, s);
+    case EP_RELU: return launch_h2_halo_t<H2_EP | EP_RELU, WM, WN, FM, FN, HR, TPK>(g, s);
+    case EP_RES | EP_RELU: return launch_h2_halo_t<H2_EP | EP_RES | EP_RELU, WM, WN, FM, FN, HR, TPK>(g, s);
+    case EP_RES: return launch_h2_halo_t<H2_EP | EP_RES, WM, WN, FM, FN, HR, TPK>(g, s);
+    default: return launch_h2_halo_t<H2_EP, WM, WN, FM, FN, HR, TPK>(g, s);
   }
+}
+static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s, int hr) {
+  if (hr == 288) return launch_h2_halo_ep<2, 4, 4, 2, 288, 1>(g, s);
+  if (hr == 320) return launch_h2_halo_ep<4, 2, 2, 2, 320, 1>(g, s);
+  return launch_h2_halo_ep<4, 2, 2, 1, 384, 3>(g, s);
 }
 
 // config 8 serves dense A (1x1 convs), N % 256 == 0 and the ResNet's flag
@@ -1682,11 +1738,16 @@ static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int
 
 template <int AM>
 static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
-  // config 13 (halo A) is the pick wherever it serves: the 3x3 256@14 and
-  // 512@7 layers 2.7 % / 1.6 % faster than config 12 at 1280 images
-  // (profiles/r03t_h2_cfg_sweep.txt)
+  // config 13 (halo A) is the pick for N % 256 == 0 and N == 64: the 3x3
+  // 256@14 and 512@7 layers 2.7 % / 1.6 % faster than config 12 at 1280
+  // images (profiles/r03t_h2_cfg_sweep.txt)
   if constexpr (AM == A_CONV) {
-    if ((forced == 0 || forced == 13) && h2_halo_ok(g)) return launch_h2_halo(g, s);
+    // (N == 64 too: the 256x64 instance with three taps per barrier runs the
+    // 64@56 3x3 layers 1.455 -> 1.297 ms; the 256x128 one lost on 128@28,
+    // 0.888 -> 0.922 ms, and stays opt-in; profiles/r03w_h2_cfg_sweep.txt)
+    if (forced == 13 || (forced == 0 && ((g.N % 256) == 0 || g.N == 64))) {
+      if (const int hr = h2_halo_rows(g)) return launch_h2_halo(g, s, hr);
+    }
   }
   if (forced == 13) forced = 0;
   int cfg = pick_h2(g, forced);

@@ -207,6 +207,10 @@ HALO_SHAPES = [  # stride-1 3x3, Cin % 32 == 0, N % 256 == 0, W <= 15: config 13
     (2, 15, 15, 256, 256, 3, 1, 1, True),   # the widest map the 288-row halo holds
     (1, 13, 11, 64, 512, 3, 1, 1, False),   # odd sizes, two Cin slices
     (5, 14, 14, 32, 256, 3, 1, 1, False),   # one Cin slice, ragged M (980 rows)
+    (2, 28, 28, 128, 128, 3, 1, 1, False),  # the 256x128 instance (halo 320 rows)
+    (1, 27, 31, 64, 128, 3, 1, 1, True),    # its widest map
+    (1, 56, 56, 64, 64, 3, 1, 1, False),    # the 256x64 instance (halo 384 rows)
+    (1, 9, 63, 32, 64, 3, 1, 1, True),      # its widest map
 ]
 
 
