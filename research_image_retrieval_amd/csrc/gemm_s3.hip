@@ -1801,6 +1801,197 @@ int launch_gemm_h2_seg2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int ti
   return check_hip(h, e, "gemm_h2_seg2 launch");
 }
 
+// ---- The stem (7x7 / 2, pad 3, NHWC4) + ReLU + 3x3 / 2 max-pool as a halo
+// tile (f16x2) ---------------------------------------------------------------
+// The implicit-GEMM stem reads each input pixel's 16 B once per filter tap
+// that covers it (~12x at stride 2) plus the 64 x 224 weight planes for every
+// 256-row tile (more bytes than the tile's whole input patch).  Here one
+// persistent block per CU keeps both weight planes resident in LDS (loaded
+// once) and, per tile, stages the tile's input patch once: the tile is the
+// same 17 x 15 patch of conv outputs (8 x 7 pooled outputs plus their window
+// halo) as the fused config-7 stem, so its input is a 39 x 35-pixel patch,
+// fetched once (one 16-B load per pixel, zero outside the image) and split
+// into two fp16 planes of 4 channels (8 B per pixel).  The k-loop then reads
+// only LDS and has no barrier: k-step s = taps 4s .. 4s + 3 (16 k), lane half
+// h supplies taps 4s + 2h, 4s + 2h + 1 (one ds_read_b64 each per plane), taps
+// past 49 read a zero pixel (their weight columns are zero as well).  Same
+// per-accumulator products and order as the fused config-7 stem (a0b0 into
+// one set; a0b1, a1b0 into the other; 32x32x16 f16) over taps 0..51 instead of
+// 0..55 (the four dropped k-steps add exact zeros).  The next tile's patch is
+// loaded into registers under the k-loop; the pool epilogue stages the raw
+// accumulators through LDS exactly as the config-7 stem does.
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void stem_pool_halo_kernel(GemmArgs g, int ntiles) {
+  constexpr int NT = 512, NW = 8, BN = 64, HR = 39, HC = 35, HP = HR * HC;  // 1365 patch pixels
+  constexpr int KP = 224, BS = KP + 8;        // weight row (k) length; LDS row stride (u16, padded)
+  constexpr int NKS = 13;                     // k-steps of 4 taps (taps 0..51)
+  constexpr int B_U16 = 2 * BN * BS;          // both weight planes
+  constexpr int A_U16 = 2 * (HP + 1) * 4;     // both patch planes + the zero pixel
+  constexpr int CS = BN + 4;                  // C staging row stride (floats)
+  constexpr int C_U16 = 256 * CS * 2;
+  constexpr int AC_U16 = A_U16 > C_U16 ? A_U16 : C_U16;
+  constexpr int A_PASS = (HP + NT - 1) / NT;  // 3
+  __shared__ __attribute__((aligned(16))) uint16_t lds[B_U16 + AC_U16];
+  uint16_t* lb = lds;
+  uint16_t* la = lds + B_U16;
+  float* ct = reinterpret_cast<float*>(lds + B_U16);
+  typedef f16x8 frag_t;
+  typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int lr = lane & 31, lh = lane >> 5;
+  const uint32_t a_amax_w = amax_load_slot(g.a_amax);
+  float a_sc, a_isc;
+  {
+    uint32_t u = a_amax_w;
+    const int lo = s3_opaque(lane);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((lo ^ o) << 2, (int)u);
+      u = v > u ? v : u;
+    }
+    const int e = __builtin_amdgcn_readfirstlane(h2_exp(__uint_as_float(u)));
+    a_sc = __int_as_float((127 + e) << 23);
+    a_isc = __int_as_float((127 - e) << 23);
+  }
+
+  // ---- both weight planes into LDS, once: [plane][n][k], rows padded ----
+  {
+    const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
+    for (int i = tid; i < 2 * BN * (KP / 8); i += NT) {
+      const int row = i / (KP / 8), c8 = i - row * (KP / 8);  // row = plane * 64 + n
+      const int p = row / BN, n = row - p * BN;
+      *reinterpret_cast<u32x4*>(lb + row * BS + c8 * 8) =
+          *reinterpret_cast<const u32x4*>(Bp + p * g.b_plane + (long long)n * g.ldb + c8 * 8);
+    }
+  }
+
+  const int tpi = g.pool_tr * g.pool_tc;
+  // the patch of tile tl: pixel p -> input (32 pr - 5 + p / 35, 28 pc - 5 + p % 35)
+  f32x4 px[A_PASS];
+  auto load_patch = [&](int tl) {
+    const int b = tl / tpi, t2 = tl - b * tpi, pr = t2 / g.pool_tc, pc = t2 - pr * g.pool_tc;
+#pragma unroll
+    for (int q = 0; q < A_PASS; ++q) {
+      const int p = tid + q * NT, hr = p / HC, hc = p - hr * HC;
+      const int ih = 32 * pr - 5 + hr, iw = 28 * pc - 5 + hc;
+      const bool ok = tl < ntiles && p < HP && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const f32x4* src = ok ? reinterpret_cast<const f32x4*>(g.A + (((long long)b * g.H + ih) * g.W + iw) * 4)
+                            : s3_zero_page();
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(px[q]) : "v"(src) : "memory");
+    }
+  };
+  auto store_patch = [&]() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int q = 0; q < A_PASS; ++q) {
+      asm volatile("" : "+v"(px[q]));
+      const int p = tid + q * NT;
+      const f32x4 v = px[q] * a_sc;
+      const f16x4 hi = __builtin_convertvector(v, f16x4);
+      const f16x4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), f16x4);
+      if (p < HP) {
+        *reinterpret_cast<f16x4*>(la + p * 4) = hi;
+        *reinterpret_cast<f16x4*>(la + (HP + 1) * 4 + p * 4) = lo;
+      }
+    }
+    if (tid < 2) *reinterpret_cast<uint2*>(la + tid * (HP + 1) * 4 + HP * 4) = uint2{0u, 0u};  // the zero pixel
+  };
+
+  // lane rows: wave w owns tile rows 32 w .. +31; row r -> conv output (q, c) =
+  // (r / 15, r % 15) of the patch, input pixel of tap (kh, kw) = (2q + kh) 35 + 2c + kw
+  const int row = wave * 32 + lr, rq = row / 15, rc = row - rq * 15;
+  const int pbase = row < 255 ? (2 * rq) * HC + 2 * rc : -1;
+
+  float am = 0.f;
+  const int G = gridDim.x;
+  int tl = blockIdx.x;
+  load_patch(tl);
+  store_patch();
+  __syncthreads();
+  for (; tl < ntiles; tl += G) {
+    load_patch(tl + G);  // the next tile's patch lands under this tile's k-loop
+    f32x16 hi[2], lo[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) hi[j][r] = lo[j][r] = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      frag_t a[2], b[2][2];
+      const int t0 = 4 * ks + 2 * lh;
+      int pix[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const int t = t0 + u, kh = t / 7, kw = t - kh * 7;
+        pix[u] = (pbase >= 0 && t < 49) ? pbase + kh * HC + kw : HP;
+      }
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        const uint16_t* pl = la + p * (HP + 1) * 4;
+        const f16x4 x0 = *reinterpret_cast<const f16x4*>(pl + pix[0] * 4);
+        const f16x4 x1 = *reinterpret_cast<const f16x4*>(pl + pix[1] * 4);
+        a[p] = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          b[p][j] = *reinterpret_cast<const frag_t*>(lb + (p * BN + 32 * j + lr) * BS + 16 * ks + 8 * lh);
+      }
+#pragma unroll
+      for (int j = 0; j < 2; ++j) hi[j] = s3_mf32<2>(a[0], b[0][j], hi[j]);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        lo[j] = s3_mf32<2>(a[0], b[1][j], lo[j]);
+        lo[j] = s3_mf32<2>(a[1], b[0][j], lo[j]);
+      }
+    }
+    __syncthreads();  // every wave done with the patch: its LDS becomes the C staging
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        ct[(wave * 32 + acc_row<false>(0, r, lane)) * CS + acc_col<false>(j, r, lane)] = hi[j][r] + lo[j][r];
+    __syncthreads();
+    // the pooled outputs of the tile: max over the window's in-map conv
+    // outputs of the raw accumulators, then scale, bias, ReLU (all monotone)
+    {
+      const int b = tl / tpi, t2 = tl - b * tpi, pr = t2 / g.pool_tc, pc = t2 - pr * g.pool_tc;
+      constexpr int C4 = BN / 4;
+      for (int it = tid; it < 56 * C4; it += NT) {
+        const int qd = it / C4, c4 = it - qd * C4, pi = qd / 7, pj = qd - 7 * pi;
+        const int ph = 8 * pr + pi, pw = 7 * pc + pj;
+        if (ph >= g.POH || pw >= g.POW) continue;
+        f32x4 mx = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+#pragma unroll
+        for (int dr = -1; dr <= 1; ++dr)
+#pragma unroll
+          for (int dc = -1; dc <= 1; ++dc) {
+            const int oh = 2 * ph + dr, ow = 2 * pw + dc;
+            if ((unsigned)oh >= (unsigned)g.OH || (unsigned)ow >= (unsigned)g.OW) continue;
+            const f32x4 v = *reinterpret_cast<const f32x4*>(ct + ((2 * pi + dr + 1) * 15 + 2 * pj + dc + 1) * CS + c4 * 4);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) mx[e] = __builtin_fmaxf(mx[e], v[e]);
+          }
+        const f32x4 sc = *reinterpret_cast<const f32x4*>(g.col_scale + c4 * 4) * a_isc;
+        const f32x4 bv = g.bias != nullptr ? *reinterpret_cast<const f32x4*>(g.bias + c4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = __builtin_fmaxf(mx[e] * sc[e] + bv[e], 0.f);
+          am = amax_acc(am, o[e]);
+        }
+        *reinterpret_cast<f32x4*>(g.pool_out + (((long long)b * g.POH + ph) * g.POW + pw) * BN + c4 * 4) = o;
+      }
+    }
+    __syncthreads();  // the staging read: the next patch may overwrite it
+    store_patch();
+    __syncthreads();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr ((EPI & EP_AMAX) != 0) {
+    if (g.c_amax != nullptr) amax_publish(g.c_amax, am, blockIdx.x * NW + wave);
+  }
+}
+
 int launch_stem_pool_h2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int timer_cls) {
   if (g.N != 64 || g.Cin != 4 || g.K % 32 || g.K < g.KH * g.KW * 4 || g.relu != 1 || g.residual != nullptr ||
       g.col_scale == nullptr || g.a_amax == nullptr || g.pool_out == nullptr || g.POH <= 0 || g.POW <= 0 ||
@@ -1815,7 +2006,14 @@ int launch_stem_pool_h2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int ti
   hipError_t e;
   {
     TimedLaunch tl(h, timer_cls, s);
-    e = launch_s3_t<8, 1, 1, 2, 16, A_CONV_C4, 4, 0, H2_EP | EP_RELU, 2, 2, 1>(q, s, device_cu_count(h), 0);
+    // the halo stem (7x7 / 2, pad 3; s3_cfg 7 forces the implicit-GEMM one)
+    if (h->tune.s3_cfg != 7 && g.KH == 7 && g.KW == 7 && g.stride == 2 && g.pad == 3 && g.K == 224 && g.ldb == 224) {
+      const int grid = (int)std::min<long long>(tiles, device_cu_count(h));
+      hipLaunchKernelGGL((stem_pool_halo_kernel<H2_EP | EP_RELU>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles);
+      e = hipGetLastError();
+    } else {
+      e = launch_s3_t<8, 1, 1, 2, 16, A_CONV_C4, 4, 0, H2_EP | EP_RELU, 2, 2, 1>(q, s, device_cu_count(h), 0);
+    }
   }
   return check_hip(h, e, "stem_pool_h2 launch");
 }

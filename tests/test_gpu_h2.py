@@ -358,10 +358,16 @@ def test_stem_pool_h2_bit_identical(cuda, b, h, w):
     ops.amax_f32(x4, rec[0])
     y = ops.conv2d_h2(x4, rec[0], wc, bias, 2, 3, None, True, rec[1])
     ref = ops.maxpool2d(y, 3, 2, 1)
-    got = ops.stem_pool_h2(x4, rec[0], wc, bias, 2, 3, rec[2])
-    assert got.shape == ref.shape
-    assert torch.equal(got.view(torch.int32), ref.view(torch.int32))
-    assert ops.amax_value(rec[2]) == ops.amax_value(rec[1])
+    # default: the persistent halo stem (resident weights, one patch fetch per
+    # tile); s3_cfg 7: the implicit-GEMM config-7 stem — the same products
+    # and per-accumulator order, so both match the unfused bits
+    for cfg in (0, 7):
+        rec[2].zero_()
+        with ops.tuning(cuda.index, s3_cfg=cfg):
+            got = ops.stem_pool_h2(x4, rec[0], wc, bias, 2, 3, rec[2])
+        assert got.shape == ref.shape
+        assert torch.equal(got.view(torch.int32), ref.view(torch.int32)), cfg
+        assert ops.amax_value(rec[2]) == ops.amax_value(rec[1])
 
 
 def test_resnet_h2_fused_stem_pool_bit_identical(cuda):

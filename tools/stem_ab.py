@@ -1,5 +1,6 @@
 """The ResNet stem at B images, 224x224: f16x2 conv + ReLU then the max-pool
-(two launches) vs rr_stem_pool_h2 (one), interleaved, median ms; outputs
+(two launches) vs rr_stem_pool_h2 (one launch: the halo stem by default, the
+implicit-GEMM config-7 stem with s3_cfg 7), interleaved, median ms; outputs
 compared bit for bit.  usage: stem_ab.py [B]"""
 import os
 import statistics
@@ -30,6 +31,11 @@ def one():
     return ops.stem_pool_h2(x, rec[0], wc, bias, 2, 3, rec[1])
 
 
+def one_cfg7():
+    with ops.tuning(0, s3_cfg=7):
+        return ops.stem_pool_h2(x, rec[0], wc, bias, 2, 3, rec[1])
+
+
 def timed(fn, reps=5):
     fn()
     st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -41,11 +47,13 @@ def timed(fn, reps=5):
     return st.elapsed_time(en) / reps
 
 
-t = {"conv+maxpool": [], "stem_pool": []}
+t = {"conv+maxpool": [], "stem_pool (halo)": [], "stem_pool (config 7)": []}
 for _ in range(5):
     t["conv+maxpool"].append(timed(two))
-    t["stem_pool"].append(timed(one))
-same = torch.equal(two().view(torch.int32), one().view(torch.int32))
+    t["stem_pool (halo)"].append(timed(one))
+    t["stem_pool (config 7)"].append(timed(one_cfg7))
+same = torch.equal(two().view(torch.int32), one().view(torch.int32)) and \
+    torch.equal(two().view(torch.int32), one_cfg7().view(torch.int32))
 fl = 2.0 * B * 112 * 112 * 64 * 7 * 7 * 3
 for k, v in t.items():
     m = statistics.median(v)
