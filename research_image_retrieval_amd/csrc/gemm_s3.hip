@@ -1573,399 +1573,6 @@ static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s, int hr) {
   return launch_h2_halo_ep<4, 2, 2, 1, 384, 3>(g, s);
 }
 
-// ---- Residual expansions with the epilogue pipelined into the next tile
-// (config 14, f16x2, gemm_h2_rp_kernel) ---------------------------------------
-// A 1x1 conv with a residual (conv3 of every bottleneck: y = ReLU(W h + b +
-// x)) is HBM-bound, but at one block per CU its tile's k-loop (MFMA) and its
-// epilogue (residual read + output write) run one after the other: measured,
-// time ~ MFMA time + HBM time (profiles/r03x_resid_stagger_ab.txt).  Here the
-// persistent config-8 tile (128x256, 8 waves of 64x64, 16x16x32 f16, the A / B
-// stream running across tile boundaries) keeps two accumulator sets and uses
-// them alternately from tile to tile (one accumulator per tile, configs 10-12's
-// arithmetic: a0b1, a1b0, a0b0 per k-tile).  Tile t's epilogue runs during
-// tile t + 1's first four k-iterations, one 32-row chunk per iteration (row
-// band c of both wave rows): the chunk's residual rows arrive by LDS-DMA one
-// iteration ahead into one of two 32 KB LDS buffers (the LDS the config-8
-// epilogue staged C in), each lane reads its 16 values in the accumulator
-// layout (16-B slots XOR-swizzled by row so the four row groups of a read hit
-// different banks), applies scale, bias, residual and ReLU in registers and
-// stores dwords straight from the accumulator layout (64-B runs).  The stores
-// go out at the start of an iteration, before its loads: a counted vmcnt wait
-// only counts loads issued after the last store (so it is never short).
-// K % 64 == 0, K >= 128 (the four chunks need four k-iterations).
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm_h2_rp_kernel(GemmArgs g, int tiles_n, int ntiles) {
-  static_assert((EPI & EP_RES) && (EPI & EP_SCALE), "residual epilogue, f16x2");
-  typedef f16x8 frag_t;
-  constexpr int NP = 2, WM = 2, FM = 2, FN = 2, BK = 32, NT = 512, NW = 8;
-  constexpr int WTM = 64, WTN = 64, BM = 128, BN = 256, SL = BK / 8;
-  constexpr int A_EL = NP * BM * BK, BUF = A_EL + NP * BN * BK;  // u16 per stage (48 KB)
-  constexpr int B_INS = NP * BN / (64 / SL) / NW;                // LDS-DMA instructions per wave per k-tile (4)
-  constexpr int A_LD = 2;                                        // A loads per thread per k-tile
-  constexpr int RROWS = 32, RB = RROWS * BN;                     // residual chunk: 32 rows x 256 floats (32 KB)
-  constexpr int R_DMA = RROWS / NW;                              // residual DMA instructions per wave (4)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * BUF + 2 * RB * 2];
-  float* rbuf = reinterpret_cast<float*>(lds + 2 * BUF);  // [2][32][256], 16-B slots swizzled
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave % WM, wn = wave / WM;
-  const int l16 = lane & 15, lg = lane >> 4;
-  const int G = gridDim.x, bid = blockIdx.x;
-  const int nk = g.K / BK;
-  const int my_tiles = (ntiles - bid + G - 1) / G;
-
-  float a_sc, a_isc;
-  {
-    uint32_t u = amax_load_slot(g.a_amax);
-    const int lo = s3_opaque(lane);
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const uint32_t v = (uint32_t)__builtin_amdgcn_ds_bpermute((lo ^ o) << 2, (int)u);
-      u = v > u ? v : u;
-    }
-    const int e = __builtin_amdgcn_readfirstlane(h2_exp(__uint_as_float(u)));
-    a_sc = __int_as_float((127 + e) << 23);
-    a_isc = __int_as_float((127 - e) << 23);
-  }
-
-  auto tile_origin = [&](int tl, int& m0, int& n0) {
-    const int v = bid + tl * G;
-    const int xcd = v & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
-    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
-    const int tn = wgid % tiles_n, tm = wgid / tiles_n;
-    m0 = tm * BM;
-    n0 = tn * BN;
-  };
-
-  // ---- A stream (as config 8): one 8-k chunk of one row per thread, two
-  // k-tiles ahead, across tile boundaries ----
-  const float* a_ptr = g.A;
-  int a_kt = 0, a_tl = 0;
-  auto a_tile = [&](int tl) {
-    int m0, n0;
-    tile_origin(tl, m0, n0);
-    const int t = s3_opaque(tid);
-    const int m = min(m0 + t / SL, g.M - 1);
-    a_ptr = g.A + (long long)m * g.lda + (t % SL) * 8;
-  };
-  a_tile(0);
-  f32x4 ra2[2][2];
-  auto load_a = [&](int rb) __attribute__((always_inline)) {
-    s3_load2<1>(reinterpret_cast<const f32x4*>(a_ptr + a_kt * BK), ra2[rb]);
-    if (++a_kt == nk) {
-      a_kt = 0;
-      a_tile(++a_tl);
-    }
-  };
-  u32x4 pk[NP];
-  auto split_a = [&](int rb) { split2h8(ra2[rb], a_sc, pk[0], pk[1]); };
-  auto write_a = [&](int buf) {
-    uint16_t* la = lds + buf * BUF;
-    const int a_slot = tid % SL, a_row = tid / SL;
-    const int off = a_row * BK + pswz<BK, 2>(a_row, a_slot) * 8;
-#pragma unroll
-    for (int p = 0; p < NP; ++p) *reinterpret_cast<u32x4*>(la + p * BM * BK + off) = pk[p];
-  };
-  auto launder_a = [&](int rb) {
-    s3_launder(ra2[rb][0]);
-    s3_launder(ra2[rb][1]);
-  };
-
-  // ---- B stream (as config 8) ----
-  const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
-  const int b_r = wave * (64 / SL) + lane / SL;
-  const int b_sw = pswz<BK, 2>(b_r, lane % SL) * 8;
-  const uint16_t* b_src = Bp;
-  int b_kt = 0, b_tl = 0;
-  auto b_tile = [&](int tl) {
-    int m0, n0;
-    tile_origin(tl, m0, n0);
-    b_src = Bp + (long long)(n0 + b_r) * g.ldb + b_sw;
-  };
-  b_tile(0);
-  auto glds_b = [&](int buf) __attribute__((always_inline)) {
-    uint16_t* lb = lds + buf * BUF + A_EL;
-#pragma unroll
-    for (int i = 0; i < B_INS; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src + (i >> 1) * g.b_plane + (long long)(i & 1) * (BN / 2) * g.ldb +
-                                                     b_kt * BK),
-                                       (__attribute__((address_space(3))) void*)(lb + (i * NW + wave) * (64 / SL) * BK),
-                                       16, 0, 0);
-    if (++b_kt == nk) {
-      b_kt = 0;
-      b_tile(++b_tl);
-    }
-  };
-
-  // ---- MFMAs (16x16x32 sub-tiles), one accumulator set per tile ----
-  f32x4 acc[2][FM][FN][4];
-  // fragments: every B fragment of the k-tile, the A fragments of one MFMA row
-  // tile at a time (re-read for the a0b0 pass)
-  frag_t fa[NP][2], fb[NP][FN][2];
-  auto rd_a_p = [&](int cur, int i, int p) __attribute__((always_inline)) {
-    const uint16_t* la = lds + cur * BUF;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int row = wm * WTM + i * 32 + h * 16 + l16;
-      fa[p][h] = *reinterpret_cast<const frag_t*>(la + (p * BM + row) * BK + pswz<BK, 2>(row, lg) * 8);
-    }
-  };
-  auto rd_a = [&](int cur, int i) __attribute__((always_inline)) {
-    rd_a_p(cur, i, 0);
-    rd_a_p(cur, i, 1);
-  };
-  auto rd_a0 = [&](int cur, int i) __attribute__((always_inline)) { rd_a_p(cur, i, 0); };
-  auto rd_b = [&](int cur) __attribute__((always_inline)) {
-    const uint16_t* lb = lds + cur * BUF + A_EL;
-#pragma unroll
-    for (int p = 0; p < NP; ++p)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const int row = wn * WTN + j * 32 + h * 16 + l16;
-          fb[p][j][h] = *reinterpret_cast<const frag_t*>(lb + (p * BN + row) * BK + pswz<BK, 2>(row, lg) * 8);
-        }
-  };
-
-  // ---- the pipelined epilogue ----
-  // residual chunk c of tile tl -> rbuf[buf]: chunk row q < 16: tile row 16 c + q,
-  // q >= 16: tile row 64 + 16 c + (q - 16); DMA instruction u of wave w fills
-  // chunk row 8 u + w (one 1 KB row per instruction), lane l -> physical slot
-  // l, logical slot l ^ rsw(q)
-  auto rsw = [](int q) { return ((q >> 2) & 3) << 2; };
-  auto dma_res = [&](int tl, int c, int buf) __attribute__((always_inline)) {
-    int m0, n0;
-    tile_origin(tl, m0, n0);
-    const int te = s3_opaque(tid);
-    const int lane = te & 63, wave = te >> 6;
-#pragma unroll
-    for (int u = 0; u < R_DMA; ++u) {
-      const int q = 8 * u + wave;
-      const int r = (q < 16 ? 0 : 64) + 16 * c + (q & 15);
-      const int m = min(m0 + r, g.M - 1);
-      const float* src = g.residual + (long long)m * g.ldc + n0 + (lane ^ rsw(q)) * 4;
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (__attribute__((address_space(3))) void*)(rbuf + buf * RB + q * BN), 16, 0, 0);
-    }
-  };
-  // the lane's 4 column scales and biases of tile tl (loaded with the chunk-0
-  // residual DMA, one iteration before the epilogue starts)
-  float e_sc[FN][2], e_bi[FN][2];
-  auto load_cols = [&](int tl) __attribute__((always_inline)) {
-    int m0, n0;
-    tile_origin(tl, m0, n0);
-    const int te = s3_opaque(tid);
-    const int l16 = te & 15, wn = (te >> 6) / WM;
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        const int n = n0 + wn * WTN + 32 * j + 16 * b + l16;
-        asm volatile("global_load_dword %0, %1, off" : "=&v"(e_sc[j][b]) : "v"(g.col_scale + n) : "memory");
-        const float* bp = (g.bias != nullptr ? g.bias : g.col_scale) + n;
-        asm volatile("global_load_dword %0, %1, off" : "=&v"(e_bi[j][b]) : "v"(bp) : "memory");
-      }
-  };
-  auto launder_cols = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int b = 0; b < 2; ++b) {
-        asm volatile("" : "+v"(e_sc[j][b]));
-        asm volatile("" : "+v"(e_bi[j][b]));
-        e_sc[j][b] *= a_isc;
-        if (g.bias == nullptr) e_bi[j][b] = 0.f;
-      }
-  };
-  float am = 0.f;
-  // chunk C of tile tl from accumulator set S: 16 values per lane (S and C
-  // compile-time: the accumulators stay registers)
-  auto epi_chunk = [&](auto S_, auto C_, int tl) __attribute__((always_inline)) {
-    constexpr int S = decltype(S_)::value, c = decltype(C_)::value;
-    int m0, n0;
-    tile_origin(tl, m0, n0);
-    constexpr int i = c >> 1, a = c & 1;
-    const float* rb = rbuf + (c & 1) * RB;
-    // lane / wave ids through an opaque copy: address math hoisted out of the
-    // tile loop would stay live through every k-loop (and spill)
-    const int te = s3_opaque(tid);
-    const int l16 = te & 15, lg = (te >> 4) & 3, wm = (te >> 6) % WM, wn = (te >> 6) / WM;
-#pragma unroll
-    for (int j = 0; j < FN; ++j)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int q = wm * 16 + 4 * lg + e;
-          const int r = wm * 64 + 32 * i + 16 * a + 4 * lg + e;
-          const int nl = wn * WTN + 32 * j + 16 * b + l16;
-          const float res = rb[q * BN + (((nl >> 2) ^ rsw(q)) << 2) + (nl & 3)];
-          float v = acc[S][i][j][2 * a + b][e] * e_sc[j][b] + e_bi[j][b] + res;
-          if constexpr ((EPI & EP_RELU) != 0) v = __builtin_fmaxf(v, 0.f);
-          if (m0 + r < g.M) {
-            am = amax_acc(am, v);
-            float* dst = g.C + (long long)(m0 + r) * g.ldc + n0 + nl;
-            asm volatile("global_store_dword %0, %1, off" ::"v"(dst), "v"(v) : "memory");
-          }
-          if (e == 3) __builtin_amdgcn_sched_barrier(0);  // four values live at a time
-        }
-  };
-  auto zero_set = [&](auto S_) __attribute__((always_inline)) {
-    constexpr int S = decltype(S_)::value;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[S][i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
-  };
-
-  // ---- prologue (as config 8) ----
-  load_a(0);
-  glds_b(0);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_INS) : "memory");  // A(0) landed
-  launder_a(0);
-  split_a(0);
-  write_a(0);
-  load_a(1);
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B(0) landed
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-
-  // one k-iteration of local tile tl (set S) at k-tile c, stage cur; with
-  // `prev`, chunk c < 4 of tile tl - 1 (set 1 - S) goes out first
-  // (CC: the chunk as a compile-time value, -1 past the first four iterations)
-  auto iter = [&](auto S_, auto CC_, int tl, int c, int cur, bool prev) __attribute__((always_inline)) {
-    constexpr int S = decltype(S_)::value, CC = decltype(CC_)::value;
-    const bool epi = prev && CC >= 0;
-    if constexpr (CC >= 0) {
-      if (prev) {
-        if (CC == 0) launder_cols();
-        epi_chunk(std::integral_constant<int, 1 - S>(), std::integral_constant<int, CC>(), tl - 1);
-      }
-      __builtin_amdgcn_sched_barrier(0);  // the chunk's registers die before the k-tile's fragments load
-    }
-    // residual DMA: chunk c + 1 of the previous tile, or chunk 0 of this one
-    // (with its column scales / biases) in the tile's last k-iteration
-    const bool rd_prev = epi && c + 1 < 4;
-    const bool rd_own = c == nk - 1 && tl + 1 <= my_tiles;  // the last tile's own epilogue runs after the loop
-    if (rd_prev) dma_res(tl - 1, c + 1, (c + 1) & 1);
-    if (rd_own) {
-      dma_res(tl, 0, 0);
-      load_cols(tl);
-    }
-    glds_b(cur ^ 1);
-    load_a(cur);
-    rd_b(cur);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      rd_a(cur, i);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) {
-          acc[S][i][j][t] = s3_mf16<2>(fa[0][t >> 1], fb[1][j][t & 1], acc[S][i][j][t]);
-          acc[S][i][j][t] = s3_mf16<2>(fa[1][t >> 1], fb[0][j][t & 1], acc[S][i][j][t]);
-        }
-    }
-    // A(k+1) landed: only loads were issued after this iteration's stores
-    if (rd_own) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R_DMA + 2 * FN * 2 + B_INS + A_LD) : "memory");
-    else if (rd_prev) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(R_DMA + B_INS + A_LD) : "memory");
-    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_INS + A_LD) : "memory");
-    launder_a(cur ^ 1);
-    split_a(cur ^ 1);
-#pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      rd_a0(cur, i);
-#pragma unroll
-      for (int j = 0; j < FN; ++j)
-#pragma unroll
-        for (int t = 0; t < 4; ++t) acc[S][i][j][t] = s3_mf16<2>(fa[0][t >> 1], fb[0][j][t & 1], acc[S][i][j][t]);
-    }
-#pragma unroll
-    for (int x = 0; x < FM * FN * 4; ++x) {
-      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // 1 MFMA
-      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);  // 2 VALU
-    }
-    write_a(cur ^ 1);
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // the B DMA and the residual DMA landed
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  };
-  // the k-loop of local tile tl into set S (nk even: stage cur = c & 1)
-  auto tile_loop = [&](auto S_, int tl) __attribute__((always_inline)) {
-    zero_set(S_);
-    const bool prev = tl > 0;
-    iter(S_, std::integral_constant<int, 0>(), tl, 0, 0, prev);
-    iter(S_, std::integral_constant<int, 1>(), tl, 1, 1, prev);
-    iter(S_, std::integral_constant<int, 2>(), tl, 2, 0, prev);
-    iter(S_, std::integral_constant<int, 3>(), tl, 3, 1, prev);
-    for (int c = 4; c < nk; c += 2) {
-      iter(S_, std::integral_constant<int, -1>(), tl, c, 0, prev);
-      iter(S_, std::integral_constant<int, -1>(), tl, c + 1, 1, prev);
-    }
-  };
-  // the last tile's epilogue, with no k-loop to hide in: chunk 0's residual
-  // and the column values were loaded in its last k-iteration
-  auto last_epilogue = [&](auto S_, int tl) __attribute__((always_inline)) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    launder_a(0);
-    launder_a(1);
-    launder_cols();
-    auto one = [&](auto C_) __attribute__((always_inline)) {
-      constexpr int c = decltype(C_)::value;
-      if constexpr (c + 1 < 4) dma_res(tl, c + 1, (c + 1) & 1);
-      epi_chunk(S_, C_, tl);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    };
-    one(std::integral_constant<int, 0>());
-    one(std::integral_constant<int, 1>());
-    one(std::integral_constant<int, 2>());
-    one(std::integral_constant<int, 3>());
-  };
-  int tl = 0;
-  for (; tl + 1 < my_tiles; tl += 2) {
-    tile_loop(std::integral_constant<int, 0>(), tl);
-    tile_loop(std::integral_constant<int, 1>(), tl + 1);
-  }
-  if (tl < my_tiles) {
-    tile_loop(std::integral_constant<int, 0>(), tl);
-    last_epilogue(std::integral_constant<int, 0>(), tl);
-  } else {
-    last_epilogue(std::integral_constant<int, 1>(), tl - 1);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr ((EPI & EP_AMAX) != 0) {
-    if (g.c_amax != nullptr) amax_publish(g.c_amax, am, bid * NW + wave);
-  }
-}
-
-template <int EPI>
-static hipError_t launch_h2_rp_t(GemmArgs g, hipStream_t s, int n_cu) {
-  const long long tiles_m = (g.M + 127) / 128, tiles_n = g.N / 256;
-  const long long ntiles = tiles_m * tiles_n;
-  if (ntiles <= 0) return hipSuccess;
-  if (ntiles * (g.K / 32) > 0x7fffffffLL) return hipErrorInvalidValue;
-  const int slots = std::max(8, n_cu & ~7);
-  const int grid = ntiles <= slots ? (int)ntiles : slots;
-  hipLaunchKernelGGL((gemm_h2_rp_kernel<EPI>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
-  return hipGetLastError();
-}
-// config 14 serves: dense A, N % 256 == 0, a residual, K % 64 == 0, K >= 128
-static bool h2_rp_ok(const GemmArgs& g) {
-  return (g.N % 256) == 0 && g.residual != nullptr && (g.K % 64) == 0 && g.K >= 128 && (g.ldc & 3) == 0 &&
-         g.out_bf16 == 0 && g.relu != 2;
-}
-static hipError_t launch_h2_rp(const GemmArgs& g, hipStream_t s, int n_cu) {
-  if (g.relu == 1) return launch_h2_rp_t<H2_EP | EP_RES | EP_RELU>(g, s, n_cu);
-  return launch_h2_rp_t<H2_EP | EP_RES>(g, s, n_cu);
-}
-
 // config 8 serves dense A (1x1 convs), N % 256 == 0 and the ResNet's flag
 // sets (conv + BN + ReLU, + residual + ReLU, the projection conv; f16x2: any
 // residual / ReLU combination); the rest falls back to the library's pick
@@ -2142,10 +1749,7 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
       if (const int hr = h2_halo_rows(g)) return launch_h2_halo(g, s, hr);
     }
   }
-  if constexpr (AM == A_DENSE) {
-    if (forced == 14 && h2_rp_ok(g)) return launch_h2_rp(g, s, n_cu);
-  }
-  if (forced == 13 || forced == 14) forced = 0;
+  if (forced == 13) forced = 0;
   int cfg = pick_h2(g, forced);
   // N % 256 == 0: the 256x256 one-accumulator tile (config 12) everywhere but
   // the short-K residual expansions (K < 256: their epilogue dominates and the

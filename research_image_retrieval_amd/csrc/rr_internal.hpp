@@ -17,7 +17,7 @@ struct rr_handle_s {
     int gemm_cfg = 0;  // fp32 core: 22, 41 or 88
     int gemm_bk = 0;   // fp32 core k-tile depth: 16 or 32
     int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 / fp8 sweeps), 6 = gallery-in-VGPR bf16 / fp8 filter sweep (sweep_v.hip)
-    int s3_cfg = 0;    // split cores: 1..14 (gemm_s3.hip tile table; 9-14 f16x2 only)
+    int s3_cfg = 0;    // split cores: 1..13 (gemm_s3.hip tile table; 9-13 f16x2 only)
     int s3_stagger = -1;  // split-bf16 core round stagger in ~1 us sleeps (-1: the library's pick)
   } tune;
   int n_cu = 0;  // compute units of the handle's device (device_cu_count)

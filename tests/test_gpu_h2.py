@@ -235,37 +235,6 @@ def test_conv2d_h2_halo(cuda, b, h, w, cin, cout, k, s, p, res):
     assert bool(torch.isfinite(y).all())
 
 
-RP_SHAPES = [  # residual 1x1 convs, N % 256 == 0, K % 64 == 0, K >= 128: config 14 serves these
-    (4, 14, 14, 256, 1024, 1, 1, 0, True),   # 784 rows x 4 column tiles: several tiles per block
-    (3, 21, 19, 128, 512, 1, 1, 0, True),    # K = 128 (the four chunks take every k-iteration), ragged M
-    (2, 7, 7, 512, 2048, 1, 1, 0, True),     # K = 512
-    (1, 3, 5, 256, 256, 1, 1, 0, True),      # a single, mostly empty tile (15 rows)
-    (40, 14, 14, 256, 1024, 1, 1, 0, True),  # 245 x 4 tiles on <= 256 blocks: odd and even tile counts per block
-]
-
-
-@pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res", RP_SHAPES)
-def test_conv2d_h2_residual_pipelined(cuda, b, h, w, cin, cout, k, s, p, res):
-    """Config 14 (the residual expansion with tile t's epilogue pipelined into
-    tile t + 1's k-loop: two accumulator sets, the residual by LDS-DMA one
-    chunk ahead, stores straight from the accumulator layout): the f16x2
-    accuracy bar against float64 and the exact-fp32 core, every row and column
-    written, and the max-|y| record exact."""
-    x, wt, bias, r, ref, scale = _conv_case(cuda, b, h, w, cin, cout, k, s, p, res, seed=14)
-    with ops.tuning(0, s3_cfg=14):
-        y, rec = _run_h2(cuda, x, wt, bias, r, s, p)
-    y = y.cpu()
-    y_f32 = ops.conv2d(x.to(cuda), wt.to(cuda), bias.to(cuda), s, p, r.to(cuda), True).cpu()
-    live = ref > 0
-    e = _rel_err(y[live], ref[live], scale[live])
-    ef32 = _rel_err(y_f32[live], ref[live], scale[live])
-    print(f"rp {b}x{h}x{w}x{cin}->{cout}: max {e[0]:.3g} mean {e[1]:.3g} | f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
-    assert bool(torch.isfinite(y).all())
-    assert bool(((y > 0) == (ref > 0)).float().mean() > 0.999)
-    assert e[0] <= 1.25 * max(ef32[0], 1e-7) and e[1] <= ef32[1] * 1.05 + 1e-9
-    assert ops.amax_value(rec[1]) == float(y.abs().max())
-
-
 def test_h2_persistent_tile_bit_identical(cuda):
     """Config 8 (persistent k-stream), config 9 (three LDS stages) and config
     4 keep the same per-accumulator k order and epilogue arithmetic:
