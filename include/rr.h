@@ -81,11 +81,12 @@ int rr_get_device(rr_handle_t h, int* device);
  *   RR_TUNE_LP_CFG:   bf16/fp8 core, 1 (128x128), 2 (256x64), 3 (256x256),
  *                     4 (256x320 for bf16 filter / score sweeps, 256x256 otherwise),
  *                     5 (bf16 sweeps with K % 128 == 0, fp8 sweeps with K % 256 == 0:
- *                     256x256 8-phase pipeline; otherwise as 3), 6 (bf16 filter sweeps with K % 64 == 0:
- *                     gallery rows in VGPRs, query panel in LDS, sweep_v.hip;
- *                     otherwise the pick)
- *   RR_TUNE_S3_CFG:   split cores (bf16x3 and f16x2), 1..11 (gemm_s3.hip tile table;
- *                     9, 10, 11 f16x2 only)
+ *                     256x256 8-phase pipeline; otherwise as 3), 6 (filter sweeps,
+ *                     bf16 with K % 32 == 0 or fp8 with K % 128 == 0: gallery rows in
+ *                     VGPRs, query panel in LDS, sweep_v.hip; otherwise the pick)
+ *   RR_TUNE_S3_CFG:   split cores (bf16x3 and f16x2), 1..13 (gemm_s3.hip tile table;
+ *                     9..13 f16x2 only; 13 = the halo-staged stride-1 3x3 tile;
+ *                     7 also selects the implicit-GEMM fused stem over the halo stem)
  *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of
  *                     ~1 us for every other resident block (-1 = the library's pick)
  * Any other key or value: RR_EINVAL. */
