@@ -1302,6 +1302,15 @@ constexpr int H2_EP = EP_SCALE | EP_AMAX | EP_BIAS;
 //                      taps per k-step (and barrier): its 12 MFMAs per wave
 //                      and tap are too few to carry a barrier each
 // Row HR of each halo plane is the zero row.
+// Halo rows are read 32 at a time from any row offset r0 + kh W + kw, not from
+// 32-aligned groups, so the row-group swizzle of the other tiles (pswz<32, 2>)
+// conflicts there (PMC: 3.5e7 SQ_LDS_BANK_CONFLICT on the 3x3 256@14 layer,
+// profiles/r03pmc_layer3_sq_counters.txt).  slot ^ ((row >> 2) & 3) keeps every
+// ds_read_b128 lane group on 16 distinct bank quads for every offset: the four
+// rows of a group that share row & 3 differ by {0, 12, 20, 24} or {4, 8, 16,
+// 28}, whose (row >> 2) & 3 are four distinct values whatever the offset.
+__device__ __forceinline__ int hswz(int row, int slot) { return slot ^ ((row >> 2) & 3); }
+
 template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1>
 __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int tiles_n) {
   constexpr int NP = 2, BK = 32, NT = 512, NW = 8;
@@ -1361,7 +1370,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     split2h8(ra[TPK == 1 ? 0 : p], a_sc, p0, p1);
     if (hr < HALO_HR) {
       uint16_t* la = lds + buf * A_EL;
-      const int off = hr * BK + pswz<BK, 2>(hr, a_slot) * 8;
+      const int off = hr * BK + hswz(hr, a_slot) * 8;
       *reinterpret_cast<u32x4*>(la + off) = p0;
       *reinterpret_cast<u32x4*>(la + HRA * BK + off) = p1;
     }
@@ -1440,7 +1449,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
       for (int p = 0; p < NP; ++p) {
 #pragma unroll
         for (int i = 0; i < FM; ++i)
-          a[p][i] = *reinterpret_cast<const frag_t*>(la + (p * HRA + ar[i]) * BK + pswz<BK, 2>(ar[i], 2 * st + lh) * 8);
+          a[p][i] = *reinterpret_cast<const frag_t*>(la + (p * HRA + ar[i]) * BK + hswz(ar[i], 2 * st + lh) * 8);
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
           const int row = wn * WTN + j * 32 + lr;
