@@ -419,11 +419,24 @@ int rr_layernorm_ex(rr_handle_t h, const float* x, long long ldx, int m, int d,
 int rr_patchify(rr_handle_t h, const float* x, int b, int hgt, int wid, int c,
                 int patch, float* y, void* stream);
 
+/* Same, output dtype 0 = fp32, 1 = bf16 (RNE, the rows rr_linear_bf16 reads;
+ * equal to rr_patchify followed by rr_quantize_rows bf16).                 */
+int rr_patchify_ex(rr_handle_t h, const float* x, int b, int hgt, int wid,
+                   int c, int patch, int out_dtype, void* y, void* stream);
+
 /* tokens [b][1+np][width]: row 0 = cls + pos[0], row 1+i = patches[b][i] +
  * pos[1+i]  (class_embedding concat + positional_embedding, :226-227).     */
 int rr_vit_tokens(rr_handle_t h, const float* patches, int b, int npatch,
                   int width, const float* cls, const float* pos, float* y,
                   void* stream);
+
+/* Same with ln_pre (:229) fused when gamma and beta are given (both or
+ * neither; width <= 4096): y = LayerNorm(tokens), bit-identical to
+ * rr_vit_tokens followed by rr_layernorm, without the HBM round trip.      */
+int rr_vit_tokens_ex(rr_handle_t h, const float* patches, int b, int npatch,
+                     int width, const float* cls, const float* pos,
+                     const float* gamma, const float* beta, float eps,
+                     float* y, void* stream);
 
 /* Multi-head self-attention core: qkv [b*seq][3*heads*64] (q | k | v, the
  * in_proj output) -> out [b*seq][heads*64] = softmax(q k^T / 8) v per head

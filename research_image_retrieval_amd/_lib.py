@@ -75,6 +75,8 @@ SIGNATURES = {
     "rr_layernorm": (_i, [_vp, _vp, _ll, _i, _i, _vp, _vp, _f, _vp, _vp]),
     "rr_patchify": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "rr_vit_tokens": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "rr_patchify_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _vp, _vp]),
+    "rr_vit_tokens_ex": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp]),
     "rr_attention": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     "rr_attention_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "rr_attention_bf16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),

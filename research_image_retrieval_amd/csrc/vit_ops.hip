@@ -60,23 +60,15 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 // Same, vectorised for D % 256 == 0 and 16-B aligned rows (ViT width 768):
 // lane l holds the float4s at columns 4l + 256i, so every load and store is
 // one 1-KB (fp32) or 512-B (bf16) coalesced wave instruction.
+// The row body is shared with the fused token-assembly kernel below so both
+// give bit-identical rows.
 template <int NV, typename OutT>
-__global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restrict__ x, long long ldx, int M,
-                                                            const float* __restrict__ gamma,
-                                                            const float* __restrict__ beta, float eps,
-                                                            OutT* __restrict__ y) {
+__device__ __forceinline__ void ln_row_vec(const f32x4 (&v)[NV], int lane, const float* __restrict__ gamma,
+                                           const float* __restrict__ beta, float eps, OutT* __restrict__ yr) {
   constexpr int D = 256 * NV;
-  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (row >= M) return;
-  const float* xr = x + (long long)row * ldx;
-  f32x4 v[NV];
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < NV; ++i) {
-    v[i] = *reinterpret_cast<const f32x4*>(xr + 4 * lane + 256 * i);
-    s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
-  }
+  for (int i = 0; i < NV; ++i) s += (v[i][0] + v[i][1]) + (v[i][2] + v[i][3]);
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   const float mean = s / (float)D;
@@ -91,7 +83,6 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restr
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
   const float rstd = 1.0f / sqrtf(q / (float)D + eps);
-  OutT* yr = y + (long long)row * D;
 #pragma unroll
   for (int i = 0; i < NV; ++i) {
     const int c = 4 * lane + 256 * i;
@@ -109,10 +100,86 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restr
   }
 }
 
+template <int NV, typename OutT>
+__global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restrict__ x, long long ldx, int M,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float eps,
+                                                            OutT* __restrict__ y) {
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (long long)row * ldx;
+  f32x4 v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) v[i] = *reinterpret_cast<const f32x4*>(xr + 4 * lane + 256 * i);
+  ln_row_vec<NV>(v, lane, gamma, beta, eps, y + (long long)row * (256 * NV));
+}
+
+// Token assembly with ln_pre fused (:226-229): one wave per token row, the
+// row (cls or patch embedding, + positional embedding) is formed in registers
+// and normalised there, so the un-normalised tokens never reach HBM.  Same
+// adds and the same LN body as vit_tokens_kernel + layernorm_vec_kernel.
+template <int NV>
+__global__ __launch_bounds__(256) void vit_tokens_ln_kernel(const float* __restrict__ patches, int B, int NP,
+                                                            const float* __restrict__ cls,
+                                                            const float* __restrict__ pos,
+                                                            const float* __restrict__ gamma,
+                                                            const float* __restrict__ beta, float eps,
+                                                            float* __restrict__ y) {
+  constexpr int Wd = 256 * NV;
+  const long long t = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (t >= (long long)B * (NP + 1)) return;
+  const int l = (int)(t % (NP + 1));
+  const long long b = t / (NP + 1);
+  const float* src = l == 0 ? cls : patches + (b * NP + (l - 1)) * Wd;
+  const float* pr = pos + (long long)l * Wd;
+  f32x4 v[NV];
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * lane + 256 * i;
+    v[i] = *reinterpret_cast<const f32x4*>(src + c) + *reinterpret_cast<const f32x4*>(pr + c);
+  }
+  ln_row_vec<NV>(v, lane, gamma, beta, eps, y + t * Wd);
+}
+
+// Vectorised patchify for (P*C) % 4 == 0, (W*C) % 4 == 0 and 16-B aligned
+// buffers (224x224x3, P = 16): each thread moves 4 consecutive outputs, which
+// lie in one (kh) row of the patch and are contiguous in the NHWC input too,
+// so the index math runs once per float4.  OutT = __bf16 writes the rows the
+// bf16 patch GEMM reads directly (RNE, as rr_quantize_rows rounds).
+template <typename OutT>
+__global__ void patchify_vec_kernel(const float* __restrict__ x, int B, int H, int W, int C, int P,
+                                    OutT* __restrict__ y) {
+  const int gh = H / P, gw = W / P;
+  const int pc = P * C;
+  const int kdim4 = P * pc / 4;
+  const long long total4 = (long long)B * gh * gw * kdim4;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long q = (long long)blockIdx.x * blockDim.x + threadIdx.x; q < total4; q += stride) {
+    const long long patch = q / kdim4;
+    const int k = 4 * (int)(q - patch * kdim4);
+    const int kh = k / pc;
+    const int r = k - kh * pc;
+    const int b = (int)(patch / (gh * gw));
+    const int pp = (int)(patch - (long long)b * gh * gw);
+    const int ph = pp / gw, pw = pp - ph * gw;
+    const f32x4 v =
+        *reinterpret_cast<const f32x4*>(x + (((long long)b * H + ph * P + kh) * W + pw * P) * C + r);
+    if constexpr (sizeof(OutT) == 4) {
+      *reinterpret_cast<f32x4*>(y + 4 * q) = v;
+    } else {
+      typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+      *reinterpret_cast<bf16x4*>(y + 4 * q) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+    }
+  }
+}
+
 // NHWC [B][H][W][C] -> patch rows [B*(H/P)*(W/P)][P*P*C] in (kh, kw, c) order,
 // which matches conv weights permuted to [Cout][P][P][C].
+template <typename OutT>
 __global__ void patchify_kernel(const float* __restrict__ x, int B, int H, int W, int C, int P,
-                                float* __restrict__ y) {
+                                OutT* __restrict__ y) {
   const int gh = H / P, gw = W / P;
   const long long kdim = (long long)P * P * C;
   const long long total = (long long)B * gh * gw * kdim;
@@ -127,7 +194,7 @@ __global__ void patchify_kernel(const float* __restrict__ x, int B, int H, int W
     const int b = (int)(patch / (gh * gw));
     const int pp = (int)(patch - (long long)b * gh * gw);
     const int ph = pp / gw, pw = pp - (pp / gw) * gw;
-    y[o] = x[(((long long)b * H + ph * P + kh) * W + pw * P + kw) * C + c];
+    y[o] = (OutT)x[(((long long)b * H + ph * P + kh) * W + pw * P + kw) * C + c];
   }
 }
 
@@ -573,28 +640,70 @@ extern "C" int rr_layernorm_ex(rr_handle_t h, const float* x, long long ldx, int
 
 extern "C" int rr_patchify(rr_handle_t h, const float* x, int b, int hgt, int wid, int c, int patch, float* y,
                            void* stream) {
+  return rr_patchify_ex(h, x, b, hgt, wid, c, patch, 0, y, stream);
+}
+
+template <typename OutT>
+static void launch_patchify(const float* x, int b, int hgt, int wid, int c, int patch, OutT* y, long long total,
+                            hipStream_t s) {
+  const bool vec = (patch * c) % 4 == 0 && (wid * c) % 4 == 0 && (((uintptr_t)x | (uintptr_t)y) & 15) == 0;
+  if (vec)
+    hipLaunchKernelGGL((patchify_vec_kernel<OutT>), grid_for(total / 4, 256), dim3(256), 0, s, x, b, hgt, wid, c,
+                       patch, y);
+  else
+    hipLaunchKernelGGL((patchify_kernel<OutT>), grid_for(total, 256), dim3(256), 0, s, x, b, hgt, wid, c, patch, y);
+}
+
+extern "C" int rr_patchify_ex(rr_handle_t h, const float* x, int b, int hgt, int wid, int c, int patch,
+                              int out_dtype, void* y, void* stream) {
   RR_ENTRY(h);
-  if (!x || !y || b < 0 || c <= 0 || patch <= 0 || hgt % patch || wid % patch)
-    return set_error(h, RR_EINVAL, "rr_patchify: bad argument (H, W must be multiples of the patch)");
+  if (!x || !y || b < 0 || c <= 0 || patch <= 0 || hgt % patch || wid % patch || (out_dtype != 0 && out_dtype != 1))
+    return set_error(h, RR_EINVAL,
+                     "rr_patchify: bad argument (H, W must be multiples of the patch, out_dtype 0|1)");
   const long long total = (long long)b * hgt * wid * c;
   if (total == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeElem, s);
-  hipLaunchKernelGGL(patchify_kernel, grid_for(total, 256), dim3(256), 0, s, x, b, hgt, wid, c, patch, y);
+  if (out_dtype == 1)
+    launch_patchify<__bf16>(x, b, hgt, wid, c, patch, (__bf16*)y, total, s);
+  else
+    launch_patchify<float>(x, b, hgt, wid, c, patch, (float*)y, total, s);
   return check_hip(h, hipGetLastError(), "patchify launch");
 }
 
 extern "C" int rr_vit_tokens(rr_handle_t h, const float* patches, int b, int npatch, int width, const float* cls,
                              const float* pos, float* y, void* stream) {
+  return rr_vit_tokens_ex(h, patches, b, npatch, width, cls, pos, nullptr, nullptr, 0.f, y, stream);
+}
+
+extern "C" int rr_vit_tokens_ex(rr_handle_t h, const float* patches, int b, int npatch, int width, const float* cls,
+                                const float* pos, const float* gamma, const float* beta, float eps, float* y,
+                                void* stream) {
   RR_ENTRY(h);
-  if (!patches || !cls || !pos || !y || b < 0 || npatch <= 0 || width <= 0)
-    return set_error(h, RR_EINVAL, "rr_vit_tokens: bad argument");
-  const long long total = (long long)b * (npatch + 1) * width;
+  if (!patches || !cls || !pos || !y || b < 0 || npatch <= 0 || width <= 0 || (!gamma) != (!beta) ||
+      (gamma && width > 4096))
+    return set_error(h, RR_EINVAL, "rr_vit_tokens: bad argument (gamma and beta both or neither, width <= 4096)");
+  const long long rows = (long long)b * (npatch + 1);
+  const long long total = rows * width;
   if (total == 0) return RR_OK;
   hipStream_t s = (hipStream_t)stream;
   TimedLaunch tl(h, kTimeElem, s);
-  hipLaunchKernelGGL(vit_tokens_kernel, grid_for(total, 256), dim3(256), 0, s, patches, b, npatch, width, cls, pos,
-                     y);
+  const bool vec = (((uintptr_t)patches | (uintptr_t)cls | (uintptr_t)pos | (uintptr_t)y | (uintptr_t)gamma |
+                     (uintptr_t)beta) & 15) == 0;
+  const dim3 grid((unsigned)((rows * 64 + 255) / 256));
+  if (gamma && vec && width == 768) {
+    hipLaunchKernelGGL(vit_tokens_ln_kernel<3>, grid, dim3(256), 0, s, patches, b, npatch, cls, pos, gamma, beta,
+                       eps, y);
+  } else if (gamma && vec && width == 512) {
+    hipLaunchKernelGGL(vit_tokens_ln_kernel<2>, grid, dim3(256), 0, s, patches, b, npatch, cls, pos, gamma, beta,
+                       eps, y);
+  } else {
+    hipLaunchKernelGGL(vit_tokens_kernel, grid_for(total, 256), dim3(256), 0, s, patches, b, npatch, width, cls, pos,
+                       y);
+    // other widths: LayerNorm in place over the assembled rows (each wave
+    // reads its whole row into registers before writing it back)
+    if (gamma) launch_ln<float>((width + 63) / 64, grid, s, y, width, (int)rows, width, gamma, beta, eps, y);
+  }
   return check_hip(h, hipGetLastError(), "vit_tokens launch");
 }
 

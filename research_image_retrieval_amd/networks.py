@@ -350,9 +350,9 @@ class VisionTransformer(_Extractor):
                     blk[k + ".bf16"] = blk[k].to(torch.bfloat16)
 
     def _forward_bf16(self, x_nhwc, b):
-        p, _ = ops.quantize_rows(ops.patchify(x_nhwc, self.patch), "bf16")
-        x = ops.vit_tokens(ops.linear_bf16(p, self.conv_w_bf), b, self.cls, self.pos)
-        x = ops.layernorm(x, *self.ln_pre)
+        # patch rows straight to bf16; ln_pre fused into the token assembly
+        p = ops.patchify(x_nhwc, self.patch, out_bf16=True)
+        x = ops.vit_tokens(ops.linear_bf16(p, self.conv_w_bf), b, self.cls, self.pos, ln=self.ln_pre)
         for blk in self.blocks:
             y = ops.layernorm_bf16(x, blk["ln_1.weight"], blk["ln_1.bias"])
             # QKV rows in bf16 (RNE, exactly as the attention rounds fp32 rows): half the bytes
@@ -373,8 +373,7 @@ class VisionTransformer(_Extractor):
             raise ValueError(f"VisionTransformer: fixed {self.res}x{self.res} input (positional embedding has "
                              f"{self.seq} tokens; networks/model.py:228)")
         x = ops.linear(ops.patchify(x_nhwc, self.patch), self.conv_w)
-        x = ops.vit_tokens(x, b, self.cls, self.pos)
-        x = ops.layernorm(x, *self.ln_pre)
+        x = ops.vit_tokens(x, b, self.cls, self.pos, ln=self.ln_pre)
         for blk in self.blocks:
             y = ops.layernorm(x, blk["ln_1.weight"], blk["ln_1.bias"])
             qkv = ops.linear(y, blk["attn.in_proj_weight"], blk["attn.in_proj_bias"])

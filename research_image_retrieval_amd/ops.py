@@ -596,25 +596,30 @@ def layernorm(x, gamma, beta, eps=1e-5, rows=None, row_stride=None):
     return y
 
 
-def patchify(x_nhwc, patch):
+def patchify(x_nhwc, patch, out_bf16=False):
+    """NHWC image -> patch rows (fp32, or bf16 RNE for the bf16 patch GEMM)."""
     _f32(x_nhwc, "patchify")
     dev = _dev(x_nhwc)
     b, h, w, c = x_nhwc.shape
-    y = torch.empty((b * (h // patch) * (w // patch), patch * patch * c), dtype=torch.float32, device=x_nhwc.device)
+    y = torch.empty((b * (h // patch) * (w // patch), patch * patch * c),
+                    dtype=torch.bfloat16 if out_bf16 else torch.float32, device=x_nhwc.device)
     hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_patchify(hd, _ptr(x_nhwc), b, h, w, c, patch, _ptr(y), _stream(dev)), hd, "rr_patchify")
+    _lib.check(_lib.lib().rr_patchify_ex(hd, _ptr(x_nhwc), b, h, w, c, patch, int(out_bf16), _ptr(y), _stream(dev)),
+               hd, "rr_patchify_ex")
     return y
 
 
-def vit_tokens(patches, b, cls, pos):
+def vit_tokens(patches, b, cls, pos, ln=None, eps=1e-5):
+    """[cls; patches] + pos per image; with ln = (gamma, beta), ln_pre fused."""
     _f32(patches, "vit_tokens")
     dev = _dev(patches)
     width = patches.shape[1]
     npatch = patches.shape[0] // b
     y = torch.empty((b * (npatch + 1), width), dtype=torch.float32, device=patches.device)
     hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_vit_tokens(hd, _ptr(patches), b, npatch, width, _ptr(cls), _ptr(pos), _ptr(y),
-                                        _stream(dev)), hd, "rr_vit_tokens")
+    gamma, beta = ln if ln is not None else (None, None)
+    _lib.check(_lib.lib().rr_vit_tokens_ex(hd, _ptr(patches), b, npatch, width, _ptr(cls), _ptr(pos), _ptr(gamma),
+                                           _ptr(beta), float(eps), _ptr(y), _stream(dev)), hd, "rr_vit_tokens_ex")
     return y
 
 

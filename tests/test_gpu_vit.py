@@ -63,6 +63,42 @@ def test_layernorm_and_quickgelu(cuda):
                                rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("b,h,w,c,p", [(3, 224, 224, 3, 16), (2, 32, 48, 3, 16), (2, 30, 20, 5, 10),
+                                       (1, 16, 16, 4, 4)])
+def test_patchify_fp32_and_bf16(cuda, b, h, w, c, p):
+    """patchify (vectorised when p*c and w*c are multiples of 4, else scalar)
+    against torch's unfold order (kh, kw, c); the bf16 form is bit-identical
+    to patchify fp32 + quantize_rows bf16."""
+    x = torch.randn(b, h, w, c, generator=torch.Generator().manual_seed(h * w + c))
+    ref = x.view(b, h // p, p, w // p, p, c).permute(0, 1, 3, 2, 4, 5).reshape(-1, p * p * c)
+    got = ops.patchify(x.to(cuda), p)
+    assert torch.equal(got.cpu(), ref)
+    got16 = ops.patchify(x.to(cuda), p, out_bf16=True)
+    q, _ = ops.quantize_rows(got, "bf16")
+    assert got16.dtype == torch.bfloat16 and torch.equal(got16.cpu(), q.cpu())
+    assert torch.equal(got16.cpu(), ref.to(torch.bfloat16))
+
+
+@pytest.mark.parametrize("b,npatch,width", [(3, 196, 768), (2, 49, 512), (2, 16, 384), (1, 5, 200)])
+def test_vit_tokens_ln_pre_fused(cuda, b, npatch, width):
+    """tokens + ln_pre in one kernel (widths 512 / 768) or tokens then an in-
+    place LayerNorm (other widths): bit-identical to vit_tokens followed by
+    layernorm, and within 1e-5 of torch float64."""
+    g = torch.Generator().manual_seed(width + npatch)
+    pt = torch.randn(b * npatch, width, generator=g)
+    cls, pos = torch.randn(width, generator=g), torch.randn(npatch + 1, width, generator=g)
+    gm, bt = torch.randn(width, generator=g), torch.randn(width, generator=g)
+    d = [t.to(cuda) for t in (pt, cls, pos, gm, bt)]
+    plain = ops.vit_tokens(d[0], b, d[1], d[2])
+    fused = ops.vit_tokens(d[0], b, d[1], d[2], ln=(d[3], d[4]))
+    two = ops.layernorm(plain, d[3], d[4])
+    assert torch.equal(fused.cpu(), two.cpu())
+    tok = torch.cat([cls.expand(b, 1, width), pt.view(b, npatch, width)], 1) + pos
+    assert torch.equal(plain.cpu(), tok.reshape(-1, width))
+    ref = torch.nn.functional.layer_norm(tok.double(), (width,), gm.double(), bt.double(), 1e-5).float()
+    torch.testing.assert_close(fused.cpu(), ref.reshape(-1, width), rtol=1e-5, atol=1e-5)
+
+
 @pytest.mark.parametrize("seq", [197, 50, 256, 31])
 def test_attention_bf16_kernel_vs_float64(cuda, seq):
     """bf16-MFMA attention (C4): q/k/v and P rounded to bf16, fp32 softmax.
