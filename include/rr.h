@@ -312,7 +312,10 @@ int rr_split3_bf16(rr_handle_t h, const float* x, long long n, void* planes,
  * (optional, zeroed by the caller): receives max |y| over the finite stored
  * values.  Needs cin % 32 == 0, or cin == 4 for the NHWC4 stem (w2 then holds
  * the flattened [kh][kw][4] filter zero-padded to K = kh*kw*4 rounded up to
- * 32).  Replaces the same reference ops as rr_conv2d
+ * 32).  y, bias and residual must be 16-byte aligned (RR_EINVAL otherwise).
+ * The split scale of x is one per tensor: values more than 2^18 below its
+ * max keep an absolute error <= 2^-40 max|x| instead of full relative
+ * precision.  Replaces the same reference ops as rr_conv2d
  * (networks/backbone.py:103-109, :305-346; models/gem_pooling.py:44,61).    */
 int rr_conv2d_h2(rr_handle_t h, const float* x, const unsigned* x_amax, int b,
                  int hgt, int wid, int cin, const void* w2,

@@ -405,6 +405,9 @@ int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, c
   }
   if (amode != A_CONV_GENERIC && (((uintptr_t)x & 15) || ((uintptr_t)w & 15)))
     return set_error(h, RR_EINVAL, "rr_conv2d: x/w must be 16-byte aligned");
+  // cout % 4 == 0: the epilogue's vector path (f32x4 bias, 16-byte C / residual rows)
+  if ((cout & 3) == 0 && (((uintptr_t)y & 15) || (bias && ((uintptr_t)bias & 15)) || (residual && ((uintptr_t)residual & 15))))
+    return set_error(h, RR_EINVAL, "rr_conv2d: bias/residual/y must be 16-byte aligned");
   return launch_gemm(h, amode, E_STORE, g, (hipStream_t)stream, kTimeGemm);
 }
 
@@ -421,6 +424,9 @@ int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin
   const long long M = (long long)b * oh * ow;
   if (M > 0x7fffffffLL) return set_error(h, RR_EINVAL, "rr_conv2d_s3: too many output pixels");
   if (((uintptr_t)x & 15) || ((uintptr_t)w3 & 15)) return set_error(h, RR_EINVAL, "rr_conv2d_s3: x/w3 must be 16-byte aligned");
+  // cout % 4 == 0: the epilogue's vector path (f32x4 bias, 16-byte C / residual rows)
+  if ((cout & 3) == 0 && (((uintptr_t)y & 15) || (bias && ((uintptr_t)bias & 15)) || (residual && ((uintptr_t)residual & 15))))
+    return set_error(h, RR_EINVAL, "rr_conv2d_s3: bias/residual/y must be 16-byte aligned");
   GemmArgs g;
   g.A = x;
   g.M = (int)M;
@@ -463,8 +469,11 @@ int rr_conv2d_h2(rr_handle_t h, const float* x, const unsigned* x_amax, int b, i
   if (oh <= 0 || ow <= 0) return set_error(h, RR_EINVAL, "rr_conv2d_h2: empty output");
   const long long M = (long long)b * oh * ow;
   if (M > 0x7fffffffLL) return set_error(h, RR_EINVAL, "rr_conv2d_h2: too many output pixels");
-  if (((uintptr_t)x & 15) || ((uintptr_t)w2 & 15) || ((uintptr_t)w_iscale & 15))
-    return set_error(h, RR_EINVAL, "rr_conv2d_h2: x/w2/w_iscale must be 16-byte aligned");
+  // the epilogues load bias / col_scale as f32x4 and store C / read the
+  // residual in 16-byte pieces
+  if (((uintptr_t)x & 15) || ((uintptr_t)w2 & 15) || ((uintptr_t)w_iscale & 15) || ((uintptr_t)y & 15) ||
+      (bias && ((uintptr_t)bias & 15)) || (residual && ((uintptr_t)residual & 15)))
+    return set_error(h, RR_EINVAL, "rr_conv2d_h2: x/w2/w_iscale/bias/residual/y must be 16-byte aligned");
   GemmArgs g;
   g.A = x;
   g.M = (int)M;
@@ -558,8 +567,9 @@ int rr_bottleneck_out_h2(rr_handle_t h, const float* y, const unsigned* y_amax, 
   const long long M = (long long)b * oh * ow;
   if (M > 0x7fffffffLL || (long long)b * hx * wx > 0x7fffffffLL)
     return set_error(h, RR_EINVAL, "rr_bottleneck_out_h2: too many pixels");
-  if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || ((uintptr_t)w2 & 15) || ((uintptr_t)w_iscale & 15))
-    return set_error(h, RR_EINVAL, "rr_bottleneck_out_h2: y/x/w2/w_iscale must be 16-byte aligned");
+  if (((uintptr_t)y & 15) || ((uintptr_t)x & 15) || ((uintptr_t)w2 & 15) || ((uintptr_t)w_iscale & 15) ||
+      ((uintptr_t)out & 15) || (bias && ((uintptr_t)bias & 15)))
+    return set_error(h, RR_EINVAL, "rr_bottleneck_out_h2: y/x/w2/w_iscale/bias/out must be 16-byte aligned");
   GemmArgs g;
   g.A = y;
   g.lda = planes;

@@ -18,24 +18,14 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 // One wave per row: y = (x - mean) / sqrt(var + eps) * gamma + beta, biased
-// variance, two-pass over the row held in registers (D <= 64 * 64).
+// variance, two-pass over the row held in registers (D <= 64 * 64).  The row
+// body is shared with the generic-width fused token assembly below.
 template <int PER_LANE, typename OutT>
-__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, long long ldx, int M, int D,
-                                                        const float* __restrict__ gamma,
-                                                        const float* __restrict__ beta, float eps,
-                                                        OutT* __restrict__ y) {
-  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const int lane = threadIdx.x & 63;
-  if (row >= M) return;
-  const float* xr = x + (long long)row * ldx;
-  float v[PER_LANE];
+__device__ __forceinline__ void ln_row(const float (&v)[PER_LANE], int lane, int D, const float* __restrict__ gamma,
+                                       const float* __restrict__ beta, float eps, OutT* __restrict__ yr) {
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < PER_LANE; ++i) {
-    const int c = lane + 64 * i;
-    v[i] = c < D ? xr[c] : 0.f;
-    s += v[i];
-  }
+  for (int i = 0; i < PER_LANE; ++i) s += v[i];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
   const float mean = s / (float)D;
@@ -49,12 +39,57 @@ __global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict_
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off, 64);
   const float rstd = 1.0f / sqrtf(q / (float)D + eps);
-  OutT* yr = y + (long long)row * D;
 #pragma unroll
   for (int i = 0; i < PER_LANE; ++i) {
     const int c = lane + 64 * i;
     if (c < D) yr[c] = (OutT)((v[i] - mean) * rstd * gamma[c] + beta[c]);
   }
+}
+
+template <int PER_LANE, typename OutT>
+__global__ __launch_bounds__(256) void layernorm_kernel(const float* __restrict__ x, long long ldx, int M, int D,
+                                                        const float* __restrict__ gamma,
+                                                        const float* __restrict__ beta, float eps,
+                                                        OutT* __restrict__ y) {
+  const int row = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (row >= M) return;
+  const float* xr = x + (long long)row * ldx;
+  float v[PER_LANE];
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < D ? xr[c] : 0.f;
+  }
+  ln_row<PER_LANE>(v, lane, D, gamma, beta, eps, y + (long long)row * D);
+}
+
+// Token assembly with ln_pre fused for any width <= 4096 (the 512 / 768
+// vectorised forms are vit_tokens_ln_kernel below): the row (cls or patch
+// embedding, + positional embedding) is formed in registers and normalised
+// there, with layernorm_kernel's row body — the same bits as assembling the
+// tokens and normalising them in a separate pass, without writing y twice.
+template <int PER_LANE>
+__global__ __launch_bounds__(256) void vit_tokens_ln_generic_kernel(const float* __restrict__ patches, int B, int NP,
+                                                                    int D, const float* __restrict__ cls,
+                                                                    const float* __restrict__ pos,
+                                                                    const float* __restrict__ gamma,
+                                                                    const float* __restrict__ beta, float eps,
+                                                                    float* __restrict__ y) {
+  const long long t = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (t >= (long long)B * (NP + 1)) return;
+  const int l = (int)(t % (NP + 1));
+  const long long b = t / (NP + 1);
+  const float* src = l == 0 ? cls : patches + (b * NP + (l - 1)) * D;
+  const float* pr = pos + (long long)l * D;
+  float v[PER_LANE];
+#pragma unroll
+  for (int i = 0; i < PER_LANE; ++i) {
+    const int c = lane + 64 * i;
+    v[i] = c < D ? src[c] + pr[c] : 0.f;
+  }
+  ln_row<PER_LANE>(v, lane, D, gamma, beta, eps, y + t * D);
 }
 
 // Same, vectorised for D % 256 == 0 and 16-B aligned rows (ViT width 768):
@@ -698,11 +733,26 @@ extern "C" int rr_vit_tokens_ex(rr_handle_t h, const float* patches, int b, int 
     hipLaunchKernelGGL(vit_tokens_ln_kernel<2>, grid, dim3(256), 0, s, patches, b, npatch, cls, pos, gamma, beta,
                        eps, y);
   } else {
-    hipLaunchKernelGGL(vit_tokens_kernel, grid_for(total, 256), dim3(256), 0, s, patches, b, npatch, width, cls, pos,
-                       y);
-    // other widths: LayerNorm in place over the assembled rows (each wave
-    // reads its whole row into registers before writing it back)
-    if (gamma) launch_ln<float>((width + 63) / 64, grid, s, y, width, (int)rows, width, gamma, beta, eps, y);
+    if (!gamma) {
+      hipLaunchKernelGGL(vit_tokens_kernel, grid_for(total, 256), dim3(256), 0, s, patches, b, npatch, width, cls,
+                         pos, y);
+    } else {
+      // other widths: assemble and normalise each row in registers (no
+      // in-place pass over y: x and y of layernorm_kernel are __restrict__)
+      const int per = (width + 63) / 64;
+      if (per <= 4)
+        hipLaunchKernelGGL(vit_tokens_ln_generic_kernel<4>, grid, dim3(256), 0, s, patches, b, npatch, width, cls,
+                           pos, gamma, beta, eps, y);
+      else if (per <= 12)
+        hipLaunchKernelGGL(vit_tokens_ln_generic_kernel<12>, grid, dim3(256), 0, s, patches, b, npatch, width, cls,
+                           pos, gamma, beta, eps, y);
+      else if (per <= 16)
+        hipLaunchKernelGGL(vit_tokens_ln_generic_kernel<16>, grid, dim3(256), 0, s, patches, b, npatch, width, cls,
+                           pos, gamma, beta, eps, y);
+      else
+        hipLaunchKernelGGL(vit_tokens_ln_generic_kernel<64>, grid, dim3(256), 0, s, patches, b, npatch, width, cls,
+                           pos, gamma, beta, eps, y);
+    }
   }
   return check_hip(h, hipGetLastError(), "vit_tokens launch");
 }

@@ -23,8 +23,9 @@ class ResNet:
     forward(x_nhwc [B,H,W,3]) -> [B,H/32,W/32,2048] NHWC.
 
     conv_math: "h2" (default) runs every conv, the stem included (NHWC4
-    taps, K padded to 224), on the f16x2 split core (fp32-accurate: error vs
-    float64 at or below the exact-fp32 core's, tests/test_gpu_h2.py; three
+    taps, K padded to 224), on the f16x2 split core (fp32-accurate: per conv
+    mean error vs float64 within 1.05x and max within 1.25x of the exact-fp32
+    core's, descriptors within 2x and <= 1e-6, tests/test_gpu_h2.py; three
     fp16 MFMAs per product; weights split once here, each conv publishes max
     |y| for the next one's split scale); "s3" runs them on the split-bf16 core
     (six bf16 MFMAs per product); "f32" keeps all convs on the exact-fp32 MFMA

@@ -60,6 +60,18 @@ def _end_to_end_parity(name, ranks, ranks_ref, srt, gnd):
     raw = compute_map_and_print(name, "gpu-raw", "global", ranks, gnd)
     raw_ref = compute_map_and_print(name, "ref-raw", "global", ranks_ref, gnd)
     print(f"{name}: raw mAP gpu {raw} ref {raw_ref}")
+    if not mism.any():
+        assert raw == raw_ref
+    else:
+        # each misplaced position p (0-based) is a near-tie swap: moving a
+        # positive between p and a neighbour changes its precision term by at
+        # most 1/(p+1), and AP averages those terms (npos >= 1); so each mAP
+        # (percent, rounded to 2 dp on both sides) moves by at most
+        # 100/Q * sum over misplaced positions of 1/(p+1)
+        pos = np.nonzero(mism)[0]
+        bound = 100.0 / ranks.shape[1] * float(np.sum(1.0 / (pos + 1.0))) + 0.011
+        for a, b in zip(raw, raw_ref):
+            assert abs(a - b) <= bound, (raw, raw_ref, bound)
 
 
 @pytest.mark.parametrize("name", ["roxford5k", "rparis6k"])

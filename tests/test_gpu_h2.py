@@ -381,3 +381,79 @@ def test_resnet_h2_fused_stem_pool_bit_identical(cuda):
     net.fuse_stem_pool = False
     b = net.forward(x)
     assert torch.equal(a.view(torch.int32), b.view(torch.int32))
+
+
+@pytest.mark.parametrize("ratio", [1e3, 1e5])
+def test_conv2d_h2_heavy_tailed_channels(cuda, ratio):
+    """A few input channels 1e3-1e5x larger than the rest (BN-folded real
+    weights give such channel imbalance): one split scale per tensor puts the
+    small channels ~2^10-2^17 below the max, still inside the 2^18 the two
+    fp16 pieces keep at full precision.  The same bar against float64 and
+    the exact-fp32 core as every f16x2 conv."""
+    for shape in ((2, 14, 14, 256, 256, 3, 1, 1, True), (2, 14, 14, 256, 1024, 1, 1, 0, True)):
+        b, h, w, cin, cout, k, s, p, res = shape
+        x, wt, bias, r, _, _ = _conv_case(cuda, *shape, seed=21)
+        x[..., [3, 77, 200]] *= ratio
+        xn, wn = x.permute(0, 3, 1, 2).double(), wt.permute(0, 3, 1, 2).double()
+        conv = F.conv2d(xn, wn, None, s, p).permute(0, 2, 3, 1)
+        scale = F.conv2d(xn.abs(), wn.abs(), None, s, p).permute(0, 2, 3, 1)
+        ref = torch.relu(conv + bias.double() + r.double())
+        y, rec = _run_h2(cuda, x, wt, bias, r, s, p)
+        y_f32 = ops.conv2d(x.to(cuda), wt.to(cuda), bias.to(cuda), s, p, r.to(cuda), True).cpu()
+        live = ref > 0
+        e = _rel_err(y.cpu()[live], ref[live], scale[live])
+        ef32 = _rel_err(y_f32[live], ref[live], scale[live])
+        print(f"heavy-tailed x{ratio:g} {shape}: h2 max {e[0]:.3g} mean {e[1]:.3g} | "
+              f"f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
+        assert e[0] <= 1.25 * max(ef32[0], 1e-7) and e[1] <= ef32[1] * 1.05 + 1e-9
+        assert ops.amax_value(rec[1]) == float(y.abs().max())
+
+
+def test_resnet_h2_heavy_tailed_activations_vs_float64(cuda):
+    """The R50-GeM extractor with heavy-tailed intermediate activations: a
+    few channels of layer1.0's and layer3.2's first ReLU outputs scaled by
+    1e4 (their BN affine x1e4, the next conv's input columns x1e-4: the same
+    function, every such channel 1e4x the rest).  f16x2 vs float64 within 2x
+    the exact-fp32 trunk's error, and <= 1e-6 (the descriptor bar)."""
+    rs = np.random.RandomState(5)
+    img = torch.from_numpy(rs.randint(0, 256, size=(2, 64, 72, 3), dtype=np.uint8))
+    x = embed_ref.normalize_u8(img)
+    sd = W.synthetic_resnet_state_dict("resnet50", 6)
+    for blk, chans in (("layer1.0", [1, 9, 30]), ("layer3.2", [5, 100, 200])):
+        for key in ("weight", "bias"):
+            sd[f"{blk}.bn1.{key}"][chans] *= 1e4
+        sd[f"{blk}.conv2.weight"][:, chans] *= 1e-4
+    got = {}
+    for math in ("h2", "f32"):
+        net = GeM(2048, backbone="resnet50", state_dict=sd, seed=6, device=cuda, conv_math=math)
+        got[math] = net.forward_test(x.to(cuda)).cpu().double()
+    ww, wb = W.synthetic_linear(2048, 2048, 7)
+    ref = embed_ref.gem_net_forward_test(x.double(), {k: v.double() for k, v in sd.items()},
+                                         W.RESNET_LAYERS["resnet50"], ww.double(), wb.double())
+    e_h2 = (got["h2"] - ref).abs().max().item()
+    e_f32 = (got["f32"] - ref).abs().max().item()
+    print(f"heavy-tailed R50-GeM descriptors vs float64: h2 {e_h2:.3g}  f32 {e_f32:.3g}")
+    assert e_h2 < DESC_TOL and e_h2 <= 2.0 * e_f32
+
+
+@pytest.mark.parametrize("ratio_log2", [10, 20])
+def test_h2_batch_coupling_bounded(cuda, ratio_log2):
+    """One split scale per activation tensor couples the images of a batch:
+    an image next to one whose activations are 2^r larger has its values
+    split 2^r below the tensor max.  Its descriptor embedded alone and inside
+    such a batch (networks.GeM R50, the f16x2 trunk) differ by <= 1e-6, and
+    both stay <= 1e-6 from float64."""
+    rs = np.random.RandomState(8)
+    img = torch.from_numpy(rs.randint(0, 256, size=(2, 64, 72, 3), dtype=np.uint8))
+    x = embed_ref.normalize_u8(img)
+    big = x[1:2] * 2.0 ** ratio_log2
+    net = GeM(2048, backbone="resnet50", seed=9, device=cuda)
+    alone = net.forward_test(x[:1].to(cuda)).cpu().double()
+    batch = net.forward_test(torch.cat([x[:1], big]).to(cuda)).cpu().double()
+    sd = {k: v.double() for k, v in W.synthetic_resnet_state_dict("resnet50", 9).items()}
+    ww, wb = W.synthetic_linear(2048, 2048, 10)
+    ref = embed_ref.gem_net_forward_test(x[:1].double(), sd, W.RESNET_LAYERS["resnet50"], ww.double(), wb.double())
+    d = (alone[0] - batch[0]).abs().max().item()
+    ea, eb = (alone - ref).abs().max().item(), (batch[:1] - ref).abs().max().item()
+    print(f"batch coupling 2^{ratio_log2}: alone vs in batch {d:.3g}; vs float64 alone {ea:.3g} in batch {eb:.3g}")
+    assert d <= DESC_TOL and ea <= DESC_TOL and eb <= DESC_TOL

@@ -30,7 +30,7 @@ def test_vit_vs_reference_fixture(cuda, tag):
     ref = fx[tag]
     err = np.abs(got - ref).max() / max(1.0, np.abs(ref).max())
     print(tag, "rel max err", err)
-    assert err < 2e-4
+    assert err < 1e-5  # measured 1.2e-6 (B/16, fp32 MFMA core vs the reference's torch CPU fp32)
     d = net.forward_test(x.to(cuda)).cpu().numpy()
     np.testing.assert_allclose(np.linalg.norm(d, axis=1), 1.0, rtol=1e-5)
 
@@ -81,9 +81,9 @@ def test_patchify_fp32_and_bf16(cuda, b, h, w, c, p):
 
 @pytest.mark.parametrize("b,npatch,width", [(3, 196, 768), (2, 49, 512), (2, 16, 384), (1, 5, 200)])
 def test_vit_tokens_ln_pre_fused(cuda, b, npatch, width):
-    """tokens + ln_pre in one kernel (widths 512 / 768) or tokens then an in-
-    place LayerNorm (other widths): bit-identical to vit_tokens followed by
-    layernorm, and within 1e-5 of torch float64."""
+    """tokens + ln_pre in one kernel (vectorised for widths 512 / 768, a
+    per-lane row loop for other widths): bit-identical to vit_tokens followed
+    by layernorm, and within 1e-5 of torch float64."""
     g = torch.Generator().manual_seed(width + npatch)
     pt = torch.randn(b * npatch, width, generator=g)
     cls, pos = torch.randn(width, generator=g), torch.randn(npatch + 1, width, generator=g)
