@@ -89,12 +89,18 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     7 also selects the implicit-GEMM fused stem over the halo stem)
  *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of
  *                     ~1 us for every other resident block (-1 = the library's pick)
+ *   RR_TUNE_SWEEP_ORDER: bf16 / fp8 filter sweeps' block -> tile order: 0 = each XCD a
+ *                     contiguous range of gallery tiles against every query panel;
+ *                     2 / 4 / 8 = the XCDs split into that many query-panel groups x
+ *                     8 / value gallery ranges (when the panels divide evenly);
+ *                     -1 = the library's pick
  * Any other key or value: RR_EINVAL. */
 #define RR_TUNE_GEMM_CFG 1
 #define RR_TUNE_GEMM_BK 2
 #define RR_TUNE_LP_CFG 3
 #define RR_TUNE_S3_CFG 4
 #define RR_TUNE_S3_STAGGER 5
+#define RR_TUNE_SWEEP_ORDER 6
 int rr_set_tuning(rr_handle_t h, int key, int value);
 
 /* ---- search (ranker) ----------------------------------------------------

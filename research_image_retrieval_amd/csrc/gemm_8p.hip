@@ -60,11 +60,10 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g, int tiles_n
   const int wr = wave & 1, wc = wave >> 1;  // 2 x 4 waves: 64 rows x 32 cols per quadrant
   const int l16 = lane & 15, lg = lane >> 4;
 
-  // XCD-aware bijective block remap (blocks b, b+8, ... share an XCD)
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tn = wgid % tiles_n, tm = wgid / tiles_n;
+  // XCD-aware block -> tile order (rr_internal.hpp tile_coords)
+  int tm, tn;
+  if (!tile_coords(g.tile_order, blockIdx.x, gridDim.x, (g.M + 255) / 256, tiles_n, tm, tn))
+    return;  // a padding block of a reordered grid, before any barrier
   const int m0 = tm * 256, n0 = tn * 256;
   const int nk = g.K / EPR;  // even (K % (2 EPR) == 0, checked on the host)
 
@@ -352,7 +351,7 @@ bool gemm_8p_eligible(const GemmArgs& g, int dt) {
 
 hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s, int dt) {
   const long long tiles_m = (g.M + 255) / 256, tiles_n = (g.N + 255) / 256;
-  const long long nblk = tiles_m * tiles_n;
+  const long long nblk = tile_grid(g.tile_order, tiles_m, tiles_n);
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
   if (emode == E_FILTER && dt == DT_FP8)

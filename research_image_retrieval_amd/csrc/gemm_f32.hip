@@ -112,11 +112,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   const int wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
 
-  // XCD-aware bijective block remap (blocks b, b+8, ... share an XCD).
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tn = wgid % tiles_n, tm = wgid / tiles_n;
+  // XCD-aware block -> tile order (rr_internal.hpp tile_coords)
+  int tm, tn;
+  if (!tile_coords(g.tile_order, blockIdx.x, gridDim.x, (g.M + BM - 1) / BM, tiles_n, tm, tn))
+    return;  // a padding block of a reordered grid, before any barrier
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int slot = tid % SLOTS;
@@ -674,7 +673,7 @@ static hipError_t launch_t1(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM;
   const long long tiles_n = (g.N + BN - 1) / BN;
-  const long long nblk = tiles_m * tiles_n;
+  const long long nblk = tile_grid(g.tile_order, tiles_m, tiles_n);
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
   const unsigned splits = g.k_split > 0 ? (unsigned)((g.K + g.k_split - 1) / g.k_split) : 1u;
@@ -800,14 +799,34 @@ static int pick_lp(const GemmArgs& g, int emode, bool dt_bf16, const rr_handle_s
 // ViT-B/16 linears +4-7 %, 128x128 cosine sweeps +2-5 % over 32x32x16), except
 // the 256x320 sweep tile, whose 16x16 fragments spill (180 B/lane).
 template <int EM, int DT>
+static hipError_t launch_lp_cfg(const GemmArgs& g, hipStream_t s, int cfg);
+
+template <int EM, int DT>
 static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s::Tuning& tu) {
   constexpr int EPR = DT == DT_BF16 ? 64 : 128;  // elements per 128-B k-tile row
-  constexpr int MF = DT == DT_BF16 ? 1 : 0;
   if constexpr (EM == E_FILTER && DT != DT_F32) {
     if (tu.lp_cfg == 6 && sweep_v_eligible(g, DT)) return launch_sweep_v(g, s, DT);
   }
   int cfg = pick_lp(g, EM, DT == DT_BF16, tu);
   if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles
+  if constexpr (EM == E_FILTER) {
+    // panel-grouped XCD order for the filter sweeps (tile_coords), when the
+    // picked tile's query panels split evenly into the groups
+    const int ord = tu.sweep_order < 0 ? 0 : tu.sweep_order;
+    const int bn = (cfg == 4 && DT == DT_BF16) ? 320 : (cfg >= 3 ? 256 : (cfg == 2 ? 64 : 128));
+    const long long tn = ((long long)g.N + bn - 1) / bn;
+    if (ord > 0 && tn % ord == 0) {
+      GemmArgs g2 = g;
+      g2.tile_order = ord;
+      return launch_lp_cfg<EM, DT>(g2, s, cfg);
+    }
+  }
+  return launch_lp_cfg<EM, DT>(g, s, cfg);
+}
+
+template <int EM, int DT>
+static hipError_t launch_lp_cfg(const GemmArgs& g, hipStream_t s, int cfg) {
+  constexpr int MF = DT == DT_BF16 ? 1 : 0;
   if (cfg == 5) {
     if constexpr (DT != DT_F32 && EM != E_STORE) {
       if (gemm_8p_eligible(g, DT)) return launch_gemm_8p(g, EM, s, DT);

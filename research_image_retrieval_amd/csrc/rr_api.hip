@@ -150,6 +150,10 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       if (value < -1 || value > 200) break;
       h->tune.s3_stagger = value;
       return RR_OK;
+    case RR_TUNE_SWEEP_ORDER:
+      if (!in({-1, 0, 2, 4, 8})) break;
+      h->tune.sweep_order = value;
+      return RR_OK;
     default:
       return set_error(h, RR_EINVAL, "rr_set_tuning: unknown key");
   }

@@ -19,6 +19,7 @@ struct rr_handle_s {
     int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 / fp8 sweeps), 6 = gallery-in-VGPR bf16 / fp8 filter sweep (sweep_v.hip)
     int s3_cfg = 0;    // split cores: 1..13 (gemm_s3.hip tile table; 9-13 f16x2 only)
     int s3_stagger = -1;  // split-bf16 core round stagger in ~1 us sleeps (-1: the library's pick)
+    int sweep_order = -1;  // bf16 / fp8 filter sweeps: block -> tile order (tile_coords); -1: the library's pick
   } tune;
   int n_cu = 0;  // compute units of the handle's device (device_cu_count)
   // timing (see rr_timing_enable)
@@ -218,7 +219,41 @@ struct GemmArgs {
   // columns 7 pc .. +6 of the POH x POW pooled map pool_out (NHWC, N channels)
   float* pool_out = nullptr;
   int POH = 0, POW = 0, pool_tr = 0, pool_tc = 0;
+  // block -> tile order of the low-precision filter sweeps (tile_coords)
+  int tile_order = 0;
 };
+
+// Block -> (tm, tn) of a tiles_m x tiles_n grid (tm: A / gallery-row tiles,
+// tn: B / query-panel tiles).  Blocks b, b + 8, ... share an XCD (dispatch is
+// round-robin over the 8 XCDs; used for speed only, never for correctness).
+// order 0: the bijective XCD remap: each XCD a contiguous range of tile ids,
+//   tn fastest (an XCD sweeps its rows against every panel).
+// order NP (2, 4 or 8, tiles_n % NP == 0): the 8 XCD slots are NP panel
+//   groups x 8 / NP row ranges; slot x sweeps rows [(x / NP) R, +R) against
+//   panels (x % NP) tiles_n / NP .. +tiles_n / NP - 1, R = ceil(tiles_m NP / 8):
+//   an XCD keeps tiles_n / NP panels L2-resident, and the NP slots of a row
+//   range stream the same rows at about the same time.  The grid is
+//   tile_grid(...) blocks; the padding blocks get false (exit before any
+//   barrier).
+__host__ __device__ inline long long tile_grid(int order, long long tiles_m, long long tiles_n) {
+  if (order <= 0) return tiles_m * tiles_n;
+  const long long nr = 8 / order, r = (tiles_m + nr - 1) / nr;
+  return 8 * r * (tiles_n / order);
+}
+__device__ __forceinline__ bool tile_coords(int order, int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
+  if (order <= 0) {
+    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    tn = wgid % tiles_n;
+    tm = wgid / tiles_n;
+    return true;
+  }
+  const int nr = 8 / order, tpg = tiles_n / order, x = bid & 7, j = bid >> 3;
+  const int r = (tiles_m + nr - 1) / nr;
+  tm = (x / order) * r + j / tpg;
+  tn = (x % order) * tpg + j % tpg;
+  return tm < tiles_m;
+}
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,
                 int dt = DT_F32);

@@ -294,3 +294,34 @@ def test_bounded_workspace_overflow_recovery(cuda):
     s3, i3 = ops.cosine_topk_lp(qb, None, gb, None, k, "bf16")
     s4, i4 = ops.cosine_topk_lp(qb, None, gb, None, k, "bf16", max_workspace_bytes=budget)
     assert torch.equal(i3, i4) and torch.equal(s3, s4)
+
+
+@pytest.mark.parametrize("order", [2, 4, 8])
+def test_prefilter_sweep_tile_orders_bit_identical(cuda, order):
+    """The filter sweep's panel-grouped XCD block orders (rr_set_tuning
+    sweep_order; 8 does not divide 4 panels of 320 and falls back to the
+    default): the same bits as the default order, with a ragged last gallery
+    tile and planted matches in the first and last rows."""
+    rs = np.random.RandomState(order)
+    d, nq, n = 2048, 1280, 90_001
+    g = rs.standard_normal((n, d)).astype(np.float32)
+    q = rs.standard_normal((nq, d)).astype(np.float32)
+    g[0], g[n - 1] = q[5], q[nq - 1]
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    qd, gd = torch.from_numpy(q).to(cuda), torch.from_numpy(g).to(cuda)
+    gbf, _ = ops.quantize_rows(gd, "bf16")
+    bound = ops.prefilter_gallery_bound(gd, gbf)
+    s0, i0 = ops.cosine_topk_prefilter(qd, gd, gbf, bound, 100)
+    with ops.tuning(cuda.index, sweep_order=order):
+        s1, i1 = ops.cosine_topk_prefilter(qd, gd, gbf, bound, 100)
+        # the bf16 / fp8 lp rankers' filter sweeps take the same orders
+        for dt in ("bf16", "fp8"):
+            ql, qs = ops.quantize_rows(qd, dt)
+            gl, gs = ops.quantize_rows(gd, dt)
+            with ops.tuning(cuda.index, sweep_order=0):
+                a = ops.cosine_topk_lp(ql, qs, gl, gs, 100, dt)
+            b = ops.cosine_topk_lp(ql, qs, gl, gs, 100, dt)
+            assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0]), dt
+    assert torch.equal(i0, i1) and torch.equal(s0.view(torch.int32), s1.view(torch.int32))
+    assert int(i1[5, 0]) == 0 and int(i1[nq - 1, 0]) == n - 1

@@ -160,6 +160,66 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
   if (lane == 0) out[blockIdx.x * 8 + wv] = s;
 }
 
+// The chip's sustained bf16 MFMA rate on random operands held in registers
+// (no memory traffic at all): WPS waves per SIMD, each with independent
+// accumulators (16 of 16x16, 4 of 32x32), for the two MFMA shapes the sweeps use.  This is the ceiling
+// any bf16 sweep can reach at the clock the chip holds under that load.
+template <int MF16, int WPS>
+__global__ __launch_bounds__(256 * WPS, 1) void mfma_only(const uint16_t* __restrict__ seed, int iters,
+                                                          float* __restrict__ out) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  bf16x8 a, b;
+  for (int e = 0; e < 8; ++e) {
+    uint16_t u = seed[(blockIdx.x * 97 + tid * 8 + e) & 65535];
+    uint16_t v = seed[(blockIdx.x * 31 + tid * 8 + e + 4096) & 65535];
+    a[e] = __builtin_bit_cast(__bf16, u);
+    b[e] = __builtin_bit_cast(__bf16, v);
+  }
+  float s = 0.f;
+  if constexpr (MF16) {
+    f32x4 acc[16];
+    for (int i = 0; i < 16; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i], 0, 0, 0);
+    }
+    for (int i = 0; i < 16; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  } else {
+    f32x16 acc[4];
+    for (int i = 0; i < 4; ++i)
+      for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    for (int it = 0; it < iters; ++it) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, acc[i], 0, 0, 0);
+    }
+    for (int i = 0; i < 4; ++i)
+      for (int r = 0; r < 16; ++r) s += acc[i][r];
+  }
+  if (lane == 0) out[blockIdx.x * 16 + (tid >> 6)] = s;
+}
+
+template <int MF16, int WPS>
+static void run_mfma(const char* name, const uint16_t* seed, float* out) {
+  // per wave and iteration: 16 x (16x16x32) or 4 x (32x32x16) = 131072 FLOP
+  const int iters = 20000;
+  auto k = mfma_only<MF16, WPS>;
+  hipLaunchKernelGGL(k, dim3(256), dim3(256 * WPS), 0, 0, seed, iters, out);
+  CK(hipDeviceSynchronize());
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  CK(hipEventRecord(a));
+  for (int r = 0; r < 20; ++r) hipLaunchKernelGGL(k, dim3(256), dim3(256 * WPS), 0, 0, seed, iters, out);
+  CK(hipEventRecord(b));
+  CK(hipEventSynchronize(b));
+  float ms = 0;
+  CK(hipEventElapsedTime(&ms, a, b));
+  ms /= 20;
+  const double flop = 256.0 * 4 * WPS * iters * 131072.0;
+  printf("%-44s %8.3f ms  %7.1f TF/s (%.3f of 2500)\n", name, ms, flop / ms / 1e9, flop / ms / 1e9 / 2500.0);
+  fflush(stdout);
+}
+
 __global__ void fill_rand(uint16_t* p, long long n, unsigned seed) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
     unsigned h = (unsigned)i * 2654435761u ^ seed;
@@ -214,6 +274,10 @@ int main(int argc, char** argv) {
   hipLaunchKernelGGL(fill_rand, dim3(1024), dim3(256), 0, 0, qry, NQ * K, 7u);
   CK(hipDeviceSynchronize());
   printf("C3 sweep shape: %d gallery tiles x %d query panels (256 x 320 x 2048 bf16), %d reps\n", Mt, T, reps);
+  run_mfma<0, 1>("register-only MFMA 32x32x16, 1 wave/SIMD", qry, out);
+  run_mfma<0, 2>("register-only MFMA 32x32x16, 2 waves/SIMD", qry, out);
+  run_mfma<1, 1>("register-only MFMA 16x16x32, 1 wave/SIMD", qry, out);
+  run_mfma<1, 2>("register-only MFMA 16x16x32, 2 waves/SIMD", qry, out);
   run<1, 1, 0, 0, 0>("DMA  gallery+query, no MFMA, order 0", gal, qry, Mt, T, out, reps);
   run<0, 1, 0, 0, 0>("DMA  query panel only (L2), no MFMA", gal, qry, Mt, T, out, reps);
   run<1, 0, 0, 0, 0>("DMA  gallery only (HBM), no MFMA", gal, qry, Mt, T, out, reps);

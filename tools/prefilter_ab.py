@@ -1,9 +1,10 @@
 """Interleaved A/B of the exact prefilter ranker's bf16 filter sweep configs
-(rr_set_tuning lp_cfg: 0 = the pick, 6 = sweep_v.hip) on the C3 shape
+(rr_set_tuning lp_cfg: 0 = the pick, 6 = sweep_v.hip; or, with PF_KEY=sweep_order,
+the block -> tile orders 0 / 2 / 4 / 8) on the C3 shape
 (Q queries x 1.6 M x 2048, top-100): the sweep launch's HIP-event time, its
 fraction of the bf16 dense peak, and the whole ranker's results compared bit
 for bit between configs.
-usage: PF_CFGS="0 6" PF_Q=1280 python tools/prefilter_ab.py"""
+usage: [PF_KEY=lp_cfg|sweep_order] PF_CFGS="0 6" PF_Q=1280 python tools/prefilter_ab.py"""
 import json
 import os
 import statistics
@@ -18,6 +19,7 @@ from research_image_retrieval_amd import _lib, ops  # noqa: E402
 dev = torch.device("cuda:0")
 Q = int(os.environ.get("PF_Q", "1280"))
 cfgs = [int(c) for c in os.environ.get("PF_CFGS", "0 6").split()]
+KEY = os.environ.get("PF_KEY", "lp_cfg")
 N, D, K = int(os.environ.get("PF_N", "1600000")), 2048, 100
 g = torch.Generator(device=dev).manual_seed(0)
 gal = F.normalize(torch.randn(N, D, device=dev, generator=g), dim=1)
@@ -32,7 +34,7 @@ CLS = (_lib.TIME_COSINE, _lib.TIME_COSINE_SEED, _lib.TIME_SELECT, _lib.TIME_ELEM
 
 
 def run(cfg, iters=3):
-    with ops.tuning(0, lp_cfg=cfg):
+    with ops.tuning(0, **{KEY: cfg}):
         ops.cosine_topk_prefilter(q, gal, gbf, bound, K, workspace=ws)
         torch.cuda.synchronize()
         timer.enable(True)
@@ -57,6 +59,6 @@ for c in cfgs:
     ms = statistics.median(res[c])
     same = torch.equal(outs[c][1], outs[base][1]) and torch.equal(outs[c][0].view(torch.int32),
                                                                   outs[base][0].view(torch.int32))
-    print(json.dumps({"lp_cfg": c, "Q": Q, "N": N, "sweep_ms": round(ms, 3), "tflops": round(fl / ms / 1e9, 1),
+    print(json.dumps({KEY: c, "Q": Q, "N": N, "sweep_ms": round(ms, 3), "tflops": round(fl / ms / 1e9, 1),
                       "frac_bf16_peak": round(fl / ms / 1e9 / 2500.0, 4), "identical_to_cfg_%d" % base: same}),
           flush=True)
