@@ -496,6 +496,9 @@ def main():
     ap.add_argument("--ws-budget-gb", type=float, default=4.0,
                     help="ranker workspace budget per rank (bounded candidate buffers, overflowed queries re-run; "
                          "0 = the worst-case size, ~Q*N*8 bytes)")
+    ap.add_argument("--pipeline", type=int, choices=(0, 1), default=0,
+                    help="1: rank batch i on a second HIP stream while batch i+1 is embedded (n embeds + n rankings "
+                         "per n steps either way)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c2-dataset", choices=("both", "roxford5k", "rparis6k"), default="both",
                     help="C2 sets per step (BASELINE C2: full ROxford5k + RParis6k)")
@@ -588,7 +591,9 @@ def main():
         return ops.l2_normalize(acc, 1e-12, out=acc)
 
     def step():
-        desc = embed()
+        return rank_step(embed())
+
+    def rank_step(desc):
         if sharded is not None:
             # C3 / C4: sharded search; C5: + alpha-QE with neighbour rows fetched
             # from their owning shards (bit-identical to 1 GPU); tests/test_distributed_gloo.py
@@ -613,8 +618,36 @@ def main():
                                              max_workspace_bytes=ws_max)
         return ops.cosine_topk(desc, gallery, a.k, idx_offset=lo, workspace=ws, max_workspace_bytes=ws_max)
 
-    for _ in range(a.warmup):
-        out = step()
+    s_rank = torch.cuda.Stream(dev) if a.pipeline else None
+
+    def run_steps(n):
+        """n steps.  --pipeline: batch i's ranking runs on its own HIP stream
+        (after an event on batch i's descriptors) while batch i+1 is embedded
+        on the current stream -- the ranker's MFMA / L2-bound sweep beside the
+        trunk's HBM-bound layers; still exactly n embeds and n rankings, the
+        last ranking joined before returning."""
+        if s_rank is None:
+            out = None
+            for _ in range(n):
+                out = step()
+            return out
+        prev, ev_prev, out = None, None, None
+        for i in range(n + 1):
+            if i < n:
+                d = embed()
+                ev = torch.cuda.Event()
+                ev.record()
+            if prev is not None:
+                with torch.cuda.stream(s_rank):
+                    s_rank.wait_event(ev_prev)
+                    prev.record_stream(s_rank)  # not reused by the embed stream's allocations meanwhile
+                    out = rank_step(prev)
+            if i < n:
+                prev, ev_prev = d, ev
+        torch.cuda.current_stream(dev).wait_stream(s_rank)
+        return out
+
+    out = run_steps(a.warmup) if a.warmup > 0 else None
     torch.cuda.synchronize()
     prefilter_stats = None
     if gal_bf is not None:  # the prefilter must reproduce the exhaustive fp32 ranking bit for bit
@@ -643,8 +676,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        out = step()
+    out = run_steps(a.steps)
     if DIST_ON:
         dist.barrier()
     torch.cuda.synchronize()
@@ -809,6 +841,7 @@ def main():
                       "images_per_gpu_per_step": a.batch, "gallery_rows": a.gallery, "dim": a.dim, "k": a.k,
                       "parallelism": f"query-dp{world} + gallery-shard{world}",
                       "conv_math": a.conv_math if a.workload != "c4" else None,
+                      "pipeline": bool(a.pipeline),
                       "ranker_workspace_bytes_per_rank": int(ws.numel()),
                       "ranker_workspace_worst_case_bytes": int(ws_full)},
            "roofline": roof, "roofline_by_kernel": rk}

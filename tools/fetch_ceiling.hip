@@ -13,6 +13,9 @@
 //      k-step, fragments read from LDS exactly as the real tile does)
 //   VG register staging (global_load_dwordx4 -> ds_write_b128) instead of
 //      LDS-DMA (global_load_lds_dwordx4)
+//   PF   prefetch the gallery k-slice two k-tiles ahead into L2 (4-byte
+//        LDS-DMA per 128-B line into a dummy LDS word, left in flight across
+//        the barrier: counted vmcnt + raw s_barrier instead of vmcnt(0))
 //   ORD block -> (gallery tile, query panel) order: 0 = the library's (each
 //      XCD a contiguous range of gallery tiles x all 4 panels); 2 / 4 = the 8
 //      XCDs split into 2 / 4 panel groups x 4 / 2 gallery ranges, so an XCD
@@ -66,10 +69,10 @@ __device__ __forceinline__ bool tile_of(int bid, int nwg, int Mt, int T, int& tm
   }
 }
 
-template <int G, int Q, int MF, int VG, int ORD>
+template <int G, int Q, int MF, int VG, int ORD, int PF = 0>
 __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__ gal, const uint16_t* __restrict__ qry,
                                                     int Mt, int T, float* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * BUFB];
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2 * BUFB + 256];
   int tm, tn;
   if (!tile_of<ORD>(blockIdx.x, gridDim.x, Mt, T, tm, tn)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -106,6 +109,14 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
       *reinterpret_cast<f32x4*>(lds + buf * BUFB + row * 128 + slot * 16) = rv[i];
     }
   };
+  // PF: waves 0-3 each touch 64 of the block's 256 gallery rows' 128-B line
+  // of k-tile kt (one 4-byte LDS-DMA per lane into a dummy word)
+  const uint16_t* pf_src = gal + ((long long)tm * BM + (wv & 3) * 64 + lane) * K;
+  auto prefetch = [&](int kt) {
+    if (PF && wv < 4 && kt < NK)
+      __builtin_amdgcn_global_load_lds((const void*)(pf_src + kt * EPR),
+                                       (__attribute__((address_space(3))) void*)(lds + 2 * BUFB), 4, 0, 0);
+  };
   f32x16 acc[2][5];
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -118,9 +129,11 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
   if constexpr (VG) vstore(0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  prefetch(1);
   for (int kt = 0; kt < NK; ++kt) {
     const int cur = kt & 1;
     if (kt + 1 < NK) issue(kt + 1, cur ^ 1);
+    prefetch(kt + 2);
     if constexpr (MF) {
       const unsigned char* la = lds + cur * BUFB;
       const unsigned char* lb = la + BM * 128;
@@ -146,9 +159,20 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
     if constexpr (VG) {
       if (kt + 1 < NK) vstore(cur ^ 1);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (PF) {
+      // everything but this iteration's prefetch (the youngest VMEM op of
+      // waves 0-3) has landed; it stays in flight across the raw barrier
+      if (wv < 4 && kt + 2 < NK) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -231,14 +255,14 @@ __global__ void fill_rand(uint16_t* p, long long n, unsigned seed) {
   }
 }
 
-template <int G, int Q, int MF, int VG, int ORD>
+template <int G, int Q, int MF, int VG, int ORD, int PF = 0>
 static void run(const char* name, const uint16_t* gal, const uint16_t* qry, int Mt, int T, float* out, int reps) {
   int nblk = Mt * T;
   if (ORD) {
     const int NR = 8 / ORD, R = (Mt + NR - 1) / NR;
     nblk = 8 * R * (T / ORD);
   }
-  auto k = sweep_fill<G, Q, MF, VG, ORD>;
+  auto k = sweep_fill<G, Q, MF, VG, ORD, PF>;
   hipLaunchKernelGGL(k, dim3(nblk), dim3(NT), 0, 0, gal, qry, Mt, T, out);
   CK(hipDeviceSynchronize());
   hipEvent_t a, b;
@@ -292,6 +316,10 @@ int main(int argc, char** argv) {
   run<1, 1, 1, 1, 0>("VGPR + MFMA, order 0", gal, qry, Mt, T, out, reps);
   run<0, 1, 1, 0, 0>("DMA  query only + MFMA (gallery stale)", gal, qry, Mt, T, out, reps);
   run<1, 0, 1, 0, 0>("DMA  gallery only + MFMA (queries stale)", gal, qry, Mt, T, out, reps);
+  run<1, 1, 1, 0, 0, 1>("DMA  + MFMA + L2 prefetch 2 ahead, order 0", gal, qry, Mt, T, out, reps);
+  run<1, 1, 1, 0, 2, 1>("DMA  + MFMA + L2 prefetch 2 ahead, order 2", gal, qry, Mt, T, out, reps);
+  run<1, 1, 1, 0, 4, 1>("DMA  + MFMA + L2 prefetch 2 ahead, order 4", gal, qry, Mt, T, out, reps);
+  run<1, 1, 0, 0, 0, 1>("DMA  gallery+query + L2 prefetch, no MFMA", gal, qry, Mt, T, out, reps);
   CK(hipFree(gal));
   CK(hipFree(qry));
   CK(hipFree(out));
