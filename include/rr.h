@@ -94,6 +94,9 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     2 / 4 / 8 = the XCDs split into that many query-panel groups x
  *                     8 / value gallery ranges (when the panels divide evenly);
  *                     -1 = the library's pick
+ *   RR_TUNE_SWEEP_PF: the 256x320 bf16 filter sweep: 1 = touch each gallery row's
+ *                     line of k-tile kt + 2 while kt computes (L2 prefetch, DMA left in
+ *                     flight across the barrier), 0 = off, -1 = the library's pick
  * Any other key or value: RR_EINVAL. */
 #define RR_TUNE_GEMM_CFG 1
 #define RR_TUNE_GEMM_BK 2
@@ -101,6 +104,7 @@ int rr_get_device(rr_handle_t h, int* device);
 #define RR_TUNE_S3_CFG 4
 #define RR_TUNE_S3_STAGGER 5
 #define RR_TUNE_SWEEP_ORDER 6
+#define RR_TUNE_SWEEP_PF 7
 int rr_set_tuning(rr_handle_t h, int key, int value);
 
 /* ---- search (ranker) ----------------------------------------------------

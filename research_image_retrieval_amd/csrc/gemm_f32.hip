@@ -85,8 +85,14 @@ __device__ __forceinline__ void interleave2() {
 // 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
 // 'DVFS give-back' item 7).  Register r of tile (i, j) then maps through
 // acc_row / acc_col<true> (gemm_epilogue.hpp) instead of the 32x32 map.
+// PF (LDS-DMA, non-MF16 tiles, EMODE != E_STORE; the long-K gallery sweeps):
+// the A rows' (gallery's) 128-B line of k-tile kt + 2 is touched by one
+// 4-byte LDS-DMA per row into a dummy LDS word while tile kt computes, so
+// the HBM fetch has two k-tiles of lead time and the real DMA of kt + 2 hits
+// L2; that DMA stays in flight across the k-tile's barrier (counted vmcnt and
+// a raw s_barrier instead of __syncthreads' vmcnt(0)).
 template <int WM, int WN, int FM, int FN, int AMODE, int EMODE, int BK, int DT, int MINB, int GL, int MF16 = 0,
-          int EPI = -1>
+          int EPI = -1, int PF = 0>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, int tiles_n) {
   using ET = typename ElemT<DT>::T;
   static_assert(!MF16 || DT == DT_BF16, "MF16: bf16 only");
@@ -105,7 +111,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for block");
   static_assert(BM % ROWS_PER_PASS == 0 && BN % ROWS_PER_PASS == 0, "staging passes must tile the block");
   constexpr int BUF = (BM + BN) * BK;  // floats per LDS buffer
-  __shared__ __attribute__((aligned(16))) float lds[2 * BUF];
+  static_assert(!PF || (GL && !MF16 && EMODE != E_STORE), "PF: LDS-DMA sweep tiles");
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF + (PF ? 64 : 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -381,9 +388,21 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     __builtin_amdgcn_s_setprio(0);
     __syncthreads();  // every wave's last reads done: the epilogue reuses the LDS
   } else {
+  // PF: waves 0 .. BM/64 - 1 each touch 64 A rows (one per lane)
+  const ET* pf_src = reinterpret_cast<const ET*>(g.A) +
+                     (long long)min(m0 + (PF ? (wave % (BM / 64)) * 64 + lane : 0), g.M - 1) * g.lda + koff;
+  const bool pf_wave = PF && wave < BM / 64;
+  auto prefetch = [&](int kt) {
+    if constexpr (PF) {
+      if (pf_wave && kt < nk)
+        __builtin_amdgcn_global_load_lds((const void*)(pf_src + (long long)kt * EPR),
+                                         (__attribute__((address_space(3))) void*)(lds + 2 * BUF), 4, 0, 0);
+    }
+  };
   if constexpr (GL) {
     glds_tile(0, 0);
     __syncthreads();
+    prefetch(1);
   } else {
     load_tile(0);
     store_tile(0);
@@ -396,6 +415,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
       if constexpr (GL) glds_tile(kt + 1, cur ^ 1);
       else load_tile(kt + 1);
     }
+    prefetch(kt + 2);
     const float* la = lds + cur * BUF;
     const float* lb = la + BM * BK;
     if constexpr (DT == DT_F32) {
@@ -534,8 +554,19 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     if constexpr (!GL) {
       if (kt + 1 < nk) store_tile(cur ^ 1);
     }
-    __syncthreads();  // with GL: also the vmcnt(0) that retires the DMA
+    if constexpr (PF) {
+      // every DMA of tile kt + 1 has landed; only this iteration's prefetch
+      // (the wave's youngest VMEM op) may still be in flight
+      if (pf_wave && kt + 2 < nk) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    } else {
+      __syncthreads();  // with GL: also the vmcnt(0) that retires the DMA
+    }
   }
+  if constexpr (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if constexpr (MF16) {
 #pragma unroll
@@ -668,7 +699,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
 }
 
 template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0,
-          int EPI = -1>
+          int EPI = -1, int PF = 0>
 static hipError_t launch_t1(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM;
@@ -677,7 +708,7 @@ static hipError_t launch_t1(const GemmArgs& g, hipStream_t s) {
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
   const unsigned splits = g.k_split > 0 ? (unsigned)((g.K + g.k_split - 1) / g.k_split) : 1u;
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EPI>), dim3((unsigned)nblk, splits),
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EPI, PF>), dim3((unsigned)nblk, splits),
                      dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
@@ -815,9 +846,10 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
     const int ord = tu.sweep_order < 0 ? 0 : tu.sweep_order;
     const int bn = (cfg == 4 && DT == DT_BF16) ? 320 : (cfg >= 3 ? 256 : (cfg == 2 ? 64 : 128));
     const long long tn = ((long long)g.N + bn - 1) / bn;
-    if (ord > 0 && tn % ord == 0) {
+    if ((ord > 0 && tn % ord == 0) || tu.sweep_pf > 0) {
       GemmArgs g2 = g;
-      g2.tile_order = ord;
+      if (ord > 0 && tn % ord == 0) g2.tile_order = ord;
+      g2.l2_prefetch = tu.sweep_pf > 0;
       return launch_lp_cfg<EM, DT>(g2, s, cfg);
     }
   }
@@ -837,7 +869,10 @@ static hipError_t launch_lp_cfg(const GemmArgs& g, hipStream_t s, int cfg) {
     case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF>(g, s);
     case 3: return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);
     case 4:  // bf16 sweeps only (fp8: the 256x256 tile; its 256x320 form spills the dequantisation)
-      if constexpr (EM != E_STORE && DT == DT_BF16) return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0>(g, s);
+      if constexpr (EM != E_STORE && DT == DT_BF16) {
+        if (g.l2_prefetch) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0, -1, 1>(g, s);
+        return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0>(g, s);
+      }
       else if constexpr (EM != E_STORE) return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);
       return hipErrorInvalidValue;
     default: return launch_t<2, 2, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF>(g, s);

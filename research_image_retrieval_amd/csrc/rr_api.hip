@@ -154,6 +154,10 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       if (!in({-1, 0, 2, 4, 8})) break;
       h->tune.sweep_order = value;
       return RR_OK;
+    case RR_TUNE_SWEEP_PF:
+      if (!in({-1, 0, 1})) break;
+      h->tune.sweep_pf = value;
+      return RR_OK;
     default:
       return set_error(h, RR_EINVAL, "rr_set_tuning: unknown key");
   }

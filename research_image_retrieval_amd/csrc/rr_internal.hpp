@@ -20,6 +20,7 @@ struct rr_handle_s {
     int s3_cfg = 0;    // split cores: 1..13 (gemm_s3.hip tile table; 9-13 f16x2 only)
     int s3_stagger = -1;  // split-bf16 core round stagger in ~1 us sleeps (-1: the library's pick)
     int sweep_order = -1;  // bf16 / fp8 filter sweeps: block -> tile order (tile_coords); -1: the library's pick
+    int sweep_pf = -1;     // bf16 256x320 filter sweep: L2 prefetch of the gallery two k-tiles ahead; -1: the pick
   } tune;
   int n_cu = 0;  // compute units of the handle's device (device_cu_count)
   // timing (see rr_timing_enable)
@@ -221,6 +222,8 @@ struct GemmArgs {
   int POH = 0, POW = 0, pool_tr = 0, pool_tc = 0;
   // block -> tile order of the low-precision filter sweeps (tile_coords)
   int tile_order = 0;
+  // the 256x320 bf16 filter sweep's L2 prefetch of A (gemm_kernel PF)
+  int l2_prefetch = 0;
 };
 
 // Block -> (tm, tn) of a tiles_m x tiles_n grid (tm: A / gallery-row tiles,

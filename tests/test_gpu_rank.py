@@ -325,3 +325,25 @@ def test_prefilter_sweep_tile_orders_bit_identical(cuda, order):
             assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0]), dt
     assert torch.equal(i0, i1) and torch.equal(s0.view(torch.int32), s1.view(torch.int32))
     assert int(i1[5, 0]) == 0 and int(i1[nq - 1, 0]) == n - 1
+
+
+def test_prefilter_sweep_l2_prefetch_bit_identical(cuda):
+    """The 256x320 bf16 sweep with the gallery's L2 prefetch two k-tiles
+    ahead (rr_set_tuning sweep_pf; DMA in flight across the raw barrier):
+    the same bits as without, ragged last tile, planted matches."""
+    rs = np.random.RandomState(77)
+    d, nq, n = 2048, 1280, 70_001
+    g = rs.standard_normal((n, d)).astype(np.float32)
+    q = rs.standard_normal((nq, d)).astype(np.float32)
+    g[3], g[n - 1] = q[0], q[nq - 1]
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    qd, gd = torch.from_numpy(q).to(cuda), torch.from_numpy(g).to(cuda)
+    gbf, _ = ops.quantize_rows(gd, "bf16")
+    bound = ops.prefilter_gallery_bound(gd, gbf)
+    out = {}
+    for pf in (0, 1):
+        with ops.tuning(cuda.index, sweep_pf=pf):
+            out[pf] = ops.cosine_topk_prefilter(qd, gd, gbf, bound, 100)
+    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][0].view(torch.int32), out[1][0].view(torch.int32))
+    assert int(out[1][1][0, 0]) == 3 and int(out[1][1][nq - 1, 0]) == n - 1
