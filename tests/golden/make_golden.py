@@ -82,6 +82,38 @@ def trunk_fixture():
     np.savez_compressed(os.path.join(HERE, "resnet_dolg.npz"), **out)
 
 
+def trunk_fixture_v15():
+    """(ix-b) The same ResNet_DOLG with each stage-entry block's stride moved
+    from its 1x1 `a` conv to its 3x3 `b` conv (BottleneckTransform's own
+    comment, networks/backbone.py:310: "TH/C2 -> stride=2 is on 3x3"), i.e. the
+    torchvision v1.5 placement of the reference's `ResNet` (networks/backbone.py
+    :60-109, torchvision absent here), composed from the reference's modules.
+    Only the two Conv2d modules' stride attributes change."""
+    from networks.backbone import ResNet_DOLG, ResBlock
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from research_image_retrieval_amd.weights import synthetic_resnet_state_dict, to_dolg_keys
+    torch.set_num_threads(8)
+    net = ResNet_DOLG()
+    sd = to_dolg_keys(synthetic_resnet_state_dict("resnet101", I.TRUNK_WEIGHT_SEED))
+    net.load_state_dict(sd, strict=True)
+    moved = 0
+    for m in net.modules():
+        if isinstance(m, ResBlock) and m.f.a.stride != (1, 1):
+            m.f.b.stride, m.f.a.stride = m.f.a.stride, (1, 1)
+            moved += 1
+    assert moved == 3, moved
+    net.eval()
+    out = {"weight_seed": I.TRUNK_WEIGHT_SEED}
+    with torch.no_grad():
+        for tag, (seed, b, h, w) in I.TRUNK_CASES.items():
+            x3, x4 = net(I.trunk_input(seed, b, h, w))
+            out[tag + "_x4"] = x4.numpy()
+            if tag == "b1_odd":
+                out[tag + "_x3"] = x3.numpy()
+            out[tag + "_case"] = np.array([seed, b, h, w])
+    np.savez_compressed(os.path.join(HERE, "resnet_dolg_v15.npz"), **out)
+
+
 def extract_fixture():
     """(vi) extract_vectors on a tiny networks-style extractor (utils/helpfunc.py:18-48):
     single scale ms=[1], single scale ms=[0.5] (the reference's len(ms) == 1
@@ -108,8 +140,12 @@ def main():
     if "--only-extract" in sys.argv:
         extract_fixture()
         return
+    if "--only-trunk-v15" in sys.argv:
+        trunk_fixture_v15()
+        return
     loader_fixture()
     trunk_fixture()
+    trunk_fixture_v15()
     from networks.RetrievalNet import gem, GeM
     from networks.backbone import pcawhitenlearn_shrinkage
     from networks.spca import ConvDimReduction

@@ -52,6 +52,27 @@ def test_trunk_vs_reference_resnet_dolg(cuda, fixture, conv_math, tag):
         assert err3 < TRUNK_TOL
 
 
+@pytest.mark.parametrize("conv_math", ["h2", "s3", "f32"])
+@pytest.mark.parametrize("tag", ["b2_224", "b1_odd"])
+def test_trunk_v15_vs_reference_modules(cuda, conv_math, tag):
+    """The default torchvision-v1.5 placement (stride on the 3x3) against
+    tests/golden/resnet_dolg_v15.npz: the reference's ResNet_DOLG modules with
+    each stage-entry stride moved from the 1x1 `a` conv to the 3x3 `b` conv
+    (make_golden.py trunk_fixture_v15; torchvision itself is absent)."""
+    fx = np.load(os.path.join(GOLD, "resnet_dolg_v15.npz"))
+    sd = W.to_dolg_keys(W.synthetic_resnet_state_dict("resnet101", int(fx["weight_seed"])))
+    net = ResNet("resnet101", state_dict=sd, device=cuda, conv_math=conv_math, stride_on="3x3")
+    seed, b, h, w = (int(v) for v in fx[tag + "_case"])
+    x = I.trunk_input(seed, b, h, w).permute(0, 2, 3, 1).contiguous().to(cuda)
+    x3, x4 = net.forward(x, return_x3=True)
+    err4 = np.abs(x4.permute(0, 3, 1, 2).cpu().numpy() - fx[tag + "_x4"]).max()
+    print(tag, conv_math, "v1.5 max|x4 err|", err4)
+    assert err4 < TRUNK_TOL
+    if tag + "_x3" in fx:
+        err3 = np.abs(x3.permute(0, 3, 1, 2).cpu().numpy() - fx[tag + "_x3"]).max()
+        assert err3 < TRUNK_TOL
+
+
 def test_trunk_v15_vs_oracle(cuda):
     """The default torchvision-v1.5 placement against the oracle, which the
     fixture above pins (it differs only in which conv carries the stride)."""

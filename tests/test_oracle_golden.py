@@ -170,6 +170,23 @@ def test_oracle_trunk_vs_reference_resnet_dolg(tag):
         np.testing.assert_allclose(x3.numpy(), fx[tag + "_x3"], rtol=0, atol=1e-6)
 
 
+@pytest.mark.parametrize("tag", ["b2_224", "b1_odd"])
+def test_oracle_trunk_v15_vs_reference_modules(tag):
+    """The oracle's default torchvision-v1.5 trunk (stride on the 3x3) against
+    the reference's ResNet_DOLG modules with each stage-entry stride moved to
+    the 3x3 `b` conv (make_golden.py trunk_fixture_v15)."""
+    from research_image_retrieval_amd import weights as W
+    fx = load("resnet_dolg_v15")
+    sd = W.synthetic_resnet_state_dict("resnet101", int(fx["weight_seed"]))
+    seed, b, h, w = (int(v) for v in fx[tag + "_case"])
+    with torch.no_grad():
+        x3, x4 = embed_ref.resnet_trunk(I.trunk_input(seed, b, h, w), sd, W.RESNET_LAYERS["resnet101"],
+                                        stride_on="3x3", return_x3=True)
+    np.testing.assert_allclose(x4.numpy(), fx[tag + "_x4"], rtol=0, atol=1e-6)
+    if tag + "_x3" in fx:
+        np.testing.assert_allclose(x3.numpy(), fx[tag + "_x3"], rtol=0, atol=1e-6)
+
+
 def test_dolg_key_layout_round_trip():
     """ResNet_DOLG keys (stem.*, s{K}.b{M}.{proj,bn,f.*}) <-> torchvision keys."""
     from research_image_retrieval_amd import weights as W

@@ -4,6 +4,7 @@
 set -o pipefail
 O=gpurun_out/r04b; mkdir -p $O
 timeout -k 10 120 ./tools/fetch_ceiling 5 > $O/fetch_ceiling.txt 2>&1 || exit 1
+timeout -k 10 120 ./tools/hbm_pattern > $O/hbm_pattern.txt 2>&1 || exit 1
 timeout -k 10 300 python -u tools/overlap_probe.py > $O/overlap.txt 2>&1 || exit 1
 PF_KEY=sweep_order PF_CFGS="0 2 4" timeout -k 10 300 python -u tools/prefilter_ab.py > $O/sweep_order_ab.txt 2>&1 || exit 1
 PF_QKIND=corr PF_KEY=sweep_order PF_CFGS="0 2 4" timeout -k 10 300 python -u tools/prefilter_ab.py > $O/sweep_order_ab_corr.txt 2>&1 || exit 1
