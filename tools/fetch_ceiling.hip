@@ -69,7 +69,7 @@ __device__ __forceinline__ bool tile_of(int bid, int nwg, int Mt, int T, int& tm
   }
 }
 
-template <int G, int Q, int MF, int VG, int ORD, int PF = 0>
+template <int G, int Q, int MF, int VG, int ORD, int PF = 0, int M16 = 0>
 __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__ gal, const uint16_t* __restrict__ qry,
                                                     int Mt, int T, float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * BUFB + 256];
@@ -77,12 +77,10 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
   if (!tile_of<ORD>(blockIdx.x, gridDim.x, Mt, T, tm, tn)) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int slot = tid % SLOTS, crow = tid / SLOTS;
-  const uint16_t* src[9];
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    const int row = crow + i * PASS;  // LDS row of this lane's chunk
-    src[i] = row < BM ? gal + ((long long)tm * BM + row) * K : qry + ((long long)tn * BN + row - BM) * K;
-  }
+  // chunk i: LDS row crow + 64 i = gallery row crow + 64 i (i < 4) or query row crow + 64 (i - 4)
+  const uint16_t* gsrc = gal + ((long long)tm * BM + crow) * K;
+  const uint16_t* qsrc = qry + ((long long)tn * BN + crow) * K;
+  auto src_of = [&](int i) { return i < 4 ? gsrc + (long long)i * PASS * K : qsrc + (long long)(i - 4) * PASS * K; };
   auto on = [&](int i) { return i < 4 ? G != 0 : Q != 0; };
   f32x4 rv[9];
   auto issue = [&](int kt, int buf) {
@@ -90,7 +88,7 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
     for (int i = 0; i < 9; ++i) {
       if (!on(i)) continue;
       const int row = crow + i * PASS;
-      const uint16_t* s = src[i] + kt * EPR + swz(row, slot) * 8;
+      const uint16_t* s = src_of(i) + kt * EPR + swz(row, slot) * 8;
       if constexpr (VG) {
         rv[i] = *reinterpret_cast<const f32x4*>(s);
       } else {
@@ -117,13 +115,18 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
       __builtin_amdgcn_global_load_lds((const void*)(pf_src + kt * EPR),
                                        (__attribute__((address_space(3))) void*)(lds + 2 * BUFB), 4, 0, 0);
   };
-  f32x16 acc[2][5];
+  f32x16 acc[M16 ? 1 : 2][M16 ? 1 : 5];
+  f32x4 acc16[M16 ? 4 : 1][M16 ? 10 : 1];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < (M16 ? 1 : 2); ++i)
 #pragma unroll
-    for (int j = 0; j < 5; ++j)
+    for (int j = 0; j < (M16 ? 1 : 5); ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+#pragma unroll
+  for (int i = 0; i < (M16 ? 4 : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < (M16 ? 10 : 1); ++j) acc16[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int wm = wv % 4, wn = wv / 4, lr = lane & 31, lh = lane >> 5;
   issue(0, 0);
   if constexpr (VG) vstore(0);
@@ -134,7 +137,32 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
     const int cur = kt & 1;
     if (kt + 1 < NK) issue(kt + 1, cur ^ 1);
     prefetch(kt + 2);
-    if constexpr (MF) {
+    if constexpr (MF && M16) {
+      // v_mfma_f32_16x16x32_bf16: per 32-deep k-step 4 A and 10 B fragments
+      // (16 rows each; lane group l >> 4 holds k 8 (l >> 4) .. +7 = slot
+      // 4 st + (l >> 4)), 40 MFMAs into acc16[4][10]
+      const unsigned char* la = lds + cur * BUFB;
+      const unsigned char* lb = la + BM * 128;
+      const int l16 = lane & 15, lg = lane >> 4;
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 af[4], bfr[10];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int row = wm * 64 + i * 16 + l16;
+          af[i] = *reinterpret_cast<const bf16x8*>(la + row * 128 + swz(row, 4 * st + lg) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 10; ++j) {
+          const int row = wn * 160 + j * 16 + l16;
+          bfr[j] = *reinterpret_cast<const bf16x8*>(lb + row * 128 + swz(row, 4 * st + lg) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < 10; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc16[i][j], 0, 0, 0);
+      }
+    } else if constexpr (MF) {
       const unsigned char* la = lds + cur * BUFB;
       const unsigned char* lb = la + BM * 128;
 #pragma unroll
@@ -175,11 +203,15 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < (M16 ? 1 : 2); ++i)
 #pragma unroll
-    for (int j = 0; j < 5; ++j)
+    for (int j = 0; j < (M16 ? 1 : 5); ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) s += acc[i][j][r];
+#pragma unroll
+  for (int i = 0; i < (M16 ? 4 : 1); ++i)
+#pragma unroll
+    for (int j = 0; j < (M16 ? 10 : 1); ++j) s += acc16[i][j][0] + acc16[i][j][1] + acc16[i][j][2] + acc16[i][j][3];
   if (!MF) s = (float)lds[(tid * 16) % (2 * BUFB)];
   if (lane == 0) out[blockIdx.x * 8 + wv] = s;
 }
@@ -224,7 +256,7 @@ __global__ __launch_bounds__(256 * WPS, 1) void mfma_only(const uint16_t* __rest
 
 template <int MF16, int WPS>
 static void run_mfma(const char* name, const uint16_t* seed, float* out) {
-  // per wave and iteration: 16 x (16x16x32) or 4 x (32x32x16) = 131072 FLOP
+  // per wave and iteration: 16 x (16x16x32) = 262144 FLOP, 4 x (32x32x16) = 131072 FLOP
   const int iters = 20000;
   auto k = mfma_only<MF16, WPS>;
   hipLaunchKernelGGL(k, dim3(256), dim3(256 * WPS), 0, 0, seed, iters, out);
@@ -239,7 +271,7 @@ static void run_mfma(const char* name, const uint16_t* seed, float* out) {
   float ms = 0;
   CK(hipEventElapsedTime(&ms, a, b));
   ms /= 20;
-  const double flop = 256.0 * 4 * WPS * iters * 131072.0;
+  const double flop = 256.0 * 4 * WPS * iters * (MF16 ? 262144.0 : 131072.0);
   printf("%-44s %8.3f ms  %7.1f TF/s (%.3f of 2500)\n", name, ms, flop / ms / 1e9, flop / ms / 1e9 / 2500.0);
   fflush(stdout);
 }
@@ -255,14 +287,14 @@ __global__ void fill_rand(uint16_t* p, long long n, unsigned seed) {
   }
 }
 
-template <int G, int Q, int MF, int VG, int ORD, int PF = 0>
+template <int G, int Q, int MF, int VG, int ORD, int PF = 0, int M16 = 0>
 static void run(const char* name, const uint16_t* gal, const uint16_t* qry, int Mt, int T, float* out, int reps) {
   int nblk = Mt * T;
   if (ORD) {
     const int NR = 8 / ORD, R = (Mt + NR - 1) / NR;
     nblk = 8 * R * (T / ORD);
   }
-  auto k = sweep_fill<G, Q, MF, VG, ORD, PF>;
+  auto k = sweep_fill<G, Q, MF, VG, ORD, PF, M16>;
   hipLaunchKernelGGL(k, dim3(nblk), dim3(NT), 0, 0, gal, qry, Mt, T, out);
   CK(hipDeviceSynchronize());
   hipEvent_t a, b;
@@ -320,6 +352,9 @@ int main(int argc, char** argv) {
   run<1, 1, 1, 0, 2, 1>("DMA  + MFMA + L2 prefetch 2 ahead, order 2", gal, qry, Mt, T, out, reps);
   run<1, 1, 1, 0, 4, 1>("DMA  + MFMA + L2 prefetch 2 ahead, order 4", gal, qry, Mt, T, out, reps);
   run<1, 1, 0, 0, 0, 1>("DMA  gallery+query + L2 prefetch, no MFMA", gal, qry, Mt, T, out, reps);
+  run<0, 0, 1, 0, 0, 0, 1>("16x16x32: MFMA only (stale LDS operands)", gal, qry, Mt, T, out, reps);
+  run<1, 1, 1, 0, 0, 0, 1>("16x16x32: DMA + MFMA, order 0", gal, qry, Mt, T, out, reps);
+  run<1, 1, 1, 0, 2, 0, 1>("16x16x32: DMA + MFMA, order 2", gal, qry, Mt, T, out, reps);
   CK(hipFree(gal));
   CK(hipFree(qry));
   CK(hipFree(out));
