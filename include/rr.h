@@ -97,6 +97,8 @@ int rr_get_device(rr_handle_t h, int* device);
  *   RR_TUNE_SWEEP_PF: the 256x320 bf16 filter sweep: 1 = touch each gallery row's
  *                     line of k-tile kt + 2 while kt computes (L2 prefetch, DMA left in
  *                     flight across the barrier), 0 = off, -1 = the library's pick
+ *   RR_TUNE_SWEEP_MF16: the 256x320 bf16 filter sweep on v_mfma_f32_16x16x32_bf16 (1)
+ *                     or v_mfma_f32_32x32x16_bf16 (0); -1 = the library's pick
  * Any other key or value: RR_EINVAL. */
 #define RR_TUNE_GEMM_CFG 1
 #define RR_TUNE_GEMM_BK 2
@@ -105,6 +107,7 @@ int rr_get_device(rr_handle_t h, int* device);
 #define RR_TUNE_S3_STAGGER 5
 #define RR_TUNE_SWEEP_ORDER 6
 #define RR_TUNE_SWEEP_PF 7
+#define RR_TUNE_SWEEP_MF16 8
 int rr_set_tuning(rr_handle_t h, int key, int value);
 
 /* ---- search (ranker) ----------------------------------------------------

@@ -309,7 +309,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   // DMA, barrier, DMA tile kt+2 into the buffer just drained, read tile kt+1's
   // first fragments, THEN the last step's MFMAs — they hide the post-barrier
   // LDS latency that otherwise idles both waves of every SIMD at each k-tile.
-  constexpr bool PIPE16 = GL && MF16 && DT == DT_BF16;
+  constexpr bool PIPE16 = GL && MF16 == 1 && DT == DT_BF16;
   if constexpr (PIPE16) {
     constexpr int S = BK / 16;
     static_assert(S % 2 == 0, "PIPE16: an even number of k-steps per k-tile");
@@ -445,6 +445,40 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
                                                              acc[i][j], 0, 0, 0);
       }
     }
+    } else if constexpr (DT == DT_BF16 && MF16 == 2) {
+      // MF16 = 2 (the 256x320 filter sweep on v_mfma_f32_16x16x32_bf16): one
+      // fragment set per 32-deep k-step, read whole before its MFMAs (two sets
+      // do not fit beside the 160 accumulator registers); the partner wave on
+      // the SIMD covers the read latency.  Same lane -> k map as below.
+      constexpr int S = BK / 16;
+      const int l16 = lane & 15, lg = lane >> 4;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int st = 0; st < S; ++st) {
+        bf16x8 af[FM][2], bf[FN][2];
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = wm * WTM + i * 32 + h * 16 + l16;
+            af[i][h] = *reinterpret_cast<const bf16x8*>(la + row * BK + swz<BK>(row, 4 * st + lg) * 4);
+          }
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = wn * WTN + j * 32 + h * 16 + l16;
+            bf[j][h] = *reinterpret_cast<const bf16x8*>(lb + row * BK + swz<BK>(row, 4 * st + lg) * 4);
+          }
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int t = 0; t < 4; ++t)
+              acc4[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][t >> 1], bf[j][t & 1], acc4[i][j][t], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
     } else if constexpr (DT == DT_BF16 && MF16) {
       // BK/16 k-steps of 32; lane group g = lane>>4 holds k = 32s + 8g .. +7
       // = 16-B slot 4s + g of rows (lane & 15) of each 16-row half.
@@ -846,10 +880,11 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
     const int ord = tu.sweep_order < 0 ? 0 : tu.sweep_order;
     const int bn = (cfg == 4 && DT == DT_BF16) ? 320 : (cfg >= 3 ? 256 : (cfg == 2 ? 64 : 128));
     const long long tn = ((long long)g.N + bn - 1) / bn;
-    if ((ord > 0 && tn % ord == 0) || tu.sweep_pf > 0) {
+    if ((ord > 0 && tn % ord == 0) || tu.sweep_pf > 0 || tu.sweep_mf16 > 0) {
       GemmArgs g2 = g;
       if (ord > 0 && tn % ord == 0) g2.tile_order = ord;
       g2.l2_prefetch = tu.sweep_pf > 0;
+      g2.mf16_sweep = tu.sweep_mf16 > 0;
       return launch_lp_cfg<EM, DT>(g2, s, cfg);
     }
   }
@@ -869,10 +904,11 @@ static hipError_t launch_lp_cfg(const GemmArgs& g, hipStream_t s, int cfg) {
     case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF>(g, s);
     case 3: return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);
     case 4:  // bf16 sweeps only (fp8: the 256x256 tile; its 256x320 form spills the dequantisation)
-      if constexpr (EM != E_STORE && DT == DT_BF16) {
+      if constexpr (EM == E_FILTER && DT == DT_BF16) {
         if (g.l2_prefetch) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0, -1, 1>(g, s);
-        return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0>(g, s);
+        if (g.mf16_sweep) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 2>(g, s);
       }
+      if constexpr (EM != E_STORE && DT == DT_BF16) return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0>(g, s);
       else if constexpr (EM != E_STORE) return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);
       return hipErrorInvalidValue;
     default: return launch_t<2, 2, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF>(g, s);

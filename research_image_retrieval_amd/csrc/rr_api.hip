@@ -158,6 +158,10 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       if (!in({-1, 0, 1})) break;
       h->tune.sweep_pf = value;
       return RR_OK;
+    case RR_TUNE_SWEEP_MF16:
+      if (!in({-1, 0, 1})) break;
+      h->tune.sweep_mf16 = value;
+      return RR_OK;
     default:
       return set_error(h, RR_EINVAL, "rr_set_tuning: unknown key");
   }

@@ -21,6 +21,7 @@ struct rr_handle_s {
     int s3_stagger = -1;  // split-bf16 core round stagger in ~1 us sleeps (-1: the library's pick)
     int sweep_order = -1;  // bf16 / fp8 filter sweeps: block -> tile order (tile_coords); -1: the library's pick
     int sweep_pf = -1;     // bf16 256x320 filter sweep: L2 prefetch of the gallery two k-tiles ahead; -1: the pick
+    int sweep_mf16 = -1;   // bf16 256x320 filter sweep on v_mfma_f32_16x16x32_bf16 (1) or 32x32x16 (0); -1: the pick
   } tune;
   int n_cu = 0;  // compute units of the handle's device (device_cu_count)
   // timing (see rr_timing_enable)
@@ -222,8 +223,10 @@ struct GemmArgs {
   int POH = 0, POW = 0, pool_tr = 0, pool_tc = 0;
   // block -> tile order of the low-precision filter sweeps (tile_coords)
   int tile_order = 0;
-  // the 256x320 bf16 filter sweep's L2 prefetch of A (gemm_kernel PF)
+  // the 256x320 bf16 filter sweep's L2 prefetch of A (gemm_kernel PF), and
+  // its 16x16x32 MFMA form (gemm_kernel MF16 = 2)
   int l2_prefetch = 0;
+  int mf16_sweep = 0;
 };
 
 // Block -> (tm, tn) of a tiles_m x tiles_n grid (tm: A / gallery-row tiles,

@@ -347,3 +347,26 @@ def test_prefilter_sweep_l2_prefetch_bit_identical(cuda):
             out[pf] = ops.cosine_topk_prefilter(qd, gd, gbf, bound, 100)
     assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][0].view(torch.int32), out[1][0].view(torch.int32))
     assert int(out[1][1][0, 0]) == 3 and int(out[1][1][nq - 1, 0]) == n - 1
+
+
+def test_prefilter_sweep_mf16_bit_identical(cuda):
+    """The 256x320 bf16 filter sweep on v_mfma_f32_16x16x32_bf16 (rr_set_tuning
+    sweep_mf16): a different bf16 accumulation order inside the filter, the
+    same final ranking bit for bit (the rigorous bound covers any order; the
+    survivors are rescored exactly)."""
+    rs = np.random.RandomState(78)
+    d, nq, n = 2048, 1280, 70_003
+    g = rs.standard_normal((n, d)).astype(np.float32)
+    q = rs.standard_normal((nq, d)).astype(np.float32)
+    g[5], g[n - 1] = q[0], q[nq - 1]
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    qd, gd = torch.from_numpy(q).to(cuda), torch.from_numpy(g).to(cuda)
+    gbf, _ = ops.quantize_rows(gd, "bf16")
+    bound = ops.prefilter_gallery_bound(gd, gbf)
+    out = {}
+    for v in (0, 1):
+        with ops.tuning(cuda.index, sweep_mf16=v):
+            out[v] = ops.cosine_topk_prefilter(qd, gd, gbf, bound, 100)
+    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][0].view(torch.int32), out[1][0].view(torch.int32))
+    assert int(out[1][1][0, 0]) == 5 and int(out[1][1][nq - 1, 0]) == n - 1
