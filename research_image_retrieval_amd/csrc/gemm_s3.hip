@@ -1311,7 +1311,13 @@ constexpr int H2_EP = EP_SCALE | EP_AMAX | EP_BIAS;
 // 28}, whose (row >> 2) & 3 are four distinct values whatever the offset.
 __device__ __forceinline__ int hswz(int row, int slot) { return slot ^ ((row >> 2) & 3); }
 
-template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1>
+// MF = 1: v_mfma_f32_16x16x32_f16 (one 32-deep k-step per k-tile; each 32x32
+// tile of a wave is four 16x16 sub-tiles, the acc_row / acc_col<true> map),
+// which the chip holds at a higher clock than 32x32x16 in MFMA-dense loops
+// (MI355X_MICROARCH.md 'DVFS give-back' item 7; profiles/r04b_fetch_ceiling.txt:
+// register-only 0.875 vs 0.725 of the bf16 peak at two waves per SIMD).  A row
+// half's A fragments are read once, the B fragments once per row half.
+template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1, int MF = 0>
 __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int tiles_n) {
   constexpr int NP = 2, BK = 32, NT = 512, NW = 8;
   constexpr int WTM = 32 * FM, WTN = 32 * FN, BM = WTM * WM, BN = WTN * WN, SL = BK / 8;
@@ -1413,25 +1419,40 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
 
   // ---- the lanes' fragment rows: a 9-bit mask of the taps that stay inside
   // the row's image (bit kh KW + kw), empty past M ----
-  int tmask[FM];
+  // (MF: the lane's rows are i * 32 + 16 a + (lane & 15), a = 0, 1)
+  constexpr int RPT = MF ? 2 : 1;
+  const int l16 = lane & 15, lg = lane >> 4;
+  int tmask[FM][RPT];
 #pragma unroll
-  for (int i = 0; i < FM; ++i) {
-    const int m = m0 + wm * WTM + i * 32 + lr;
-    const int rem = m % (H * W), oh = rem / W, ow = rem - oh * W;
-    int mk = 0;
-    for (int kh = 0; kh < g.KH; ++kh)
-      for (int kw = 0; kw < KW; ++kw)
-        if ((unsigned)(oh + kh - g.pad) < (unsigned)H && (unsigned)(ow + kw - g.pad) < (unsigned)W) mk |= 1 << (kh * KW + kw);
-    tmask[i] = m < g.M ? mk : 0;
-  }
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int a = 0; a < RPT; ++a) {
+      const int m = m0 + wm * WTM + i * 32 + (MF ? 16 * a + l16 : lr);
+      const int rem = m % (H * W), oh = rem / W, ow = rem - oh * W;
+      int mk = 0;
+      for (int kh = 0; kh < g.KH; ++kh)
+        for (int kw = 0; kw < KW; ++kw)
+          if ((unsigned)(oh + kh - g.pad) < (unsigned)H && (unsigned)(ow + kw - g.pad) < (unsigned)W)
+            mk |= 1 << (kh * KW + kw);
+      tmask[i][a] = m < g.M ? mk : 0;
+    }
 
   f32x16 acc[FM][FN];
+  f32x4 acc4[MF ? FM : 1][MF ? FN : 1][4];
 #pragma unroll
   for (int i = 0; i < FM; ++i)
 #pragma unroll
     for (int j = 0; j < FN; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  if constexpr (MF) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t) acc4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   // one k-tile: tap t of halo buffer hb, B stage bs; two 16-deep k-steps, each
   // a0b0 first, then a0b1 + a1b0 (config 12's per-accumulator order)
@@ -1439,9 +1460,47 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     const int kh = t / KW, kw = t - kh * KW;
     const uint16_t* la = lds + hb * A_EL;
     const uint16_t* lb = lds + 2 * A_EL + bs * B_EL + u * B_TAP;
+    if constexpr (MF) {
+      // one 32-deep k-step: lane group lg holds k 8 lg .. +7 (16-B slot lg)
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        frag_t fa[NP][FM];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) {
+          const int ar = ((tmask[i][a] >> t) & 1) ? wm * WTM + i * 32 + 16 * a + l16 + kh * W + kw : HALO_HR;
+#pragma unroll
+          for (int p = 0; p < NP; ++p)
+            fa[p][i] = *reinterpret_cast<const frag_t*>(la + (p * HRA + ar) * BK + hswz(ar, lg) * 8);
+        }
+#pragma unroll
+        for (int b = 0; b < 2; ++b) {
+          frag_t fb[NP][FN];
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int row = wn * WTN + j * 32 + 16 * b + l16;
+#pragma unroll
+            for (int p = 0; p < NP; ++p)
+              fb[p][j] = *reinterpret_cast<const frag_t*>(lb + (p * BN + row) * BK + pswz<BK, 2>(row, lg) * 8);
+          }
+          // config 12's per-accumulator order: a0b0, then a0b1 + a1b0
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) acc4[i][j][2 * a + b] = s3_mf16<2>(fa[0][i], fb[0][j], acc4[i][j][2 * a + b]);
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j) {
+              acc4[i][j][2 * a + b] = s3_mf16<2>(fa[0][i], fb[1][j], acc4[i][j][2 * a + b]);
+              acc4[i][j][2 * a + b] = s3_mf16<2>(fa[1][i], fb[0][j], acc4[i][j][2 * a + b]);
+            }
+        }
+      }
+      return;
+    }
     int ar[FM];
 #pragma unroll
-    for (int i = 0; i < FM; ++i) ar[i] = ((tmask[i] >> t) & 1) ? wm * WTM + i * 32 + lr + kh * W + kw : HALO_HR;
+    for (int i = 0; i < FM; ++i) ar[i] = ((tmask[i][0] >> t) & 1) ? wm * WTM + i * 32 + lr + kh * W + kw : HALO_HR;
 #pragma unroll
     for (int st = 0; st < BK / 16; ++st) {
       frag_t a[NP][FM], b[NP][FN];
@@ -1539,7 +1598,18 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     }
   }
   __syncthreads();
-  epilogue_store<WM, WN, FM, FN, LDS_U16 / 2, false, EPI>(g, g.C, acc, reinterpret_cast<float*>(lds), m0, n0, a_isc);
+  if constexpr (MF) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int t = 0; t < 4; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[i][j][4 * t + e] = acc4[i][j][t][e];
+  }
+  epilogue_store<WM, WN, FM, FN, LDS_U16 / 2, (bool)MF, EPI>(g, g.C, acc, reinterpret_cast<float*>(lds), m0, n0,
+                                                             a_isc);
 }
 
 // config 13 serves: f16x2, conv A, 3x3 stride 1 pad 1 (output = input size),
@@ -1556,30 +1626,31 @@ static int h2_halo_rows(const GemmArgs& g) {
   if ((g.N % 64) == 0) return need <= 384 ? 384 : 0;
   return 0;
 }
-template <int EPI, int WM, int WN, int FM, int FN, int HR, int TPK>
+template <int EPI, int WM, int WN, int FM, int FN, int HR, int TPK, int MF>
 static hipError_t launch_h2_halo_t(const GemmArgs& g, hipStream_t s) {
   constexpr int BN = 32 * FN * WN;
   const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_h2_halo_kernel<EPI, WM, WN, FM, FN, HR, TPK>), dim3((unsigned)nblk), dim3(512), 0, s, g,
+  hipLaunchKernelGGL((gemm_h2_halo_kernel<EPI, WM, WN, FM, FN, HR, TPK, MF>), dim3((unsigned)nblk), dim3(512), 0, s, g,
                      (int)tiles_n);
   return hipGetLastError();
 }
-template <int WM, int WN, int FM, int FN, int HR, int TPK>
+template <int WM, int WN, int FM, int FN, int HR, int TPK, int MF>
 static hipError_t launch_h2_halo_ep(const GemmArgs& g, hipStream_t s) {
   switch (ep_flags(g) & (EP_RES | EP_RELU)) {
-    case EP_RELU: return launch_h2_halo_t<H2_EP | EP_RELU, WM, WN, FM, FN, HR, TPK>(g, s);
-    case EP_RES | EP_RELU: return launch_h2_halo_t<H2_EP | EP_RES | EP_RELU, WM, WN, FM, FN, HR, TPK>(g, s);
-    case EP_RES: return launch_h2_halo_t<H2_EP | EP_RES, WM, WN, FM, FN, HR, TPK>(g, s);
-    default: return launch_h2_halo_t<H2_EP, WM, WN, FM, FN, HR, TPK>(g, s);
+    case EP_RELU: return launch_h2_halo_t<H2_EP | EP_RELU, WM, WN, FM, FN, HR, TPK, MF>(g, s);
+    case EP_RES | EP_RELU: return launch_h2_halo_t<H2_EP | EP_RES | EP_RELU, WM, WN, FM, FN, HR, TPK, MF>(g, s);
+    case EP_RES: return launch_h2_halo_t<H2_EP | EP_RES, WM, WN, FM, FN, HR, TPK, MF>(g, s);
+    default: return launch_h2_halo_t<H2_EP, WM, WN, FM, FN, HR, TPK, MF>(g, s);
   }
 }
-static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s, int hr) {
-  if (hr == 288) return launch_h2_halo_ep<2, 4, 4, 2, 288, 1>(g, s);
-  if (hr == 320) return launch_h2_halo_ep<4, 2, 2, 2, 320, 1>(g, s);
-  return launch_h2_halo_ep<4, 2, 2, 1, 384, 3>(g, s);
+// mf: 1 = the 16x16x32 form (s3_cfg 14 forces it)
+static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s, int hr, int mf) {
+  if (hr == 288) return mf ? launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 1>(g, s) : launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 0>(g, s);
+  if (hr == 320) return mf ? launch_h2_halo_ep<4, 2, 2, 2, 320, 1, 1>(g, s) : launch_h2_halo_ep<4, 2, 2, 2, 320, 1, 0>(g, s);
+  return mf ? launch_h2_halo_ep<4, 2, 2, 1, 384, 3, 1>(g, s) : launch_h2_halo_ep<4, 2, 2, 1, 384, 3, 0>(g, s);
 }
 
 // config 8 serves dense A (1x1 convs), N % 256 == 0 and the ResNet's flag
@@ -1754,11 +1825,11 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
     // (N == 64 too: the 256x64 instance with three taps per barrier runs the
     // 64@56 3x3 layers 1.455 -> 1.297 ms; the 256x128 one lost on 128@28,
     // 0.888 -> 0.922 ms, and stays opt-in; profiles/r03w_h2_cfg_sweep.txt)
-    if (forced == 13 || (forced == 0 && ((g.N % 256) == 0 || g.N == 64))) {
-      if (const int hr = h2_halo_rows(g)) return launch_h2_halo(g, s, hr);
+    if (forced == 13 || forced == 14 || (forced == 0 && ((g.N % 256) == 0 || g.N == 64))) {
+      if (const int hr = h2_halo_rows(g)) return launch_h2_halo(g, s, hr, forced == 14 ? 1 : 0);
     }
   }
-  if (forced == 13) forced = 0;
+  if (forced == 13 || forced == 14) forced = 0;
   int cfg = pick_h2(g, forced);
   // N % 256 == 0: the 256x256 one-accumulator tile (config 12) everywhere but
   // the short-K residual expansions (K < 256: their epilogue dominates and the

@@ -143,7 +143,7 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.lp_cfg = value;
       return RR_OK;
     case RR_TUNE_S3_CFG:
-      if (value < 0 || value > 13) break;
+      if (value < 0 || value > 14) break;
       h->tune.s3_cfg = value;
       return RR_OK;
     case RR_TUNE_S3_STAGGER:

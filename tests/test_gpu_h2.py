@@ -186,7 +186,7 @@ TILE_SHAPES = [  # shapes that reach each f16x2 config's edges: ragged M, N = 64
 ]
 
 
-@pytest.mark.parametrize("cfg", [3, 4, 7, 8, 9, 10, 11, 12, 13])
+@pytest.mark.parametrize("cfg", [3, 4, 7, 8, 9, 10, 11, 12, 13, 14])
 @pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res", TILE_SHAPES)
 def test_conv2d_h2_tile_configs(cuda, cfg, b, h, w, cin, cout, k, s, p, res):
     """Every f16x2 tile config forced on every shape: fp32-grade vs float64
@@ -214,14 +214,16 @@ HALO_SHAPES = [  # stride-1 3x3, Cin % 32 == 0, N % 256 == 0, W <= 15: config 13
 ]
 
 
+@pytest.mark.parametrize("cfg", [13, 14])
 @pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res", HALO_SHAPES)
-def test_conv2d_h2_halo(cuda, b, h, w, cin, cout, k, s, p, res):
+def test_conv2d_h2_halo(cuda, cfg, b, h, w, cin, cout, k, s, p, res):
     """Config 13 (halo-staged A: each input pixel fetched once per Cin slice,
     taps read from the LDS halo, zero row for padding taps and rows past M):
     the same accuracy bar as every f16x2 conv against float64 and the
     exact-fp32 core, and the max-|y| record exact."""
     x, wt, bias, r, ref, scale = _conv_case(cuda, b, h, w, cin, cout, k, s, p, res, seed=13)
-    with ops.tuning(0, s3_cfg=13):
+    # config 14: the same tile on v_mfma_f32_16x16x32_f16 (four 16x16 sub-tiles per 32x32 tile)
+    with ops.tuning(0, s3_cfg=cfg):
         y, rec = _run_h2(cuda, x, wt, bias, r, s, p)
     y = y.cpu()
     rd = r.to(cuda) if res else None
@@ -229,7 +231,8 @@ def test_conv2d_h2_halo(cuda, b, h, w, cin, cout, k, s, p, res):
     live = ref > 0
     e = _rel_err(y[live], ref[live], scale[live])
     ef32 = _rel_err(y_f32[live], ref[live], scale[live])
-    print(f"halo {b}x{h}x{w}x{cin}->{cout}: max {e[0]:.3g} mean {e[1]:.3g} | f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
+    print(f"halo cfg {cfg} {b}x{h}x{w}x{cin}->{cout}: max {e[0]:.3g} mean {e[1]:.3g} | f32 max {ef32[0]:.3g} "
+          f"mean {ef32[1]:.3g}")
     assert e[0] <= 1.25 * max(ef32[0], 1e-7) and e[1] <= ef32[1] * 1.05 + 1e-9
     assert ops.amax_value(rec[1]) == float(y.abs().max())
     assert bool(torch.isfinite(y).all())

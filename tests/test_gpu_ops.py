@@ -118,9 +118,15 @@ def test_handle_device_and_tuning_validation(cuda):
     assert L.rr_get_device(h, ctypes.byref(d)) == 0 and d.value == cuda.index
     assert L.rr_set_tuning(h, 99, 1) == _lib.RR_EINVAL and b"unknown key" in L.rr_last_error(h)
     assert L.rr_set_tuning(h, _lib.TUNE_GEMM_CFG, 23) == _lib.RR_EINVAL
-    assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG, 14) == _lib.RR_EINVAL
-    for key in (_lib.TUNE_GEMM_CFG, _lib.TUNE_GEMM_BK, _lib.TUNE_LP_CFG, _lib.TUNE_S3_CFG):
+    assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG, 15) == _lib.RR_EINVAL
+    assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_ORDER, 3) == _lib.RR_EINVAL
+    assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_PF, 2) == _lib.RR_EINVAL
+    assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_MF16, 2) == _lib.RR_EINVAL
+    for key in (_lib.TUNE_GEMM_CFG, _lib.TUNE_GEMM_BK, _lib.TUNE_LP_CFG, _lib.TUNE_S3_CFG, _lib.TUNE_SWEEP_ORDER,
+                _lib.TUNE_SWEEP_PF, _lib.TUNE_SWEEP_MF16):
         assert L.rr_set_tuning(h, key, 0) == 0
+    for key in (_lib.TUNE_S3_STAGGER, _lib.TUNE_SWEEP_ORDER, _lib.TUNE_SWEEP_PF, _lib.TUNE_SWEEP_MF16):
+        assert L.rr_set_tuning(h, key, -1) == 0
     # a call made while another device is current still runs on the handle's device
     # (one-GPU box: the guard is exercised with the current device equal to the handle's)
     torch.cuda.set_device(cuda)
