@@ -85,8 +85,9 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     bf16 with K % 32 == 0 or fp8 with K % 128 == 0: gallery rows in
  *                     VGPRs, query panel in LDS, sweep_v.hip; otherwise the pick)
  *   RR_TUNE_S3_CFG:   split cores (bf16x3 and f16x2), 1..14 (gemm_s3.hip tile table;
- *                     9..14 f16x2 only; 13 = the halo-staged stride-1 3x3 tile, 14 = the
- *                     same on v_mfma_f32_16x16x32_f16;
+ *                     9..14 f16x2 only; 13 = the halo-staged stride-1 3x3 tile on
+ *                     v_mfma_f32_32x32x16_f16, 14 = the same on v_mfma_f32_16x16x32_f16
+ *                     (the default picks 14's form for cout % 256 == 0, 13's for cout 64);
  *                     7 also selects the implicit-GEMM fused stem over the halo stem)
  *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of
  *                     ~1 us for every other resident block (-1 = the library's pick)

@@ -1818,15 +1818,21 @@ static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int
 
 template <int AM>
 static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
-  // config 13 (halo A) is the pick for N % 256 == 0 and N == 64: the 3x3
+  // the halo-A tile (configs 13 / 14) is the pick for N % 256 == 0 and N == 64: the 3x3
   // 256@14 and 512@7 layers 2.7 % / 1.6 % faster than config 12 at 1280
   // images (profiles/r03t_h2_cfg_sweep.txt)
   if constexpr (AM == A_CONV) {
     // (N == 64 too: the 256x64 instance with three taps per barrier runs the
     // 64@56 3x3 layers 1.455 -> 1.297 ms; the 256x128 one lost on 128@28,
     // 0.888 -> 0.922 ms, and stays opt-in; profiles/r03w_h2_cfg_sweep.txt)
+    // The 256x256 instance (hr 288, the N % 256 layers) runs on
+    // v_mfma_f32_16x16x32_f16 by default: 256@14 0.716 -> 0.675 ms, 512@7
+    // 0.671 -> 0.606; the 256x64 one lost on 64@56 (1.225 -> 1.334 ms) and
+    // keeps the 32x32x16 form (profiles/r04c_h2_cfg_sweep.txt).  Forcing 13
+    // selects the 32x32x16 form everywhere, 14 the 16x16x32 form everywhere.
     if (forced == 13 || forced == 14 || (forced == 0 && ((g.N % 256) == 0 || g.N == 64))) {
-      if (const int hr = h2_halo_rows(g)) return launch_h2_halo(g, s, hr, forced == 14 ? 1 : 0);
+      if (const int hr = h2_halo_rows(g))
+        return launch_h2_halo(g, s, hr, forced == 14 ? 1 : forced == 13 ? 0 : (hr == 288 ? 1 : 0));
     }
   }
   if (forced == 13 || forced == 14) forced = 0;
