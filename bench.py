@@ -506,6 +506,8 @@ def main():
     ap.add_argument("--c2-queries", type=int, default=0, help="override every C2 set's query count (0: 70)")
     ap.add_argument("--c2-batch", type=int, default=C2_BATCH, help="same-size gallery images per extractor call")
     ap.add_argument("--c2-qstreams", type=int, default=8, help="HIP streams for the batch-1 query crops (1: serial)")
+    ap.add_argument("--tune", default="",
+                    help="A/B only: rr_set_tuning keys for the whole run, e.g. sweep_il=0,conv_il=0 (ops._TUNE_KEYS)")
     a = ap.parse_args()
     if a.workload == "c4":
         if a.dim == 2048:
@@ -545,6 +547,8 @@ def main():
         else:
             dist.init_process_group(backend)
 
+    if a.tune:  # held for the rest of the process (A/B runs; the default line sets nothing)
+        ops.tuning(dev.index, **{k: int(v) for k, v in (kv.split("=") for kv in a.tune.split(","))}).__enter__()
     if a.workload == "c2":
         return run_c2(a, world, rank, dev)
     t_setup = time.time()
@@ -842,6 +846,7 @@ def main():
                       "parallelism": f"query-dp{world} + gallery-shard{world}",
                       "conv_math": a.conv_math if a.workload != "c4" else None,
                       "pipeline": bool(a.pipeline),
+                      **({"tuning": a.tune} if a.tune else {}),
                       "ranker_workspace_bytes_per_rank": int(ws.numel()),
                       "ranker_workspace_worst_case_bytes": int(ws_full)},
            "roofline": roof, "roofline_by_kernel": rk}

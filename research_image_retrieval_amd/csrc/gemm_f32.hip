@@ -65,6 +65,22 @@ __device__ __forceinline__ void interleave() {
   if constexpr (NM > NR) __builtin_amdgcn_sched_group_barrier(0x008, NM - NR, 0);
 }
 
+// interleave<nr, NM> with the next k-tile's LDS-DMA chunks spread among the
+// MFMAs (IL sweeps): chunk c of NCH goes out before MFMA number (c * SPAN) /
+// NCH of the k-tile; base = the k-tile's MFMA number of this region's first
+// (base and nr constant once the caller's k-step loop is unrolled).
+template <int NM, int SPAN, int NCH>
+__device__ __forceinline__ void interleave_il(int base, int nr) {
+#pragma unroll
+  for (int x = 0; x < NM; ++x) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      if ((c * SPAN) / NCH == base + x) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 VMEM (the DMA)
+    __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                      // 1 MFMA
+    if (x < nr) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                          // 1 DS read
+  }
+}
+
 // Same with two DS reads per MFMA (NP pairs, NM >= NP MFMAs): the fp8 k-step
 // reads 32 bytes (two ds_read_b128) per fragment.
 template <int NP, int NM>
@@ -91,8 +107,14 @@ __device__ __forceinline__ void interleave2() {
 // the HBM fetch has two k-tiles of lead time and the real DMA of kt + 2 hits
 // L2; that DMA stays in flight across the k-tile's barrier (counted vmcnt and
 // a raw s_barrier instead of __syncthreads' vmcnt(0)).
+// IL (LDS-DMA bf16 filter sweeps): the next k-tile's DMA is not issued as one
+// burst at the top of the k-tile but chunk by chunk among the first SPAN
+// MFMAs (18 of 40 on 32x32x16, 36 of 80 on 16x16x32): a burst of 9
+// instructions from all 8 waves at once fills the vector-memory issue queue
+// and stalls the waves' MFMAs behind it (tools/fetch_ceiling.hip, r04e:
+// 0.481 -> 0.525 of peak on the bare 32x32x16 sweep loop).
 template <int WM, int WN, int FM, int FN, int AMODE, int EMODE, int BK, int DT, int MINB, int GL, int MF16 = 0,
-          int EPI = -1, int PF = 0>
+          int EPI = -1, int PF = 0, int IL = 0>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, int tiles_n) {
   using ET = typename ElemT<DT>::T;
   static_assert(!MF16 || DT == DT_BF16, "MF16: bf16 only");
@@ -269,6 +291,35 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     }
   };
 
+  // IL: chunk c (A rows, then B rows) of glds_tile(kt, buf), due before MFMA
+  // number idx; past the last k-tile it re-fetches the last one (an L2 hit)
+  // into the drained buffer, so every iteration issues the same DMAs
+  static_assert(!IL || (GL && DT == DT_BF16 && MF16 != 1 && !PF && EMODE == E_FILTER), "IL: LDS-DMA bf16 filter sweeps");
+  constexpr int NCH = A_CH + B_CH;
+  constexpr int IL_SPAN = IL ? (MF16 == 2 ? 36 : 18) : 0;
+  static_assert(IL_SPAN <= (MF16 == 2 ? 4 * FM * FN * (BK / 16) : FM * FN * (BK / 8)),
+                "IL: every chunk before an MFMA of the k-tile");
+  auto glds_due = [&](int kt, int buf, int idx) {
+    if constexpr (IL) {
+      const int kc = kt < nk ? kt : nk - 1;
+      float* la = lds + buf * BUF;
+      float* lb = la + BM * BK;
+      const int wv = tid >> 6;
+#pragma unroll
+      for (int c = 0; c < NCH; ++c) {
+        if ((c * IL_SPAN) / NCH != idx) continue;
+        const bool is_a = c < A_CH;
+        const int i = is_a ? c : c - A_CH;
+        const int row = crow + i * ROWS_PER_PASS;
+        const ET* src = (is_a ? a_ptr[is_a ? i : 0] : b_ptr[is_a ? 0 : i]) + (long long)kc * EPR + swz<BK>(row, slot) * CH;
+        __builtin_amdgcn_global_load_lds((const void*)src,
+                                         (__attribute__((address_space(3))) void*)((is_a ? la : lb) +
+                                                                                   (i * ROWS_PER_PASS + wv * (64 / SLOTS)) * BK),
+                                         16, 0, 0);
+      }
+    }
+  };
+
   auto store_tile = [&](int buf) {
     float* la = lds + buf * BUF;
     float* lb = la + BM * BK;
@@ -411,7 +462,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
 
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) {
+    if (!IL && kt + 1 < nk) {
       if constexpr (GL) glds_tile(kt + 1, cur ^ 1);
       else load_tile(kt + 1);
     }
@@ -475,8 +526,11 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int t = 0; t < 4; ++t)
+            for (int t = 0; t < 4; ++t) {
+              glds_due(kt + 1, cur ^ 1, st * 4 * FM * FN + (j * FM + i) * 4 + t);
               acc4[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][t >> 1], bf[j][t & 1], acc4[i][j][t], 0, 0, 0);
+            }
+        if constexpr (IL) interleave_il<4 * FM * FN, IL_SPAN, NCH>(st * 4 * FM * FN, 0);
       }
       __builtin_amdgcn_s_setprio(0);
     } else if constexpr (DT == DT_BF16 && MF16) {
@@ -545,9 +599,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
 #pragma unroll
         for (int i = 0; i < FM; ++i)
 #pragma unroll
-          for (int j = 0; j < FN; ++j)
+          for (int j = 0; j < FN; ++j) {
+            glds_due(kt + 1, cur ^ 1, st * FM * FN + i * FN + j);
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[st & 1][i], bf[st & 1][j], acc[i][j], 0, 0, 0);
-        if (st + 1 < S) interleave<FM + FN, FM * FN>();
+          }
+        if constexpr (IL) interleave_il<FM * FN, IL_SPAN, NCH>(st * FM * FN, st + 1 < S ? FM + FN : 0);
+        else if (st + 1 < S) interleave<FM + FN, FM * FN>();
       }
       __builtin_amdgcn_s_setprio(0);
     } else {
@@ -733,7 +790,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
 }
 
 template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0,
-          int EPI = -1, int PF = 0>
+          int EPI = -1, int PF = 0, int IL = 0>
 static hipError_t launch_t1(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM;
@@ -742,7 +799,7 @@ static hipError_t launch_t1(const GemmArgs& g, hipStream_t s) {
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
   const unsigned splits = g.k_split > 0 ? (unsigned)((g.K + g.k_split - 1) / g.k_split) : 1u;
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EPI, PF>), dim3((unsigned)nblk, splits),
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EPI, PF, IL>), dim3((unsigned)nblk, splits),
                      dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
@@ -880,13 +937,16 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
     const int ord = tu.sweep_order < 0 ? 0 : tu.sweep_order;
     const int bn = (cfg == 4 && DT == DT_BF16) ? 320 : (cfg >= 3 ? 256 : (cfg == 2 ? 64 : 128));
     const long long tn = ((long long)g.N + bn - 1) / bn;
-    if ((ord > 0 && tn % ord == 0) || tu.sweep_pf > 0 || tu.sweep_mf16 > 0) {
-      GemmArgs g2 = g;
-      if (ord > 0 && tn % ord == 0) g2.tile_order = ord;
-      g2.l2_prefetch = tu.sweep_pf > 0;
-      g2.mf16_sweep = tu.sweep_mf16 > 0;
-      return launch_lp_cfg<EM, DT>(g2, s, cfg);
-    }
+    // the 256x320 bf16 tile's defaults: v_mfma_f32_16x16x32_bf16 with the
+    // next k-tile's DMA spread among the MFMAs (sweep_mf16, sweep_il: measured
+    // on the C3 sweep, 1280 near-parallel queries x 1.6 M x 2048, 7.99 ->
+    // 7.46 ms, bit-identical rankings; profiles/r04f_sweep_il_ab.txt)
+    GemmArgs g2 = g;
+    if (ord > 0 && tn % ord == 0) g2.tile_order = ord;
+    g2.l2_prefetch = tu.sweep_pf > 0;
+    g2.mf16_sweep = tu.sweep_mf16 != 0;
+    g2.issue_spread = tu.sweep_il != 0;
+    return launch_lp_cfg<EM, DT>(g2, s, cfg);
   }
   return launch_lp_cfg<EM, DT>(g, s, cfg);
 }
@@ -906,7 +966,9 @@ static hipError_t launch_lp_cfg(const GemmArgs& g, hipStream_t s, int cfg) {
     case 4:  // bf16 sweeps only (fp8: the 256x256 tile; its 256x320 form spills the dequantisation)
       if constexpr (EM == E_FILTER && DT == DT_BF16) {
         if (g.l2_prefetch) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0, -1, 1>(g, s);
+        if (g.mf16_sweep && g.issue_spread) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 2, -1, 0, 1>(g, s);
         if (g.mf16_sweep) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 2>(g, s);
+        if (g.issue_spread) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0, -1, 0, 1>(g, s);
       }
       if constexpr (EM != E_STORE && DT == DT_BF16) return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0>(g, s);
       else if constexpr (EM != E_STORE) return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);

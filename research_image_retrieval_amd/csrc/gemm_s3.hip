@@ -205,12 +205,18 @@ struct S3Phases {
 // 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
 // 'DVFS give-back' item 7).  The k-tile's MFMAs go in two parts around the A
 // split: a0b0 + a1b1 + a0b1 + a1b0 (planes 0-1), then a0b2 + a2b0 (plane 2).
+// IL (the 32x32x16 two-stage loop, dense or Cin % 32 == 0 conv A): the next
+// k-tiles' B DMA and A loads are not issued as one burst at the top of the
+// k-tile but one instruction group at a time among the first MFMAs of its
+// first k-step (see gemm_f32.hip IL: a burst of every wave's loads at once
+// fills the vector-memory issue queue and stalls the MFMAs behind it).
 template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0, int EPI = -1, int SP = 3,
-          int NSTG = 2, int POOL = 0, int ACC1 = 0>
+          int NSTG = 2, int POOL = 0, int ACC1 = 0, int IL = 0>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
   static_assert(!ACC1 || SP == 2, "one accumulator: the f16x2 split");
   static_assert(!POOL || (AMODE == A_CONV_C4 && WM * 32 * FM == 256 && SP == 2), "stem + max-pool: 256-row NHWC4 tile");
   static_assert(NSTG == 2 || (NSTG == 3 && MF16 && SP == 2), "three LDS stages: the f16x2 16x16x32 tile");
+  static_assert(!IL || (!MF16 && NSTG == 2 && !POOL), "IL: the 32x32x16 two-stage loop");
   static_assert(!MF16 || BK == 32, "MF16: BK 32");
   static_assert(SP == 2 || SP == 3, "split kind");
   static_assert(SP == 3 || (EPI >= 0 && (EPI & EP_SCALE)), "f16x2: scaled epilogue");
@@ -373,6 +379,21 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       }
     }
   };
+  // IL: chunk i of load_a(kt, rb) alone (dense or Cin % 32 == 0 conv A)
+  auto load_a_chunk = [&](int kt, int rb, int i) {
+    static_assert(!IL || AMODE == A_DENSE || AMODE == A_CONV, "IL: dense or Cin % 32 == 0 conv A");
+    f32x4(&ra)[A_CH][2] = ra2[rb];
+    if constexpr (AMODE == A_DENSE) {
+      const f32x4* p = a_ok[i] ? reinterpret_cast<const f32x4*>(a_ptr[i] + kt * BK) : s3_zero_page();
+      s3_load2<1>(p, ra[i]);
+    } else if constexpr (AMODE == A_CONV) {
+      tap_to(kt);
+      const int ih = a_ih0[i] + tp_kh, iw = a_iw0[i] + tp_kw;
+      const bool ok = a_ok[i] && (unsigned)ih < (unsigned)g.H && (unsigned)iw < (unsigned)g.W;
+      const f32x4* p = ok ? reinterpret_cast<const f32x4*>(a_ptr[i] + tp_off) : s3_zero_page();
+      s3_load2<1>(p, ra[i]);
+    }
+  };
   // split the staged fp32 chunks into the three packed bf16 planes
   u32x4 pk[A_CH][NP];
   auto split_a = [&](int rb) {
@@ -439,6 +460,31 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
                                        16, 0, 0);
   };
 
+  auto glds_b_one = [&](int kt, int buf, int i) {
+    uint16_t* lb = lds + buf * BUF + A_EL;
+    __builtin_amdgcn_global_load_lds((const void*)(b_src[i] + (long long)kt * BK),
+                                     (__attribute__((address_space(3))) void*)(lb + min(i * NW + wave, B_TI - 1) * B_RPI * BK),
+                                     16, 0, 0);
+  };
+  // IL: the iteration's load groups in issue order (B DMA of kt + 1, then the
+  // A chunks of kt + 2: the counted waits assume that order), group q before
+  // MFMA number 2q of the first k-step, each fenced in place
+  constexpr int IL_GROUPS = B_INS + A_CH;
+  // every group's MFMA number exists: 0 .. FM FN - 1 (a0b0), then FM FN + 2m
+  static_assert(!IL || ((FM * FN) % 2 == 0 && 2 * (IL_GROUPS - 1) < 3 * FM * FN), "IL: a slot for every load group");
+  auto il_issue = [&](int kt, int cur, int idx) {
+    if constexpr (IL) {
+#pragma unroll
+      for (int q = 0; q < IL_GROUPS; ++q) {
+        if (2 * q != idx) continue;
+        __builtin_amdgcn_sched_barrier(0);
+        if (q < B_INS) glds_b_one(min(kt + 1, nk - 1), cur ^ 1, q);
+        else load_a_chunk(min(kt + 2, nk - 1), cur, q - B_INS);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
   f32x16 hi[FM][FN];
   f32x16 lo[ACC1 ? 1 : FM][ACC1 ? 1 : FN];
 #pragma unroll
@@ -451,7 +497,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
         if constexpr (!ACC1) lo[i][j][r] = 0.f;
       }
 
-  auto compute_st = [&](int cur, int st) {
+  // IL, first k-step: iteration kt_il's loads go out among the MFMAs
+  auto compute_st = [&](int cur, int st, int kt_il = 0) {
     const uint16_t* la = lds + cur * BUF;
     const uint16_t* lb = la + A_EL;
     {
@@ -472,11 +519,19 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < FN; ++j) hi[i][j] = s3_mf32<SP>(a[0][i], b[0][j], hi[i][j]);
+        for (int j = 0; j < FN; ++j) {
+          if constexpr (IL) {
+            if (st == 0) il_issue(kt_il, cur, i * FN + j);
+          }
+          hi[i][j] = s3_mf32<SP>(a[0][i], b[0][j], hi[i][j]);
+        }
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) {
+          if constexpr (IL) {
+            if (st == 0) il_issue(kt_il, cur, FM * FN + 2 * (i * FN + j));
+          }
           f32x16& L = ACC1 ? hi[i][j] : lo[ACC1 ? 0 : i][ACC1 ? 0 : j];
           if constexpr (SP == 3) {
             L = s3_mf32<SP>(a[1][i], b[1][j], L);
@@ -716,8 +771,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       auto iter = [&](int kt, int cur) __attribute__((always_inline)) {
-        glds_b(min(kt + 1, nk - 1), cur ^ 1);
-        load_a(min(kt + 2, nk - 1), cur);
+        if constexpr (!IL) {
+          glds_b(min(kt + 1, nk - 1), cur ^ 1);
+          load_a(min(kt + 2, nk - 1), cur);
+        }
         if constexpr (MF16 && AMODE == A_DENSE && SP == 3) {
           mf_dense0(cur);
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
@@ -737,7 +794,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
           mf_rest(cur, cur ^ 1, cur ^ 1);
           RR_PH(3);
         } else {
-          compute_st(cur, 0);
+          compute_st(cur, 0, kt);
           // A(kt+1) landed: its split overlaps the remaining MFMAs of tile kt
           asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");
           launder_a(cur ^ 1);
@@ -1317,7 +1374,10 @@ __device__ __forceinline__ int hswz(int row, int slot) { return slot ^ ((row >> 
 // (MI355X_MICROARCH.md 'DVFS give-back' item 7; profiles/r04b_fetch_ceiling.txt:
 // register-only 0.875 vs 0.725 of the bf16 peak at two waves per SIMD).  A row
 // half's A fragments are read once, the B fragments once per row half.
-template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1, int MF = 0>
+// IL (16x16x32, one tap per barrier): the next k-tile's B DMA goes out one
+// instruction at a time among the k-tile's first MFMAs instead of as one
+// burst before them (the halo pass load stays at the top: it comes from HBM).
+template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1, int MF = 0, int IL = 0>
 __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int tiles_n) {
   constexpr int NP = 2, BK = 32, NT = 512, NW = 8;
   constexpr int WTM = 32 * FM, WTN = 32 * FN, BM = WTM * WM, BN = WTN * WN, SL = BK / 8;
@@ -1417,6 +1477,29 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     }
   };
 
+  static_assert(!IL || (MF && TPK == 1 && B_INS <= FM * FN), "IL: the 16x16x32 one-tap-per-barrier tile");
+  // IL: DMA instruction i of glds_b(kt, buf), before a0b0 MFMA number
+  // i * IL_STEP of the k-tile's first (row half, column half) block
+  constexpr int IL_STEP = (FM * FN) / B_INS;
+  auto glds_b_due = [&](int kt, int buf, int idx) {
+    if constexpr (IL) {
+      const int c = kt / ngrp, t0 = kt - c * ngrp;
+      const long long koff = (long long)t0 * g.Cin + c * BK;
+      uint16_t* lb = lds + 2 * A_EL + buf * B_EL;
+#pragma unroll
+      for (int i = 0; i < B_INS; ++i) {
+        if (i * IL_STEP != idx) continue;
+        const uint16_t* src = BN == 256 ? b_src[0] + (i >> 1) * g.b_plane + (long long)(i & 1) * (BN / 2) * g.ldb
+                                        : b_src[BN == 256 ? 0 : i];
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_global_load_lds((const void*)(src + koff),
+                                         (__attribute__((address_space(3))) void*)(lb + (i * NW + wave) * B_RPI * BK),
+                                         16, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    }
+  };
+
   // ---- the lanes' fragment rows: a 9-bit mask of the taps that stay inside
   // the row's image (bit kh KW + kw), empty past M ----
   // (MF: the lane's rows are i * 32 + 16 a + (lane & 15), a = 0, 1)
@@ -1456,7 +1539,8 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
 
   // one k-tile: tap t of halo buffer hb, B stage bs; two 16-deep k-steps, each
   // a0b0 first, then a0b1 + a1b0 (config 12's per-accumulator order)
-  auto compute = [&](int hb, int bs, int t, int u) {
+  // kt_next: the k-tile whose B DMA an IL tile issues among these MFMAs
+  auto compute = [&](int hb, int bs, int t, int u, int kt_next = 0) {
     const int kh = t / KW, kw = t - kh * KW;
     const uint16_t* la = lds + hb * A_EL;
     const uint16_t* lb = lds + 2 * A_EL + bs * B_EL + u * B_TAP;
@@ -1486,7 +1570,12 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
-            for (int j = 0; j < FN; ++j) acc4[i][j][2 * a + b] = s3_mf16<2>(fa[0][i], fb[0][j], acc4[i][j][2 * a + b]);
+            for (int j = 0; j < FN; ++j) {
+              if constexpr (IL) {
+                if (a == 0 && b == 0) glds_b_due(kt_next, bs ^ 1, i * FN + j);
+              }
+              acc4[i][j][2 * a + b] = s3_mf16<2>(fa[0][i], fb[0][j], acc4[i][j][2 * a + b]);
+            }
 #pragma unroll
           for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -1570,7 +1659,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   int c = 0, tg = 0;
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = c + 1 < nch;
-    glds_b(min(kt + 1, nk - 1), (kt + 1) & 1);
+    if constexpr (!IL) glds_b(min(kt + 1, nk - 1), (kt + 1) & 1);
     if constexpr (TPK == 1) {
       if (more && tg >= 1 && tg <= A_PASS) store_pass((c + 1) & 1, tg - 1);
       if (more && tg < A_PASS) load_pass(c + 1, tg);
@@ -1586,7 +1675,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
       }
     }
 #pragma unroll
-    for (int u = 0; u < TPK; ++u) compute(c & 1, kt & 1, tg * TPK + u, u);
+    for (int u = 0; u < TPK; ++u) compute(c & 1, kt & 1, tg * TPK + u, u, min(kt + 1, nk - 1));
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next B (and a halo pass)
     launder_pass();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1626,28 +1715,30 @@ static int h2_halo_rows(const GemmArgs& g) {
   if ((g.N % 64) == 0) return need <= 384 ? 384 : 0;
   return 0;
 }
-template <int EPI, int WM, int WN, int FM, int FN, int HR, int TPK, int MF>
+template <int EPI, int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int IL = 0>
 static hipError_t launch_h2_halo_t(const GemmArgs& g, hipStream_t s) {
   constexpr int BN = 32 * FN * WN;
   const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_h2_halo_kernel<EPI, WM, WN, FM, FN, HR, TPK, MF>), dim3((unsigned)nblk), dim3(512), 0, s, g,
-                     (int)tiles_n);
+  hipLaunchKernelGGL((gemm_h2_halo_kernel<EPI, WM, WN, FM, FN, HR, TPK, MF, IL>), dim3((unsigned)nblk), dim3(512), 0, s,
+                     g, (int)tiles_n);
   return hipGetLastError();
 }
-template <int WM, int WN, int FM, int FN, int HR, int TPK, int MF>
+template <int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int IL = 0>
 static hipError_t launch_h2_halo_ep(const GemmArgs& g, hipStream_t s) {
   switch (ep_flags(g) & (EP_RES | EP_RELU)) {
-    case EP_RELU: return launch_h2_halo_t<H2_EP | EP_RELU, WM, WN, FM, FN, HR, TPK, MF>(g, s);
-    case EP_RES | EP_RELU: return launch_h2_halo_t<H2_EP | EP_RES | EP_RELU, WM, WN, FM, FN, HR, TPK, MF>(g, s);
-    case EP_RES: return launch_h2_halo_t<H2_EP | EP_RES, WM, WN, FM, FN, HR, TPK, MF>(g, s);
-    default: return launch_h2_halo_t<H2_EP, WM, WN, FM, FN, HR, TPK, MF>(g, s);
+    case EP_RELU: return launch_h2_halo_t<H2_EP | EP_RELU, WM, WN, FM, FN, HR, TPK, MF, IL>(g, s);
+    case EP_RES | EP_RELU: return launch_h2_halo_t<H2_EP | EP_RES | EP_RELU, WM, WN, FM, FN, HR, TPK, MF, IL>(g, s);
+    case EP_RES: return launch_h2_halo_t<H2_EP | EP_RES, WM, WN, FM, FN, HR, TPK, MF, IL>(g, s);
+    default: return launch_h2_halo_t<H2_EP, WM, WN, FM, FN, HR, TPK, MF, IL>(g, s);
   }
 }
 // mf: 1 = the 16x16x32 form (s3_cfg 14 forces it)
 static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s, int hr, int mf) {
+  // (the 16x16x32 256x256 form with its B DMA spread among the MFMAs: conv_il)
+  if (hr == 288 && mf && g.issue_spread) return launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 1, 1>(g, s);
   if (hr == 288) return mf ? launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 1>(g, s) : launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 0>(g, s);
   if (hr == 320) return mf ? launch_h2_halo_ep<4, 2, 2, 2, 320, 1, 1>(g, s) : launch_h2_halo_ep<4, 2, 2, 2, 320, 1, 0>(g, s);
   return mf ? launch_h2_halo_ep<4, 2, 2, 1, 384, 3, 1>(g, s) : launch_h2_halo_ep<4, 2, 2, 1, 384, 3, 0>(g, s);
@@ -1682,7 +1773,7 @@ static hipError_t launch_s3p(const GemmArgs& g, hipStream_t s, int n_cu, int st)
 }
 
 template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int EPI = -1, int SP = 3,
-          int NSTG = 2, int POOL = 0, int ACC1 = 0>
+          int NSTG = 2, int POOL = 0, int ACC1 = 0, int IL = 0>
 static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = (g.N + BN - 1) / BN;
@@ -1693,7 +1784,7 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
   constexpr int PER_CU = (MINB * 4) / (WM * WN) > 1 ? (MINB * 4) / (WM * WN) : 1;
   g.stagger_blocks = n_cu * PER_CU;
   g.stagger_sleeps = nblk > 2LL * n_cu * PER_CU ? stagger : 0;  // only grids of several rounds
-  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16, EPI, SP, NSTG, POOL, ACC1>), dim3((unsigned)nblk),
+  hipLaunchKernelGGL((gemm_s3_kernel<WM, WN, FM, FN, BK, AM, MINB, MF16, EPI, SP, NSTG, POOL, ACC1, IL>), dim3((unsigned)nblk),
                      dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
@@ -1768,18 +1859,18 @@ static int pick_h2(const GemmArgs& g, int forced) {
 // conv + BN + ReLU, + residual + ReLU, projection conv + BN (f16x2: the four
 // residual / ReLU combinations of H2_EP).
 template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int SP = 3, int NSTG = 2,
-          int ACC1 = 0>
+          int ACC1 = 0, int IL = 0>
 static hipError_t launch_s3_ep(const GemmArgs& g, hipStream_t s, int n_cu, int st) {
   if constexpr (SP == 2) {
     switch (ep_flags(g) & (EP_RES | EP_RELU)) {
       case EP_RELU:
-        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RELU, 2, NSTG, 0, ACC1>(g, s, n_cu, st);
+        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RELU, 2, NSTG, 0, ACC1, IL>(g, s, n_cu, st);
       case EP_RES | EP_RELU:
-        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RES | EP_RELU, 2, NSTG, 0, ACC1>(g, s, n_cu,
-                                                                                                         st);
+        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RES | EP_RELU, 2, NSTG, 0, ACC1, IL>(g, s,
+                                                                                                             n_cu, st);
       case EP_RES:
-        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RES, 2, NSTG, 0, ACC1>(g, s, n_cu, st);
-      default: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP, 2, NSTG, 0, ACC1>(g, s, n_cu, st);
+        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP | EP_RES, 2, NSTG, 0, ACC1, IL>(g, s, n_cu, st);
+      default: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP, 2, NSTG, 0, ACC1, IL>(g, s, n_cu, st);
     }
   } else {
     switch (ep_flags(g)) {
@@ -1862,7 +1953,11 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
     case 9: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1, 2, 3>(g, s, n_cu, st);
     case 10: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1, 2, 2, 1>(g, s, n_cu, st);
     case 11: return launch_s3_ep<2, 2, 2, 2, 32, AM, 2, 1, 2, 2, 1>(g, s, n_cu, st);
-    case 12: return launch_s3_ep<2, 4, 4, 2, 32, AM, 1, 0, 2, 2, 1>(g, s, n_cu, st);
+    case 12:
+      if constexpr (AM != A_CONV_C4) {
+        if (g.issue_spread) return launch_s3_ep<2, 4, 4, 2, 32, AM, 1, 0, 2, 2, 1, 1>(g, s, n_cu, st);
+      }
+      return launch_s3_ep<2, 4, 4, 2, 32, AM, 1, 0, 2, 2, 1>(g, s, n_cu, st);
     case 7: return launch_s3_ep<8, 1, 1, 2, 16, AM, 4, 0, 2>(g, s, n_cu, st);
     default: return launch_s3_ep<4, 2, 2, 2, 32, AM, 1, 0, 2>(g, s, n_cu, st);
   }
@@ -2133,11 +2228,16 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
     TimedLaunch tl(h, timer_cls, s);
     const int f = h->tune.s3_cfg;
     const int n_cu = device_cu_count(h);
-    if (sp == 2)
-      e = amode == A_DENSE ? launch_h2_am<A_DENSE>(g, s, f, n_cu, st)
-          : amode == A_CONV ? launch_h2_am<A_CONV>(g, s, f, n_cu, st)
-                            : launch_h2_am<A_CONV_C4>(g, s, f, n_cu, st);
-    else
+    if (sp == 2) {
+      // the 256x256 tile's loads spread among its MFMAs by default: every
+      // R101 layer it serves 1-3 % faster at 1280 images (256->1024 0.681 ->
+      // 0.668 ms, 1024->512 0.770 -> 0.751; profiles/r04g_h2_cfg_il.txt)
+      GemmArgs g2 = g;
+      g2.issue_spread = h->tune.conv_il != 0;
+      e = amode == A_DENSE ? launch_h2_am<A_DENSE>(g2, s, f, n_cu, st)
+          : amode == A_CONV ? launch_h2_am<A_CONV>(g2, s, f, n_cu, st)
+                            : launch_h2_am<A_CONV_C4>(g2, s, f, n_cu, st);
+    } else
       e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s, f, n_cu, st)
           : amode == A_CONV ? launch_s3_am<A_CONV>(g, s, f, n_cu, st)
                             : launch_s3_am<A_CONV_C4>(g, s, f, n_cu, st);

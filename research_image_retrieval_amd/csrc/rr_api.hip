@@ -162,6 +162,14 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       if (!in({-1, 0, 1})) break;
       h->tune.sweep_mf16 = value;
       return RR_OK;
+    case RR_TUNE_SWEEP_IL:
+      if (!in({-1, 0, 1})) break;
+      h->tune.sweep_il = value;
+      return RR_OK;
+    case RR_TUNE_CONV_IL:
+      if (!in({-1, 0, 1})) break;
+      h->tune.conv_il = value;
+      return RR_OK;
     default:
       return set_error(h, RR_EINVAL, "rr_set_tuning: unknown key");
   }

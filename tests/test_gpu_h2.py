@@ -256,6 +256,25 @@ def test_h2_persistent_tile_bit_identical(cuda):
     assert torch.equal(y9[4], y9[9])
 
 
+@pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res,cfg", [
+    (3, 29, 31, 256, 1024, 1, 1, 0, True, 12),   # 1x1 + residual (dense A), ragged last tile
+    (2, 14, 14, 1024, 256, 1, 1, 0, False, 12),  # 1x1, K = 1024
+    (2, 15, 13, 256, 512, 3, 2, 1, False, 12),   # strided 3x3 (implicit-GEMM conv A)
+    (2, 14, 15, 256, 256, 3, 1, 1, False, 14),   # halo 3x3, 16x16x32 form
+])
+def test_h2_issue_spread_bit_identical(cuda, b, h, w, cin, cout, k, s, p, res, cfg):
+    """conv_il: the 256x256 conv tile and the 16x16x32 halo tile with their
+    next k-tiles' loads issued among the MFMAs compute the same products in
+    the same order as with one burst at the top of the k-tile: identical
+    bits."""
+    x, wt, bias, r, _, _ = _conv_case(cuda, b, h, w, cin, cout, k, s, p, res, seed=11)
+    outs = {}
+    for il in (0, 1):
+        with ops.tuning(0, s3_cfg=cfg, conv_il=il):
+            outs[il] = _run_h2(cuda, x, wt, bias, r, s, p)[0].cpu()
+    assert torch.equal(outs[0], outs[1])
+
+
 def test_conv2d_h2_nonfinite_inputs(cuda):
     """An inf / NaN activation turns the outputs that read it into NaN / inf
     as fp32 does, and leaves every other output fp32-accurate (non-finite

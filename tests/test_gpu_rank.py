@@ -349,11 +349,13 @@ def test_prefilter_sweep_l2_prefetch_bit_identical(cuda):
     assert int(out[1][1][0, 0]) == 3 and int(out[1][1][nq - 1, 0]) == n - 1
 
 
-def test_prefilter_sweep_mf16_bit_identical(cuda):
+@pytest.mark.parametrize("il", [0, 1])
+def test_prefilter_sweep_mf16_bit_identical(cuda, il):
     """The 256x320 bf16 filter sweep on v_mfma_f32_16x16x32_bf16 (rr_set_tuning
     sweep_mf16): a different bf16 accumulation order inside the filter, the
     same final ranking bit for bit (the rigorous bound covers any order; the
-    survivors are rescored exactly)."""
+    survivors are rescored exactly).  il = 1: both forms with the next
+    k-tile's DMA spread among the MFMAs (sweep_il)."""
     rs = np.random.RandomState(78)
     d, nq, n = 2048, 1280, 70_003
     g = rs.standard_normal((n, d)).astype(np.float32)
@@ -366,7 +368,10 @@ def test_prefilter_sweep_mf16_bit_identical(cuda):
     bound = ops.prefilter_gallery_bound(gd, gbf)
     out = {}
     for v in (0, 1):
-        with ops.tuning(cuda.index, sweep_mf16=v):
+        with ops.tuning(cuda.index, sweep_mf16=v, sweep_il=il):
             out[v] = ops.cosine_topk_prefilter(qd, gd, gbf, bound, 100)
-    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][0].view(torch.int32), out[1][0].view(torch.int32))
+    with ops.tuning(cuda.index, sweep_mf16=0, sweep_il=0):
+        ref = ops.cosine_topk_prefilter(qd, gd, gbf, bound, 100)
+    for v in (0, 1):
+        assert torch.equal(out[v][1], ref[1]) and torch.equal(out[v][0].view(torch.int32), ref[0].view(torch.int32)), v
     assert int(out[1][1][0, 0]) == 5 and int(out[1][1][nq - 1, 0]) == n - 1

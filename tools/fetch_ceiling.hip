@@ -69,7 +69,12 @@ __device__ __forceinline__ bool tile_of(int bid, int nwg, int Mt, int T, int& tm
   }
 }
 
-template <int G, int Q, int MF, int VG, int ORD, int PF = 0, int M16 = 0>
+// IL > 0 (LDS-DMA only): instead of one burst of the next k-tile's 9 DMA
+// instructions per wave at the top of the k-tile, chunk c goes out just
+// before MFMA number (c * IL) / 9 of the k-tile's sequence (40 MFMAs of
+// 32x32x16, 80 of 16x16x32), pinned there by sched_barriers: does spreading
+// the issue over the MFMAs relieve the vector-memory issue queue?
+template <int G, int Q, int MF, int VG, int ORD, int PF = 0, int M16 = 0, int IL = 0>
 __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__ gal, const uint16_t* __restrict__ qry,
                                                     int Mt, int T, float* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[2 * BUFB + 256];
@@ -83,6 +88,28 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
   auto src_of = [&](int i) { return i < 4 ? gsrc + (long long)i * PASS * K : qsrc + (long long)(i - 4) * PASS * K; };
   auto on = [&](int i) { return i < 4 ? G != 0 : Q != 0; };
   f32x4 rv[9];
+  static_assert(!IL || (!VG && MF), "IL: LDS-DMA with MFMAs");
+  auto issue_one = [&](int kt, int buf, int i) {
+    if (!on(i)) return;
+    const int row = crow + i * PASS;
+    __builtin_amdgcn_global_load_lds((const void*)(src_of(i) + kt * EPR + swz(row, slot) * 8),
+                                     (__attribute__((address_space(3))) void*)(lds + buf * BUFB +
+                                                                               (i * PASS + wv * 8) * 128),
+                                     16, 0, 0);
+  };
+  // the chunks due before MFMA number idx of the k-tile (IL > 0)
+  auto issue_at = [&](int kt, int buf, int idx) {
+    if constexpr (IL > 0) {
+      if (kt >= NK) return;
+#pragma unroll
+      for (int c = 0; c < 9; ++c)
+        if ((c * IL) / 9 == idx) {
+          __builtin_amdgcn_sched_barrier(0);
+          issue_one(kt, buf, c);
+          __builtin_amdgcn_sched_barrier(0);
+        }
+    }
+  };
   auto issue = [&](int kt, int buf) {
 #pragma unroll
     for (int i = 0; i < 9; ++i) {
@@ -135,7 +162,7 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
   prefetch(1);
   for (int kt = 0; kt < NK; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < NK) issue(kt + 1, cur ^ 1);
+    if (!IL && kt + 1 < NK) issue(kt + 1, cur ^ 1);
     prefetch(kt + 2);
     if constexpr (MF && M16) {
       // v_mfma_f32_16x16x32_bf16: per 32-deep k-step 4 A and 10 B fragments
@@ -160,7 +187,10 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
 #pragma unroll
         for (int j = 0; j < 10; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc16[i][j], 0, 0, 0);
+          for (int i = 0; i < 4; ++i) {
+            issue_at(kt + 1, cur ^ 1, st * 40 + j * 4 + i);
+            acc16[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc16[i][j], 0, 0, 0);
+          }
       }
     } else if constexpr (MF) {
       const unsigned char* la = lds + cur * BUFB;
@@ -181,7 +211,10 @@ __global__ __launch_bounds__(NT, 1) void sweep_fill(const uint16_t* __restrict__
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 5; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          for (int j = 0; j < 5; ++j) {
+            issue_at(kt + 1, cur ^ 1, st * 10 + i * 5 + j);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          }
       }
     }
     if constexpr (VG) {
@@ -287,14 +320,14 @@ __global__ void fill_rand(uint16_t* p, long long n, unsigned seed) {
   }
 }
 
-template <int G, int Q, int MF, int VG, int ORD, int PF = 0, int M16 = 0>
+template <int G, int Q, int MF, int VG, int ORD, int PF = 0, int M16 = 0, int IL = 0>
 static void run(const char* name, const uint16_t* gal, const uint16_t* qry, int Mt, int T, float* out, int reps) {
   int nblk = Mt * T;
   if (ORD) {
     const int NR = 8 / ORD, R = (Mt + NR - 1) / NR;
     nblk = 8 * R * (T / ORD);
   }
-  auto k = sweep_fill<G, Q, MF, VG, ORD, PF, M16>;
+  auto k = sweep_fill<G, Q, MF, VG, ORD, PF, M16, IL>;
   hipLaunchKernelGGL(k, dim3(nblk), dim3(NT), 0, 0, gal, qry, Mt, T, out);
   CK(hipDeviceSynchronize());
   hipEvent_t a, b;
@@ -355,6 +388,16 @@ int main(int argc, char** argv) {
   run<0, 0, 1, 0, 0, 0, 1>("16x16x32: MFMA only (stale LDS operands)", gal, qry, Mt, T, out, reps);
   run<1, 1, 1, 0, 0, 0, 1>("16x16x32: DMA + MFMA, order 0", gal, qry, Mt, T, out, reps);
   run<1, 1, 1, 0, 2, 0, 1>("16x16x32: DMA + MFMA, order 2", gal, qry, Mt, T, out, reps);
+  if (argc > 2) {  // issue spread only (the r04e A/B)
+    run<1, 1, 1, 0, 0>("DMA  + MFMA, burst issue (as above)", gal, qry, Mt, T, out, reps);
+    run<1, 1, 1, 0, 0, 0, 0, 9>("DMA  + MFMA, issue over MFMAs 0-8", gal, qry, Mt, T, out, reps);
+    run<1, 1, 1, 0, 0, 0, 0, 18>("DMA  + MFMA, issue over MFMAs 0-17", gal, qry, Mt, T, out, reps);
+    run<1, 1, 1, 0, 0, 0, 0, 36>("DMA  + MFMA, issue over MFMAs 0-35", gal, qry, Mt, T, out, reps);
+    run<1, 1, 1, 0, 0, 0, 1>("16x16x32: DMA + MFMA, burst issue", gal, qry, Mt, T, out, reps);
+    run<1, 1, 1, 0, 0, 0, 1, 18>("16x16x32: DMA + MFMA, issue over MFMAs 0-17", gal, qry, Mt, T, out, reps);
+    run<1, 1, 1, 0, 0, 0, 1, 36>("16x16x32: DMA + MFMA, issue over MFMAs 0-35", gal, qry, Mt, T, out, reps);
+    run<1, 1, 1, 0, 0, 0, 1, 72>("16x16x32: DMA + MFMA, issue over MFMAs 0-71", gal, qry, Mt, T, out, reps);
+  }
   CK(hipFree(gal));
   CK(hipFree(qry));
   CK(hipFree(out));

@@ -1,7 +1,7 @@
 """Every f16x2 tile config forced on every R101 conv shape at B images
 (rr_set_tuning s3_cfg; 0 = the library's pick), interleaved rounds in one
 process: median ms and TF/s per (shape, config), the fastest marked.
-usage: h2_cfg_sweep.py [B] [cfgs, default 0,3,4,7,8]"""
+usage: h2_cfg_sweep.py [B] [cfgs, default 0,3,4,7,8; a trailing "i" adds conv_il=1, e.g. 0,0i]"""
 import os
 import statistics
 import sys
@@ -12,7 +12,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from research_image_retrieval_amd import ops  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 1280
-CFGS = [int(c) for c in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 3, 4, 7, 8]
+CFGS = sys.argv[2].split(",") if len(sys.argv) > 2 else ["0", "3", "4", "7", "8"]
+
+
+def tune(c):
+    """config spec -> rr_set_tuning keys: "12" = s3_cfg 12, "12i" = with conv_il 1"""
+    return {"s3_cfg": int(c.rstrip("i")), "conv_il": 1 if c.endswith("i") else 0}
 dev = torch.device("cuda:0")
 SHAPES = [  # (h, cin, cout, k, stride, residual, count in R101)
     (56, 64, 64, 3, 1, 0, 3), (56, 64, 256, 1, 1, 1, 2), (56, 256, 64, 1, 1, 0, 2), (56, 64, 64, 1, 1, 0, 1),
@@ -51,7 +56,7 @@ for h, cin, cout, k, s, res, cnt in SHAPES:
     times = {c: [] for c in CFGS}
     for _ in range(3):
         for c in CFGS:
-            with ops.tuning(0, s3_cfg=c):
+            with ops.tuning(0, **tune(c)):
                 times[c].append(timed(lambda: ops.conv2d_h2(x, rec[0], wc, bias, s, p, r, True, rec[1])))
     fl = 2.0 * B * oh * oh * cout * k * k * cin
     med = {c: statistics.median(v) for c, v in times.items()}

@@ -4,7 +4,8 @@ the block -> tile orders 0 / 2 / 4 / 8) on the C3 shape
 (Q queries x 1.6 M x 2048, top-100): the sweep launch's HIP-event time, its
 fraction of the bf16 dense peak, and the whole ranker's results compared bit
 for bit between configs.
-usage: [PF_KEY=lp_cfg|sweep_order] PF_CFGS="0 6" PF_Q=1280 python tools/prefilter_ab.py"""
+usage: [PF_KEY=lp_cfg|sweep_order|...] [PF_EXTRA="key=value ..."] PF_CFGS="0 6" PF_Q=1280
+       python tools/prefilter_ab.py"""
 import json
 import os
 import statistics
@@ -20,6 +21,8 @@ dev = torch.device("cuda:0")
 Q = int(os.environ.get("PF_Q", "1280"))
 cfgs = [int(c) for c in os.environ.get("PF_CFGS", "0 6").split()]
 KEY = os.environ.get("PF_KEY", "lp_cfg")
+# fixed extra tuning for every config, e.g. PF_EXTRA="sweep_mf16=1"
+EXTRA = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in os.environ.get("PF_EXTRA", "").split()}
 N, D, K = int(os.environ.get("PF_N", "1600000")), 2048, 100
 g = torch.Generator(device=dev).manual_seed(0)
 gal = F.normalize(torch.randn(N, D, device=dev, generator=g), dim=1)
@@ -34,7 +37,7 @@ CLS = (_lib.TIME_COSINE, _lib.TIME_COSINE_SEED, _lib.TIME_SELECT, _lib.TIME_ELEM
 
 
 def run(cfg, iters=3):
-    with ops.tuning(0, **{KEY: cfg}):
+    with ops.tuning(0, **{KEY: cfg}, **EXTRA):
         ops.cosine_topk_prefilter(q, gal, gbf, bound, K, workspace=ws)
         torch.cuda.synchronize()
         timer.enable(True)
