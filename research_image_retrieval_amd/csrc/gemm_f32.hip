@@ -937,14 +937,16 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
     const int ord = tu.sweep_order < 0 ? 0 : tu.sweep_order;
     const int bn = (cfg == 4 && DT == DT_BF16) ? 320 : (cfg >= 3 ? 256 : (cfg == 2 ? 64 : 128));
     const long long tn = ((long long)g.N + bn - 1) / bn;
-    // the 256x320 bf16 tile's defaults: v_mfma_f32_16x16x32_bf16 with the
-    // next k-tile's DMA spread among the MFMAs (sweep_mf16, sweep_il: measured
-    // on the C3 sweep, 1280 near-parallel queries x 1.6 M x 2048, 7.99 ->
-    // 7.46 ms, bit-identical rankings; profiles/r04f_sweep_il_ab.txt)
+    // the 256x320 bf16 tile's default: v_mfma_f32_32x32x16_bf16 with the next
+    // k-tile's DMA spread among the MFMAs (sweep_il).  On the C3 bench's own
+    // descriptors (tools/e2e_ab.py, profiles/r04j_e2e_ab.txt): 7.15 -> 6.81
+    // ms; the 16x16x32 form is 7.71 ms there (7.08 with the spread), though
+    // it won on synthetic near-parallel queries (r04f_sweep_il_ab.txt).
+    // Bit-identical rankings in every form.
     GemmArgs g2 = g;
     if (ord > 0 && tn % ord == 0) g2.tile_order = ord;
     g2.l2_prefetch = tu.sweep_pf > 0;
-    g2.mf16_sweep = tu.sweep_mf16 != 0;
+    g2.mf16_sweep = tu.sweep_mf16 > 0;
     g2.issue_spread = tu.sweep_il != 0;
     return launch_lp_cfg<EM, DT>(g2, s, cfg);
   }

@@ -2229,11 +2229,12 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
     const int f = h->tune.s3_cfg;
     const int n_cu = device_cu_count(h);
     if (sp == 2) {
-      // the 256x256 tile's loads spread among its MFMAs by default: every
-      // R101 layer it serves 1-3 % faster at 1280 images (256->1024 0.681 ->
-      // 0.668 ms, 1024->512 0.770 -> 0.751; profiles/r04g_h2_cfg_il.txt)
+      // conv_il (opt-in): every R101 layer the 256x256 tile serves ran 1-3 %
+      // faster alone at 1280 images (256->1024 0.681 -> 0.668 ms; profiles/
+      // r04g_h2_cfg_il.txt, r04h_h2_cfg_il.txt), but the bench's whole embed
+      // ran 0.5 % slower with it (71.77 -> 72.11 ms, r04j_e2e_ab.txt)
       GemmArgs g2 = g;
-      g2.issue_spread = h->tune.conv_il != 0;
+      g2.issue_spread = h->tune.conv_il > 0;
       e = amode == A_DENSE ? launch_h2_am<A_DENSE>(g2, s, f, n_cu, st)
           : amode == A_CONV ? launch_h2_am<A_CONV>(g2, s, f, n_cu, st)
                             : launch_h2_am<A_CONV_C4>(g2, s, f, n_cu, st);

@@ -21,9 +21,9 @@ struct rr_handle_s {
     int s3_stagger = -1;  // split-bf16 core round stagger in ~1 us sleeps (-1: the library's pick)
     int sweep_order = -1;  // bf16 / fp8 filter sweeps: block -> tile order (tile_coords); -1: the library's pick
     int sweep_pf = -1;     // bf16 256x320 filter sweep: L2 prefetch of the gallery two k-tiles ahead; -1: the pick
-    int sweep_mf16 = -1;   // bf16 256x320 filter sweep on v_mfma_f32_16x16x32_bf16 (1) or 32x32x16 (0); -1: the pick (1)
+    int sweep_mf16 = -1;   // bf16 256x320 filter sweep on v_mfma_f32_16x16x32_bf16 (1) or 32x32x16 (0); -1: the pick (0)
     int sweep_il = -1;     // bf16 256x320 filter sweep: next k-tile's DMA spread among the MFMAs (1) or one burst (0); -1: the pick (1)
-    int conv_il = -1;      // f16x2 256x256 conv tile (s3_cfg 12): next k-tiles' loads spread among the MFMAs (1) or one burst (0); -1: the pick (1)
+    int conv_il = -1;      // f16x2 256x256 conv tile (s3_cfg 12): next k-tiles' loads spread among the MFMAs (1) or one burst (0); -1: the pick (0)
   } tune;
   int n_cu = 0;  // compute units of the handle's device (device_cu_count)
   // timing (see rr_timing_enable)
