@@ -1923,7 +1923,8 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
     // selects the 32x32x16 form everywhere, 14 the 16x16x32 form everywhere.
     if (forced == 13 || forced == 14 || (forced == 0 && ((g.N % 256) == 0 || g.N == 64))) {
       if (const int hr = h2_halo_rows(g))
-        return launch_h2_halo(g, s, hr, forced == 14 ? 1 : forced == 13 ? 0 : (hr == 288 ? 1 : 0));
+        return launch_h2_halo(g, s, hr,
+                              forced == 14 ? 1 : forced == 13 ? 0 : g.halo_mf >= 0 ? g.halo_mf : (hr == 288 ? 1 : 0));
     }
   }
   if (forced == 13 || forced == 14) forced = 0;
@@ -2235,6 +2236,7 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
       // ran 0.5 % slower with it (71.77 -> 72.11 ms, r04j_e2e_ab.txt)
       GemmArgs g2 = g;
       g2.issue_spread = h->tune.conv_il > 0;
+      g2.halo_mf = h->tune.halo_mf;
       e = amode == A_DENSE ? launch_h2_am<A_DENSE>(g2, s, f, n_cu, st)
           : amode == A_CONV ? launch_h2_am<A_CONV>(g2, s, f, n_cu, st)
                             : launch_h2_am<A_CONV_C4>(g2, s, f, n_cu, st);
