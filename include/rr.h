@@ -111,6 +111,9 @@ int rr_get_device(rr_handle_t h, int* device);
  *   RR_TUNE_HALO_MF:  the f16x2 halo-staged 3x3 tiles on v_mfma_f32_16x16x32_f16 (1) or
  *                     v_mfma_f32_32x32x16_f16 (0); -1 = the library's pick (RR_TUNE_S3_CFG
  *                     13 / 14 override it)
+ *   RR_TUNE_LP_IL:    the bf16 256x256 stored-C / score tile (lp_cfg 3, the ViT linears):
+ *                     1 = the next k-tile's LDS-DMA issued chunk by chunk among the MFMAs
+ *                     after the k-tile barrier, 0 = one burst; -1 = the library's pick (0)
  * Any other key or value: RR_EINVAL. */
 #define RR_TUNE_GEMM_CFG 1
 #define RR_TUNE_GEMM_BK 2
@@ -123,6 +126,7 @@ int rr_get_device(rr_handle_t h, int* device);
 #define RR_TUNE_SWEEP_IL 9
 #define RR_TUNE_CONV_IL 10
 #define RR_TUNE_HALO_MF 11
+#define RR_TUNE_LP_IL 12
 int rr_set_tuning(rr_handle_t h, int key, int value);
 
 /* ---- search (ranker) ----------------------------------------------------

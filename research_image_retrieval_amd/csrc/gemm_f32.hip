@@ -294,10 +294,13 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   // IL: chunk c (A rows, then B rows) of glds_tile(kt, buf), due before MFMA
   // number idx; past the last k-tile it re-fetches the last one (an L2 hit)
   // into the drained buffer, so every iteration issues the same DMAs
-  static_assert(!IL || (GL && DT == DT_BF16 && MF16 != 1 && !PF && EMODE == E_FILTER), "IL: LDS-DMA bf16 filter sweeps");
+  static_assert(!IL || (GL && DT == DT_BF16 && !PF && (MF16 == 1 || EMODE == E_FILTER)),
+                "IL: LDS-DMA bf16 filter sweeps, or the PIPE16 tiles");
   constexpr int NCH = A_CH + B_CH;
-  constexpr int IL_SPAN = IL ? (MF16 == 2 ? 36 : 18) : 0;
-  static_assert(IL_SPAN <= (MF16 == 2 ? 4 * FM * FN * (BK / 16) : FM * FN * (BK / 8)),
+  // (PIPE16: the chunks go among the last k-step's MFMAs, one every
+  // 4 FM FN / NCH, right after the barrier that frees their buffer)
+  constexpr int IL_SPAN = IL ? (MF16 == 2 ? 36 : MF16 == 1 ? 4 * FM * FN : 18) : 0;
+  static_assert(IL_SPAN <= (MF16 ? 4 * FM * FN * (BK / 16) : FM * FN * (BK / 8)),
                 "IL: every chunk before an MFMA of the k-tile");
   auto glds_due = [&](int kt, int buf, int idx) {
     if constexpr (IL) {
@@ -425,6 +428,24 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
           };
           __builtin_amdgcn_sched_barrier(0);  // the previous step's MFMAs stay above the wait
           settle();
+          if constexpr (IL) {
+            // tile kt+2's DMA chunk by chunk among this step's MFMAs, into the
+            // buffer the barrier just freed.  Past the last tile it fetches the
+            // last tile again (an L2 hit); in the last iteration (no barrier:
+            // other waves may still read buffer cur) into buffer cur ^ 1, free
+            // since the previous iteration's barrier.  The epilogue's
+            // __syncthreads retires it.
+            if (kt + 1 < nk) {
+              asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+              __builtin_amdgcn_s_barrier();
+              rd(cur ^ 1, 0, af[0], bf[0]);
+            }
+            // issued as one burst in the source; the scheduler spreads it
+            // (interleave_il's VMEM groups: one DMA per 4 FM FN / NCH MFMAs)
+            glds_tile(min(kt + 2, nk - 1), kt + 1 < nk ? cur : cur ^ 1);
+            mfmas(st);
+            interleave_il<4 * FM * FN, IL_SPAN, NCH>(0, 0);
+          } else {
           if (kt + 1 < nk) {
             // every wave is done with buffer cur; tile kt+1's DMA has landed
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -433,10 +454,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
             rd(cur ^ 1, 0, af[0], bf[0]);
           }
           mfmas(st);
+          }
         }
       }
     }
     __builtin_amdgcn_s_setprio(0);
+    if constexpr (IL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last spread DMA
     __syncthreads();  // every wave's last reads done: the epilogue reuses the LDS
   } else {
   // PF: waves 0 .. BM/64 - 1 each touch 64 A rows (one per lane)
@@ -807,18 +830,19 @@ static hipError_t launch_t1(const GemmArgs& g, hipStream_t s) {
 // bf16 stored-C GEMMs (the ViT linears) with their epilogues compiled in:
 // QKV (bias -> bf16), out-proj / fc2 (bias + residual, fp32), fc1 (bias +
 // QuickGELU -> bf16); everything else reads its flags at run time.
-template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0>
+template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0, int IL = 0>
 static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   if constexpr (EM == E_STORE && DT == DT_BF16) {
     switch (ep_flags(g)) {
-      case EP_BIAS | EP_BF16: return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_BF16>(g, s);
-      case EP_BIAS | EP_RES: return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_RES>(g, s);
+      case EP_BIAS | EP_BF16:
+        return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_BF16, 0, IL>(g, s);
+      case EP_BIAS | EP_RES: return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_RES, 0, IL>(g, s);
       case EP_BIAS | EP_GELU | EP_BF16:
-        return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_GELU | EP_BF16>(g, s);
+        return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_GELU | EP_BF16, 0, IL>(g, s);
       default: break;
     }
   }
-  return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16>(g, s);
+  return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, -1, 0, IL>(g, s);
 }
 
 // k-tile depth.  Measured on MI355X (same device, interleaved A/B): BK = 16
@@ -950,6 +974,11 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
     g2.issue_spread = tu.sweep_il != 0;
     return launch_lp_cfg<EM, DT>(g2, s, cfg);
   }
+  if (tu.lp_il > 0) {  // the 256x256 bf16 tile of the stored-C / score GEMMs (ViT linears)
+    GemmArgs g2 = g;
+    g2.issue_spread = 1;
+    return launch_lp_cfg<EM, DT>(g2, s, cfg);
+  }
   return launch_lp_cfg<EM, DT>(g, s, cfg);
 }
 
@@ -964,7 +993,12 @@ static hipError_t launch_lp_cfg(const GemmArgs& g, hipStream_t s, int cfg) {
   }
   switch (cfg) {
     case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF>(g, s);
-    case 3: return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);
+    case 3:
+      // (bf16: the next k-tile's DMA spread among the MFMAs, lp_il)
+      if constexpr (DT == DT_BF16) {
+        if (g.issue_spread) return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF, 1>(g, s);
+      }
+      return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);
     case 4:  // bf16 sweeps only (fp8: the 256x256 tile; its 256x320 form spills the dequantisation)
       if constexpr (EM == E_FILTER && DT == DT_BF16) {
         if (g.l2_prefetch) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0, -1, 1>(g, s);

@@ -4,7 +4,7 @@ one process: the embed's wall time per config and the ranker's filter-sweep
 HIP-event time per config, rounds interleaved, medians.  Rankings are checked
 bit for bit between the ranker configs.
 usage: E2E_EMBED="conv_il=0 conv_il=1" E2E_RANK="sweep_il=0,sweep_mf16=0 sweep_il=1,sweep_mf16=1"
-       python tools/e2e_ab.py [B] [rounds]"""
+       [E2E_WORKLOAD=c4: the ViT-B/16 bf16 embed instead (E2E_RANK unsupported)] python tools/e2e_ab.py [B] [rounds]"""
 import os
 import statistics
 import sys
@@ -25,7 +25,13 @@ RNK = os.environ.get("E2E_RANK", "").split()
 dev = torch.device("cuda:0")
 torch.cuda.set_device(dev)
 N = 1_600_000
-net = bench.build_extractor("resnet101", dev)
+if os.environ.get("E2E_WORKLOAD") == "c4":  # bench.py --workload c4's ViT-B/16 bf16 extractor
+    from research_image_retrieval_amd import weights as W  # noqa: E402
+    from research_image_retrieval_amd.networks import VisionTransformer  # noqa: E402
+    net = VisionTransformer(224, 16, 768, 12, 12, 512, dtype="bf16", state_dict=W.synthetic_vit_state_dict(out_dim=512, seed=0),
+                            device=dev)
+else:
+    net = bench.build_extractor("resnet101", dev)
 rs = np.random.RandomState(1234)  # bench.py's rank-0 images
 imgs = torch.from_numpy(rs.randint(0, 256, size=(B, 224, 224, 3), dtype=np.uint8)).to(dev)
 
