@@ -101,9 +101,10 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     flight across the barrier), 0 = off, -1 = the library's pick
  *   RR_TUNE_SWEEP_MF16: the 256x320 bf16 filter sweep on v_mfma_f32_16x16x32_bf16 (1)
  *                     or v_mfma_f32_32x32x16_bf16 (0); -1 = the library's pick (0)
- *   RR_TUNE_SWEEP_IL: the 256x320 bf16 filter sweep: 1 = the next k-tile's LDS-DMA
+ *   RR_TUNE_SWEEP_IL: the bf16 / fp8 filter sweeps: 1 = the next k-tile's LDS-DMA
  *                     issued chunk by chunk among the k-tile's first MFMAs, 0 = one
- *                     burst at the top of the k-tile; -1 = the library's pick (1)
+ *                     burst at the top of the k-tile; -1 = the library's pick (1 for the
+ *                     256x320 bf16 sweep, 0 for the others)
  *                     (the L2 prefetch of RR_TUNE_SWEEP_PF = 1 runs without it)
  *   RR_TUNE_CONV_IL:  the f16x2 256x256 conv tile (RR_TUNE_S3_CFG 12): 1 = the next
  *                     k-tiles' B DMA and A loads issued one group at a time among the

@@ -69,7 +69,7 @@ __device__ __forceinline__ void interleave() {
 // MFMAs (IL sweeps): chunk c of NCH goes out before MFMA number (c * SPAN) /
 // NCH of the k-tile; base = the k-tile's MFMA number of this region's first
 // (base and nr constant once the caller's k-step loop is unrolled).
-template <int NM, int SPAN, int NCH>
+template <int NM, int SPAN, int NCH, int DSPER = 1>
 __device__ __forceinline__ void interleave_il(int base, int nr) {
 #pragma unroll
   for (int x = 0; x < NM; ++x) {
@@ -77,7 +77,7 @@ __device__ __forceinline__ void interleave_il(int base, int nr) {
     for (int c = 0; c < NCH; ++c)
       if ((c * SPAN) / NCH == base + x) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // 1 VMEM (the DMA)
     __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                                      // 1 MFMA
-    if (x < nr) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);                          // 1 DS read
+    if (x < nr) __builtin_amdgcn_sched_group_barrier(0x100, DSPER, 0);                      // DSPER DS reads
   }
 }
 
@@ -294,13 +294,14 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   // IL: chunk c (A rows, then B rows) of glds_tile(kt, buf), due before MFMA
   // number idx; past the last k-tile it re-fetches the last one (an L2 hit)
   // into the drained buffer, so every iteration issues the same DMAs
-  static_assert(!IL || (GL && DT == DT_BF16 && !PF && (MF16 == 1 || EMODE == E_FILTER)),
-                "IL: LDS-DMA bf16 filter sweeps, or the PIPE16 tiles");
+  static_assert(!IL || (GL && DT != DT_F32 && !PF && (MF16 == 1 || EMODE == E_FILTER)),
+                "IL: LDS-DMA bf16 / fp8 filter sweeps, or the PIPE16 tiles");
   constexpr int NCH = A_CH + B_CH;
   // (PIPE16: the chunks go among the last k-step's MFMAs, one every
   // 4 FM FN / NCH, right after the barrier that frees their buffer)
-  constexpr int IL_SPAN = IL ? (MF16 == 2 ? 36 : MF16 == 1 ? 4 * FM * FN : 18) : 0;
-  static_assert(IL_SPAN <= (MF16 ? 4 * FM * FN * (BK / 16) : FM * FN * (BK / 8)),
+  // (fp8: the first k-step's FM FN MFMAs, one chunk each)
+  constexpr int IL_SPAN = IL ? (MF16 == 2 ? 36 : MF16 == 1 ? 4 * FM * FN : DT == DT_FP8 ? FM * FN : 18) : 0;
+  static_assert(IL_SPAN <= (MF16 ? 4 * FM * FN * (BK / 16) : DT == DT_FP8 ? FM * FN * (BK / 16) : FM * FN * (BK / 8)),
                 "IL: every chunk before an MFMA of the k-tile");
   auto glds_due = [&](int kt, int buf, int idx) {
     if constexpr (IL) {
@@ -654,6 +655,10 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int st = 0; st < S; ++st) {
+        // IL: the next k-tile's DMA as one burst in the source, spread by the
+        // scheduler among the first k-step's MFMAs (past the last k-tile: the
+        // last one again, into the drained buffer)
+        if (IL && st == 0) glds_tile(min(kt + 1, nk - 1), cur ^ 1);
         if (st + 1 < S) rd(st + 1, af[(st + 1) & 1], bf[(st + 1) & 1]);
 #pragma unroll
         for (int i = 0; i < FM; ++i)
@@ -661,7 +666,12 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
           for (int j = 0; j < FN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_scale_f32_32x32x64_f8f6f4(af[st & 1][i], bf[st & 1][j], acc[i][j],
                                                                          0, 0, 0, 127, 0, 127);
-        if (st + 1 < S) interleave2<FM + FN, FM * FN>();
+        if constexpr (IL) {
+          if (st == 0) interleave_il<FM * FN, IL_SPAN, NCH, 2>(0, st + 1 < S ? FM + FN : 0);
+          else if (st + 1 < S) interleave2<FM + FN, FM * FN>();
+        } else if (st + 1 < S) {
+          interleave2<FM + FN, FM * FN>();
+        }
       }
       __builtin_amdgcn_s_setprio(0);
     }
@@ -971,7 +981,9 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
     if (ord > 0 && tn % ord == 0) g2.tile_order = ord;
     g2.l2_prefetch = tu.sweep_pf > 0;
     g2.mf16_sweep = tu.sweep_mf16 > 0;
-    g2.issue_spread = tu.sweep_il != 0;
+    // (sweep_il = 1 spreads every filter sweep's DMA: the fp8 and the 256x256
+    // bf16 ones too; the default only the 256x320 bf16 one)
+    g2.issue_spread = tu.sweep_il > 0 || (tu.sweep_il < 0 && cfg == 4 && DT == DT_BF16);
     return launch_lp_cfg<EM, DT>(g2, s, cfg);
   }
   if (tu.lp_il > 0) {  // the 256x256 bf16 tile of the stored-C / score GEMMs (ViT linears)
@@ -994,8 +1006,9 @@ static hipError_t launch_lp_cfg(const GemmArgs& g, hipStream_t s, int cfg) {
   switch (cfg) {
     case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF>(g, s);
     case 3:
-      // (bf16: the next k-tile's DMA spread among the MFMAs, lp_il)
-      if constexpr (DT == DT_BF16) {
+      // (the next k-tile's DMA spread among the MFMAs: lp_il for the bf16
+      // stored-C tile, sweep_il for the fp8 filter sweeps)
+      if constexpr (DT == DT_BF16 || (DT == DT_FP8 && EM == E_FILTER)) {
         if (g.issue_spread) return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF, 1>(g, s);
       }
       return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);

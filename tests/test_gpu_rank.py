@@ -375,3 +375,25 @@ def test_prefilter_sweep_mf16_bit_identical(cuda, il):
     for v in (0, 1):
         assert torch.equal(out[v][1], ref[1]) and torch.equal(out[v][0].view(torch.int32), ref[0].view(torch.int32)), v
     assert int(out[1][1][0, 0]) == 5 and int(out[1][1][nq - 1, 0]) == n - 1
+
+
+@pytest.mark.parametrize("dt,d", [("fp8", 2048), ("bf16", 512)])
+def test_lp_sweep_issue_spread_bit_identical(cuda, dt, d):
+    """sweep_il = 1 on the 256x256 filter sweeps (the C5 fp8 and C4 bf16
+    rankers): the next k-tile's DMA spread among the MFMAs, the same scores
+    and indices bit for bit as one burst."""
+    rs = np.random.RandomState(91)
+    nq, n = 1280, 60_007
+    g = rs.standard_normal((n, d)).astype(np.float32)
+    q = rs.standard_normal((nq, d)).astype(np.float32)
+    g[7], g[n - 1] = q[0], q[nq - 1]
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    ql, qs = ops.quantize_rows(torch.from_numpy(q).to(cuda), dt)
+    gl, gs = ops.quantize_rows(torch.from_numpy(g).to(cuda), dt)
+    out = {}
+    for il in (0, 1):
+        with ops.tuning(cuda.index, sweep_il=il):
+            out[il] = ops.cosine_topk_lp(ql, qs, gl, gs, 100, dt)
+    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][0].view(torch.int32), out[1][0].view(torch.int32))
+    assert int(out[1][1][0, 0]) == 7 and int(out[1][1][nq - 1, 0]) == n - 1
