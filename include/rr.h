@@ -104,7 +104,7 @@ int rr_get_device(rr_handle_t h, int* device);
  *   RR_TUNE_SWEEP_IL: the bf16 / fp8 filter sweeps: 1 = the next k-tile's LDS-DMA
  *                     issued chunk by chunk among the k-tile's first MFMAs, 0 = one
  *                     burst at the top of the k-tile; -1 = the library's pick (1 for the
- *                     256x320 bf16 sweep, 0 for the others)
+ *                     256x320 bf16 and the fp8 sweeps, 0 for the 256x256 bf16 one)
  *                     (the L2 prefetch of RR_TUNE_SWEEP_PF = 1 runs without it)
  *   RR_TUNE_CONV_IL:  the f16x2 256x256 conv tile (RR_TUNE_S3_CFG 12): 1 = the next
  *                     k-tiles' B DMA and A loads issued one group at a time among the

@@ -981,9 +981,10 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
     if (ord > 0 && tn % ord == 0) g2.tile_order = ord;
     g2.l2_prefetch = tu.sweep_pf > 0;
     g2.mf16_sweep = tu.sweep_mf16 > 0;
-    // (sweep_il = 1 spreads every filter sweep's DMA: the fp8 and the 256x256
-    // bf16 ones too; the default only the 256x320 bf16 one)
-    g2.issue_spread = tu.sweep_il > 0 || (tu.sweep_il < 0 && cfg == 4 && DT == DT_BF16);
+    // (sweep_il = 1 spreads every filter sweep's DMA, the 256x256 bf16 one
+    // too; the default: the 256x320 bf16 and the fp8 sweeps -- C5's fp8
+    // sweeps 7.70 -> 7.53 ms per step on the bench, profiles/r04k_c5_*.json)
+    g2.issue_spread = tu.sweep_il > 0 || (tu.sweep_il < 0 && ((cfg == 4 && DT == DT_BF16) || DT == DT_FP8));
     return launch_lp_cfg<EM, DT>(g2, s, cfg);
   }
   if (tu.lp_il > 0) {  // the 256x256 bf16 tile of the stored-C / score GEMMs (ViT linears)
