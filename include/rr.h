@@ -115,6 +115,8 @@ int rr_get_device(rr_handle_t h, int* device);
  *   RR_TUNE_LP_IL:    the bf16 256x256 stored-C / score tile (lp_cfg 3, the ViT linears):
  *                     1 = the next k-tile's LDS-DMA issued chunk by chunk among the MFMAs
  *                     after the k-tile barrier, 0 = one burst; -1 = the library's pick (0)
+ *   RR_TUNE_S3_CFG_RES: as RR_TUNE_S3_CFG, for the split-core GEMMs with a residual
+ *                     epilogue only (0 = RR_TUNE_S3_CFG's choice)
  * Any other key or value: RR_EINVAL. */
 #define RR_TUNE_GEMM_CFG 1
 #define RR_TUNE_GEMM_BK 2
@@ -128,6 +130,7 @@ int rr_get_device(rr_handle_t h, int* device);
 #define RR_TUNE_CONV_IL 10
 #define RR_TUNE_HALO_MF 11
 #define RR_TUNE_LP_IL 12
+#define RR_TUNE_S3_CFG_RES 13
 int rr_set_tuning(rr_handle_t h, int key, int value);
 
 /* ---- search (ranker) ----------------------------------------------------

@@ -23,7 +23,8 @@ AMAX_SLOTS = 64  # RR_AMAX_SLOTS
 TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM, TIME_COSINE_SEED, TIME_ATTN = 0, 1, 2, 3, 4, 5
 # rr_set_tuning keys
 TUNE_GEMM_CFG, TUNE_GEMM_BK, TUNE_LP_CFG, TUNE_S3_CFG, TUNE_S3_STAGGER, TUNE_SWEEP_ORDER, TUNE_SWEEP_PF, \
-    TUNE_SWEEP_MF16, TUNE_SWEEP_IL, TUNE_CONV_IL, TUNE_HALO_MF, TUNE_LP_IL = 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12
+    TUNE_SWEEP_MF16, TUNE_SWEEP_IL, TUNE_CONV_IL, TUNE_HALO_MF, TUNE_LP_IL, TUNE_S3_CFG_RES = \
+    1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13
 
 _lib = None
 _lock = threading.RLock()

@@ -2227,7 +2227,7 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
   hipError_t e;
   {
     TimedLaunch tl(h, timer_cls, s);
-    const int f = h->tune.s3_cfg;
+    const int f = (g.residual != nullptr && h->tune.s3_cfg_res > 0) ? h->tune.s3_cfg_res : h->tune.s3_cfg;
     const int n_cu = device_cu_count(h);
     if (sp == 2) {
       // conv_il (opt-in): every R101 layer the 256x256 tile serves ran 1-3 %

@@ -178,6 +178,10 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       if (!in({-1, 0, 1})) break;
       h->tune.lp_il = value;
       return RR_OK;
+    case RR_TUNE_S3_CFG_RES:
+      if (value < 0 || value > 14) break;
+      h->tune.s3_cfg_res = value;
+      return RR_OK;
     default:
       return set_error(h, RR_EINVAL, "rr_set_tuning: unknown key");
   }

@@ -26,6 +26,7 @@ struct rr_handle_s {
     int conv_il = -1;      // f16x2 256x256 conv tile (s3_cfg 12): next k-tiles' loads spread among the MFMAs (1) or one burst (0); -1: the pick (0)
     int halo_mf = -1;      // f16x2 halo 3x3 tiles on v_mfma_f32_16x16x32_f16 (1) or 32x32x16 (0); -1: the pick (the 256x256 tile 1, the others 0)
     int lp_il = -1;        // bf16 256x256 stored-C / score tile (the ViT linears): next k-tile's DMA spread among the MFMAs (1) or one burst (0); -1: the pick (0)
+    int s3_cfg_res = 0;    // split cores: forced tile config for the GEMMs with a residual epilogue only (0: s3_cfg's)
   } tune;
   int n_cu = 0;  // compute units of the handle's device (device_cu_count)
   // timing (see rr_timing_enable)

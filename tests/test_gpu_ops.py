@@ -126,9 +126,10 @@ def test_handle_device_and_tuning_validation(cuda):
     assert L.rr_set_tuning(h, _lib.TUNE_CONV_IL, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_HALO_MF, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_LP_IL, 2) == _lib.RR_EINVAL
+    assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG_RES, 15) == _lib.RR_EINVAL
     for key in (_lib.TUNE_GEMM_CFG, _lib.TUNE_GEMM_BK, _lib.TUNE_LP_CFG, _lib.TUNE_S3_CFG, _lib.TUNE_SWEEP_ORDER,
                 _lib.TUNE_SWEEP_PF, _lib.TUNE_SWEEP_MF16, _lib.TUNE_SWEEP_IL, _lib.TUNE_CONV_IL, _lib.TUNE_HALO_MF,
-                _lib.TUNE_LP_IL):
+                _lib.TUNE_LP_IL, _lib.TUNE_S3_CFG_RES):
         assert L.rr_set_tuning(h, key, 0) == 0
     for key in (_lib.TUNE_S3_STAGGER, _lib.TUNE_SWEEP_ORDER, _lib.TUNE_SWEEP_PF, _lib.TUNE_SWEEP_MF16,
                 _lib.TUNE_SWEEP_IL, _lib.TUNE_CONV_IL, _lib.TUNE_HALO_MF, _lib.TUNE_LP_IL):
