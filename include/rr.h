@@ -439,6 +439,34 @@ int rr_linear_bf16(rr_handle_t h, const void* x, int m, int k, const void* w,
                    const float* bias, int n, const float* residual, int act,
                    int out_bf16, void* y, void* stream);
 
+/* rr_linear_bf16 with the ViT LayerNorms (networks/model.py:157-163, the ln_1
+ * / ln_2 of :188-190) folded into the GEMMs, so no LayerNorm pass reads the
+ * fp32 residual stream.  Exactly one of stats_in / stats_out is set:
+ *  - stats_out (the out-proj / c_proj GEMMs: bias, residual, fp32 y, act 0,
+ *    n % 256 == 0): besides y, writes xb_out [m][n] = bf16(y) (RNE) and per row
+ *    and 256-column tile t the LayerNorm partials of y: stats_out [m][n/256][2]
+ *    = (mean_t, M2_t = sum (y - mean_t)^2 over the tile's 256 columns).
+ *  - stats_in (the in-proj / c_fc GEMMs: bias, bf16 y, k % 64 == 0): x holds
+ *    such bf16 rows (xb) with their partials [m][ceil(k/256)][2]; w =
+ *    bf16(W o gamma) (columns scaled by the LayerNorm weight), colsum[n] =
+ *    sum_k float(w[n][k]), bias = b + W beta:
+ *      y = act(rstd_m (x.w^T - mean_m colsum) + bias),
+ *    mean_m / rstd_m = 1 / sqrt(var + eps) from the partials (biased
+ *    variance, combined as Chan et al.).  Equal to LayerNorm -> bf16 ->
+ *    rr_linear_bf16 up to where bf16 rounding falls (bf16(y) instead of
+ *    bf16(LayerNorm(y))): tests/test_gpu_vit.py.                            */
+int rr_linear_bf16_ln(rr_handle_t h, const void* x, int m, int k, const void* w,
+                      const float* bias, int n, const float* residual, int act,
+                      int out_bf16, void* y, const float* stats_in,
+                      const float* colsum, float eps, float* stats_out,
+                      void* xb_out, void* stream);
+
+/* The producer side of rr_linear_bf16_ln for rows that no GEMM wrote (the
+ * first block's ln_1 input): xb [m][d] = bf16(x) and the partials
+ * stats [m][d/256][2] of fp32 x [m][d]; d % 256 == 0.                      */
+int rr_ln_partials_bf16(rr_handle_t h, const float* x, int m, int d, void* xb,
+                        float* stats, void* stream);
+
 /* ---- ViT-B/16 (networks/model.py:206-243) ------------------------------ */
 /* LayerNorm over the last dim (fp32, biased variance), rows x + i*ldx ->
  * dense y [m][d].  Replaces LayerNorm (:157-163): ln_pre, ln_1, ln_2, and

@@ -85,6 +85,8 @@ SIGNATURES = {
     "rr_attention_bf16_qkv16": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "rr_layernorm_ex": (_i, [_vp, _vp, _ll, _i, _i, _vp, _vp, _f, _i, _vp, _vp]),
     "rr_linear_bf16": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _vp]),
+    "rr_linear_bf16_ln": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _f, _vp, _vp, _vp]),
+    "rr_ln_partials_bf16": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp]),
     "rr_alpha_qe": (_i, [_vp, _vp, _i, _vp, _ll, _i, _vp, _vp, _i, _i, _f, _ll, _vp, _vp]),
     "rr_prefilter_gallery_bound": (_i, [_vp, _vp, _vp, _ll, _i, _vp, _vp]),
     "rr_cosine_topk_prefilter_workspace_size": (_sz, [_i, _ll, _i, _i]),

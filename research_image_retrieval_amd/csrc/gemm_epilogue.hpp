@@ -47,10 +47,34 @@ __device__ __forceinline__ float quick_gelu(float x) {
 // EP_SCALE / EP_AMAX (the f16x2 split core only, always compiled-in flag
 // sets): the accumulator times a per-column power-of-two scale before the
 // bias, and the max |C| of the stored values published to c_amax.
-enum { EP_BIAS = 1, EP_RES = 2, EP_RELU = 4, EP_GELU = 8, EP_BF16 = 16, EP_SCALE = 32, EP_AMAX = 64 };
+// EP_STATS / EP_LNFOLD (the bf16 ViT linears, 256-column tiles): the
+// LayerNorm partials + bf16 copy of C, and the LayerNorm folded into a
+// consumer's epilogue (GemmArgs stats_out / stats_in).
+enum { EP_BIAS = 1, EP_RES = 2, EP_RELU = 4, EP_GELU = 8, EP_BF16 = 16, EP_SCALE = 32, EP_AMAX = 64, EP_STATS = 128,
+       EP_LNFOLD = 256 };
 inline int ep_flags(const GemmArgs& g) {
   return (g.bias != nullptr ? EP_BIAS : 0) | (g.residual != nullptr ? EP_RES : 0) |
-         (g.relu == 1 ? EP_RELU : g.relu == 2 ? EP_GELU : 0) | (g.out_bf16 ? EP_BF16 : 0);
+         (g.relu == 1 ? EP_RELU : g.relu == 2 ? EP_GELU : 0) | (g.out_bf16 ? EP_BF16 : 0) |
+         (g.stats_out != nullptr ? EP_STATS : 0) | (g.stats_in != nullptr ? EP_LNFOLD : 0);
+}
+
+// Row m's LayerNorm mean and 1/sqrt(var + eps) from the producer's per-tile
+// partials (mean_t, M2_t over n_t = min(256, d - 256 t) columns), combined as
+// Chan et al.: mean = sum n_t mean_t / d, M2 = sum M2_t + n_t (mean_t - mean)^2
+// (biased variance M2 / d, as nn.LayerNorm).
+__device__ __forceinline__ void ln_row_stats(const float* st, long long m, int d, float eps, float& mean,
+                                             float& rstd) {
+  const int T = (d + 255) >> 8;
+  const float* p = st + m * T * 2;
+  float s = 0.f;
+  for (int t = 0; t < T; ++t) s += (float)min(256, d - 256 * t) * p[2 * t];
+  mean = s / (float)d;
+  float m2 = 0.f;
+  for (int t = 0; t < T; ++t) {
+    const float dm = p[2 * t] - mean;
+    m2 += p[2 * t + 1] + (float)min(256, d - 256 * t) * dm * dm;
+  }
+  rstd = 1.0f / sqrtf(m2 / (float)d + eps);
 }
 
 // ---- f16x2 split scales (gemm_s3.hip, SP 2) ----
@@ -103,10 +127,12 @@ __device__ __forceinline__ int h2_exp(float amax) {
 template <int FL, int P, int ITERS, int NT, int C4, int CS, int BI>
 __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const float* ct, const f32x4 (&bias_v)[BI],
                                            const f32x4 (&res)[ITERS], int tid, int mb, int n0, const f32x4 (&sc_v)[BI],
-                                           float& am) {
+                                           float& am, const f32x4& cs_v) {
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   constexpr int GR = ITERS < 4 ? ITERS : (P == 1 ? 8 : 4);
   constexpr bool FIXED = FL >= 0;
+  // EP_STATS: one row of the 256-column tile per wave and iteration
+  static_assert(!(FIXED && (FL & (EP_STATS | EP_LNFOLD))) || (BI == 1 && C4 == 64), "LayerNorm fold: 256-column tiles");
   const bool has_bias = FIXED ? (FL & EP_BIAS) != 0 : g.bias != nullptr;
   const bool has_res = FIXED ? (FL & EP_RES) != 0 : g.residual != nullptr;
   const int act = FIXED ? ((FL & EP_RELU) ? 1 : (FL & EP_GELU) ? 2 : 0) : g.relu;
@@ -144,6 +170,11 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
     if (m >= g.M || n >= g.N) continue;
     f32x4 v = cv[it];
     if constexpr (FIXED && (FL & EP_SCALE) != 0) v *= sc_v[BI == 1 ? 0 : it];
+    if constexpr (FIXED && (FL & EP_LNFOLD) != 0) {
+      float mean, rstd;
+      ln_row_stats(g.stats_in, m, g.stats_k, g.ln_eps, mean, rstd);
+      v = (v - mean * cs_v) * rstd;
+    }
     if (has_bias) v += bias_v[BI == 1 ? 0 : it];
     if (has_res) v += res[it];
     if (act == 1) {
@@ -162,6 +193,19 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
       *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(Cb) + o) = ob;
     } else {
       *reinterpret_cast<f32x4*>(Cb + o) = v;
+    }
+    if constexpr (FIXED && (FL & EP_STATS) != 0) {
+      // the row's bf16 copy and its tile's LayerNorm partials, two passes
+      // over the 256 values the wave holds (row m is wave-uniform; N % 256 == 0)
+      const bf16x4 ob = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+      *reinterpret_cast<bf16x4*>(g.c2 + o) = ob;
+      const float mt = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / 256.0f);
+      const f32x4 dv = v - mt;
+      const float m2 = wave_sum((dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]));
+      if ((threadIdx.x & 63) == 0) {
+        const int T = (g.N + 255) >> 8;
+        *reinterpret_cast<float2*>(g.stats_out + ((long long)m * T + (n0 >> 8)) * 2) = float2{mt, m2};
+      }
     }
   }
 }
@@ -208,8 +252,12 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
   constexpr int BI = (NT % C4 == 0) ? 1 : ITERS;
   constexpr bool SCALED = FL >= 0 && (FL & EP_SCALE) != 0;
   static_assert(!(FL >= 0 && (FL & (EP_SCALE | EP_AMAX))) || BI == 1, "scaled epilogues: one column per thread");
-  f32x4 bias_v[BI], sc_v[BI];
+  f32x4 bias_v[BI], sc_v[BI], cs_v = {0.f, 0.f, 0.f, 0.f};
   float am = 0.f;
+  if constexpr (FL >= 0 && (FL & EP_LNFOLD) != 0) {
+    const int n = n0 + (tid % C4) * 4;
+    if (n < g.N) cs_v = *reinterpret_cast<const f32x4*>(g.colsum + n);
+  }
   if (vec_ok) {
 #pragma unroll
     for (int it = 0; it < BI; ++it) {
@@ -277,7 +325,9 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) asm volatile("" : "+v"(res[it]));
       }
-      store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, CS, BI>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0, sc_v, am);
+      if constexpr (FL >= 0 && (FL & EP_LNFOLD) != 0) asm volatile("" : "+v"(cs_v));
+      store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, CS, BI>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0, sc_v, am,
+                                                                 cs_v);
     } else {
       for (int idx = tid; idx < SLAB * C4; idx += NT) {
         const int row = idx / C4, c4 = idx - row * C4;

@@ -851,6 +851,20 @@ static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
         return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_GELU | EP_BF16, 0, IL>(g, s);
       default: break;
     }
+    // the ViT LayerNorm fold (256-column tiles only; rr_linear_bf16_ln forces lp_cfg 3)
+    if constexpr (32 * FN * WN == 256 && MF16 == 1) {
+      switch (ep_flags(g)) {
+        case EP_BIAS | EP_RES | EP_STATS:
+          return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_RES | EP_STATS, 0, IL>(g, s);
+        case EP_BIAS | EP_BF16 | EP_LNFOLD:
+          return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_BF16 | EP_LNFOLD, 0, IL>(g, s);
+        case EP_BIAS | EP_GELU | EP_BF16 | EP_LNFOLD:
+          return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_GELU | EP_BF16 | EP_LNFOLD, 0,
+                           IL>(g, s);
+        default: break;
+      }
+    }
+    if (g.stats_out != nullptr || g.stats_in != nullptr) return hipErrorInvalidValue;
   }
   return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, -1, 0, IL>(g, s);
 }
@@ -964,6 +978,7 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
     if (tu.lp_cfg == 6 && sweep_v_eligible(g, DT)) return launch_sweep_v(g, s, DT);
   }
   int cfg = pick_lp(g, EM, DT == DT_BF16, tu);
+  if (g.stats_out != nullptr || g.stats_in != nullptr) cfg = 3;  // the LayerNorm fold: 256-column tiles
   if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles
   if constexpr (EM == E_FILTER) {
     // panel-grouped XCD order for the filter sweeps (tile_coords), when the

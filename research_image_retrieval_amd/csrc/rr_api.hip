@@ -365,6 +365,52 @@ int rr_linear_bf16(rr_handle_t h, const void* x, int m, int k, const void* w, co
   return launch_gemm(h, A_DENSE, E_STORE, g, (hipStream_t)stream, kTimeGemm, DT_BF16);
 }
 
+int rr_linear_bf16_ln(rr_handle_t h, const void* x, int m, int k, const void* w, const float* bias, int n,
+                      const float* residual, int act, int out_bf16, void* y, const float* stats_in,
+                      const float* colsum, float eps, float* stats_out, void* xb_out, void* stream) {
+  RR_ENTRY(h);
+  if (!x || !w || !y || m < 0 || k <= 0 || n <= 0 || (k & 7) || act < 0 || act > 2)
+    return set_error(h, RR_EINVAL, "rr_linear_bf16_ln: bad argument (k % 8 == 0)");
+  if (((uintptr_t)x & 15) || ((uintptr_t)w & 15) || ((uintptr_t)y & 15) || (bias && ((uintptr_t)bias & 15)) ||
+      (residual && ((uintptr_t)residual & 15)))
+    return set_error(h, RR_EINVAL, "rr_linear_bf16_ln: 16-B alignment");
+  if ((stats_in == nullptr) == (stats_out == nullptr))
+    return set_error(h, RR_EINVAL, "rr_linear_bf16_ln: exactly one of stats_in (fold) and stats_out (produce)");
+  if (stats_out) {
+    // the producer: the residual GEMM (fp32 output) writing the bf16 copy and the partials
+    if (!xb_out || !residual || !bias || act != 0 || out_bf16 || (n % 256) || ((uintptr_t)xb_out & 15) ||
+        ((uintptr_t)stats_out & 7))
+      return set_error(h, RR_EINVAL, "rr_linear_bf16_ln: stats_out needs bias, residual, fp32 output, n % 256 == 0");
+  } else {
+    // the consumer: bias, bf16 output, K in whole 64-deep k-tiles
+    if (!colsum || !bias || residual || !out_bf16 || (k % 64) || (n & 3) || ((uintptr_t)colsum & 15) ||
+        !(eps >= 0.f))
+      return set_error(h, RR_EINVAL, "rr_linear_bf16_ln: stats_in needs colsum, bias, bf16 output, k % 64 == 0");
+  }
+  if (m == 0) return RR_OK;
+  GemmArgs g;
+  g.A = (const float*)x;
+  g.lda = k;
+  g.M = m;
+  g.K = k;
+  g.B = (const float*)w;
+  g.ldb = k;
+  g.N = n;
+  g.C = (float*)y;
+  g.ldc = n;
+  g.bias = bias;
+  g.residual = residual;
+  g.relu = act;
+  g.out_bf16 = out_bf16 ? 1 : 0;
+  g.stats_out = stats_out;
+  g.c2 = (uint16_t*)xb_out;
+  g.stats_in = stats_in;
+  g.colsum = colsum;
+  g.stats_k = k;
+  g.ln_eps = eps;
+  return launch_gemm(h, A_DENSE, E_STORE, g, (hipStream_t)stream, kTimeGemm, DT_BF16);
+}
+
 int rr_cosine_scores(rr_handle_t h, const float* queries, int nq, const float* gallery, long long n, int d,
                      float* scores, void* stream) {
   RR_ENTRY(h);

@@ -226,6 +226,17 @@ struct GemmArgs {
   // columns 7 pc .. +6 of the POH x POW pooled map pool_out (NHWC, N channels)
   float* pool_out = nullptr;
   int POH = 0, POW = 0, pool_tr = 0, pool_tc = 0;
+  // ViT LayerNorm fold (bf16 stored-C GEMMs, 256-column tiles):
+  //  stats_out: also write bf16(C) to c2 ([M][ldc]) and, per row and 256-column
+  //   tile t, the LayerNorm partials (mean_t, M2_t) of C to stats_out[M][T][2];
+  //  stats_in: A holds bf16 rows of a LayerNorm input with those partials
+  //   (T = ceil(stats_k / 256)); C = rstd (A.B^T - mean colsum) + bias
+  uint16_t* c2 = nullptr;
+  float* stats_out = nullptr;
+  const float* stats_in = nullptr;
+  const float* colsum = nullptr;
+  int stats_k = 0;
+  float ln_eps = 0.f;
   // block -> tile order of the low-precision filter sweeps (tile_coords)
   int tile_order = 0;
   // the 256x320 bf16 filter sweep's L2 prefetch of A (gemm_kernel PF), and
@@ -248,6 +259,13 @@ struct GemmArgs {
 //   range stream the same rows at about the same time.  The grid is
 //   tile_grid(...) blocks; the padding blocks get false (exit before any
 //   barrier).
+// 64-lane butterfly sum (the same order on every lane and every call)
+__device__ __forceinline__ float wave_sum(float x) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
+  return x;
+}
+
 __host__ __device__ inline long long tile_grid(int order, long long tiles_m, long long tiles_n) {
   if (order <= 0) return tiles_m * tiles_n;
   const long long nr = 8 / order, r = (tiles_m + nr - 1) / nr;

@@ -150,6 +150,28 @@ __global__ __launch_bounds__(256) void layernorm_vec_kernel(const float* __restr
   ln_row_vec<NV>(v, lane, gamma, beta, eps, y + (long long)row * (256 * NV));
 }
 
+// The LayerNorm partials of rr_linear_bf16_ln for rows no GEMM produced: one
+// wave per (row, 256-column tile), the same arithmetic as the GEMM epilogue's
+// EP_STATS (gemm_epilogue.hpp store_slab): bf16 copy, tile mean, then
+// M2 = sum (x - mean)^2, each a 64-lane butterfly sum of per-lane 4-sums.
+__global__ __launch_bounds__(256) void ln_partials_kernel(const float* __restrict__ x, int M, int D,
+                                                          uint16_t* __restrict__ xb, float* __restrict__ st) {
+  typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+  const int T = D >> 8;
+  const long long w = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  if (w >= (long long)M * T) return;
+  const long long row = w / T;
+  const int t = (int)(w - row * T);
+  const long long o = row * D + 256 * t + 4 * lane;
+  const f32x4 v = *reinterpret_cast<const f32x4*>(x + o);
+  *reinterpret_cast<bf16x4*>(xb + o) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
+  const float mt = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / 256.0f);
+  const f32x4 dv = v - mt;
+  const float m2 = wave_sum((dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]));
+  if (lane == 0) *reinterpret_cast<float2*>(st + w * 2) = float2{mt, m2};
+}
+
 // Token assembly with ln_pre fused (:226-229): one wave per token row, the
 // row (cls or patch embedding, + positional embedding) is formed in registers
 // and normalised there, so the un-normalised tokens never reach HBM.  Same
@@ -671,6 +693,21 @@ extern "C" int rr_layernorm_ex(rr_handle_t h, const float* x, long long ldx, int
   else
     launch_ln<float>(per, grid, s, x, ldx, m, d, gamma, beta, eps, (float*)y);
   return check_hip(h, hipGetLastError(), "layernorm launch");
+}
+
+extern "C" int rr_ln_partials_bf16(rr_handle_t h, const float* x, int m, int d, void* xb, float* stats,
+                                   void* stream) {
+  RR_ENTRY(h);
+  if (!x || !xb || !stats || m < 0 || d <= 0 || (d % 256) || (((uintptr_t)x | (uintptr_t)xb) & 15) ||
+      ((uintptr_t)stats & 7))
+    return set_error(h, RR_EINVAL, "rr_ln_partials_bf16: bad argument (d % 256 == 0, 16-B aligned rows)");
+  if (m == 0) return RR_OK;
+  hipStream_t s = (hipStream_t)stream;
+  TimedLaunch tl(h, kTimeElem, s);
+  const long long waves = (long long)m * (d / 256);
+  hipLaunchKernelGGL(ln_partials_kernel, dim3((unsigned)((waves * 64 + 255) / 256)), dim3(256), 0, s, x, m, d,
+                     (uint16_t*)xb, stats);
+  return check_hip(h, hipGetLastError(), "ln_partials launch");
 }
 
 extern "C" int rr_patchify(rr_handle_t h, const float* x, int b, int hgt, int wid, int c, int patch, float* y,

@@ -349,11 +349,31 @@ class VisionTransformer(_Extractor):
             for blk in self.blocks:
                 for k in ("attn.in_proj_weight", "attn.out_proj.weight", "mlp.c_fc.weight", "mlp.c_proj.weight"):
                     blk[k + ".bf16"] = blk[k].to(torch.bfloat16)
+                # ln_1 / ln_2 folded into the in-proj / c_fc GEMMs (rr_linear_bf16_ln)
+                blk["qkv.fold"] = ops.ln_fold_weights(blk["attn.in_proj_weight"], blk["attn.in_proj_bias"],
+                                                      blk["ln_1.weight"], blk["ln_1.bias"])
+                blk["fc.fold"] = ops.ln_fold_weights(blk["mlp.c_fc.weight"], blk["mlp.c_fc.bias"],
+                                                     blk["ln_2.weight"], blk["ln_2.bias"])
+        # the LayerNorm fold needs 256-column residual rows
+        self.ln_fold = dtype == "bf16" and width % 256 == 0
 
     def _forward_bf16(self, x_nhwc, b):
         # patch rows straight to bf16; ln_pre fused into the token assembly
         p = ops.patchify(x_nhwc, self.patch, out_bf16=True)
         x = ops.vit_tokens(ops.linear_bf16(p, self.conv_w_bf), b, self.cls, self.pos, ln=self.ln_pre)
+        if self.ln_fold:
+            # ln_1 / ln_2 (:188-190) folded into the in-proj / c_fc GEMMs: the
+            # residual GEMMs' epilogues write the bf16 rows and the row
+            # statistics, so no LayerNorm pass re-reads the fp32 stream
+            xb, st = ops.ln_partials_bf16(x)
+            for blk in self.blocks:
+                qkv = ops.linear_bf16_ln_fold(xb, st, *blk["qkv.fold"])
+                a = ops.attention_bf16(qkv, b, self.seq, self.heads)
+                x, xb, st = ops.linear_bf16_ln_produce(a, blk["attn.out_proj.weight.bf16"], blk["attn.out_proj.bias"], x)
+                y = ops.linear_bf16_ln_fold(xb, st, *blk["fc.fold"], act=2)
+                x, xb, st = ops.linear_bf16_ln_produce(y, blk["mlp.c_proj.weight.bf16"], blk["mlp.c_proj.bias"], x)
+            cls = ops.layernorm(x, *self.ln_post, rows=b, row_stride=self.seq * self.width)
+            return ops.linear(cls, self.proj_t)
         for blk in self.blocks:
             y = ops.layernorm_bf16(x, blk["ln_1.weight"], blk["ln_1.bias"])
             # QKV rows in bf16 (RNE, exactly as the attention rounds fp32 rows): half the bytes

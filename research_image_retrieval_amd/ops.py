@@ -723,6 +723,76 @@ def linear_bf16(x, w, bias=None, residual=None, act=0, out_bf16=False):
     return y
 
 
+def linear_bf16_ln_produce(x, w, bias, residual):
+    """The residual GEMM of a ViT block with the next LayerNorm's inputs
+    produced in its epilogue (rr_linear_bf16_ln, stats_out): returns (y fp32
+    [M,N] = x.w^T + bias + residual, bf16(y), per-row 256-column-tile
+    LayerNorm partials [M, N/256, 2])."""
+    if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
+        raise TypeError("linear_bf16_ln_produce: x and w must be bfloat16")
+    if x.dim() != 2 or w.dim() != 2 or not x.is_contiguous() or not w.is_contiguous() or x.shape[1] != w.shape[1]:
+        raise ValueError("linear_bf16_ln_produce: contiguous x [M,K] and w [N,K] with matching K")
+    dev = _dev(x)
+    m, k = x.shape
+    n = w.shape[0]
+    if n % 256:
+        raise ValueError("linear_bf16_ln_produce: N % 256 == 0")
+    if _f32(bias, "bias").numel() != n or tuple(_f32(residual, "residual").shape) != (m, n):
+        raise ValueError("linear_bf16_ln_produce: bias [N] and residual [M,N]")
+    y = torch.empty((m, n), dtype=torch.float32, device=x.device)
+    yb = torch.empty((m, n), dtype=torch.bfloat16, device=x.device)
+    st = torch.empty((m, n // 256, 2), dtype=torch.float32, device=x.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_linear_bf16_ln(hd, _ptr(x), m, k, _ptr(w), _ptr(bias), n, _ptr(residual), 0, 0, _ptr(y),
+                                            None, None, 0.0, _ptr(st), _ptr(yb), _stream(dev)), hd, "rr_linear_bf16_ln")
+    return y, yb, st
+
+
+def linear_bf16_ln_fold(xb, stats, w_folded, colsum, bias_folded, act=0, eps=1e-5):
+    """act(LayerNorm(x) . W^T + b) -> bf16 with the LayerNorm folded into the
+    GEMM (rr_linear_bf16_ln, stats_in): xb = bf16 rows of x and their
+    partials (linear_bf16_ln_produce / ln_partials_bf16), w_folded =
+    bf16(W o gamma), colsum = its fp32 row sums, bias_folded = b + W beta
+    (ln_fold_weights)."""
+    if xb.dtype != torch.bfloat16 or w_folded.dtype != torch.bfloat16:
+        raise TypeError("linear_bf16_ln_fold: xb and w_folded must be bfloat16")
+    dev = _dev(xb)
+    m, k = xb.shape
+    n = w_folded.shape[0]
+    if tuple(stats.shape) != (m, (k + 255) // 256, 2) or w_folded.shape[1] != k:
+        raise ValueError("linear_bf16_ln_fold: stats [M, ceil(K/256), 2], w_folded [N, K]")
+    y = torch.empty((m, n), dtype=torch.bfloat16, device=xb.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_linear_bf16_ln(hd, _ptr(xb), m, k, _ptr(w_folded), _ptr(bias_folded), n, None, int(act),
+                                            1, _ptr(y), _ptr(stats), _ptr(colsum), float(eps), None, None,
+                                            _stream(dev)), hd, "rr_linear_bf16_ln")
+    return y
+
+
+def ln_partials_bf16(x):
+    """(bf16(x), the LayerNorm partials [M, D/256, 2]) of fp32 rows x [M, D]
+    (rr_ln_partials_bf16): the first block's ln_1 input, which no GEMM wrote."""
+    _f32(x, "ln_partials_bf16")
+    dev = _dev(x)
+    d = x.shape[-1]
+    m = x.numel() // d
+    xb = torch.empty((m, d), dtype=torch.bfloat16, device=x.device)
+    st = torch.empty((m, d // 256, 2), dtype=torch.float32, device=x.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_ln_partials_bf16(hd, _ptr(x), m, d, _ptr(xb), _ptr(st), _stream(dev)), hd,
+               "rr_ln_partials_bf16")
+    return xb, st
+
+
+def ln_fold_weights(w, b, gamma, beta):
+    """Fold a LayerNorm (gamma, beta) into the following linear (w [N,K] fp32,
+    b [N]): (bf16(w o gamma), fp32 row sums of that bf16 matrix, b + w beta)."""
+    wf = (w.float() * gamma.float()[None, :]).to(torch.bfloat16).contiguous()
+    colsum = wf.float().sum(dim=1).contiguous()
+    bf = (b.double() + w.double() @ beta.double()).float().contiguous()
+    return wf, colsum, bf
+
+
 def layernorm_bf16(x, gamma, beta, eps=1e-5):
     _f32(x, "layernorm_bf16")
     dev = _dev(x)

@@ -165,3 +165,89 @@ def test_linear_bf16_issue_spread_bit_identical(cuda, m, k, n, kind):
                 outs[il] = ops.linear_bf16(x, w, bias, residual=r)
     assert torch.equal(outs[0].view(torch.int16) if outs[0].dtype == torch.bfloat16 else outs[0].view(torch.int32),
                        outs[1].view(torch.int16) if outs[1].dtype == torch.bfloat16 else outs[1].view(torch.int32))
+
+
+def test_ln_partials_and_produce_epilogue(cuda):
+    """The LayerNorm fold's producer side: rr_ln_partials_bf16 and the residual
+    GEMM's EP_STATS epilogue give bf16(y) exactly and per-tile (mean, M2)
+    whose Chan combination matches float64 LayerNorm statistics; the GEMM's
+    fp32 output is bit-identical to rr_linear_bf16's."""
+    g = torch.Generator().manual_seed(3)
+    m, k, n = 3 * 197 + 11, 768, 768
+    a = (torch.randn(m, k, generator=g)).bfloat16().to(cuda)
+    w = (torch.randn(n, k, generator=g) / k ** 0.5).bfloat16().to(cuda)
+    bias = torch.randn(n, generator=g).to(cuda)
+    r = (torch.randn(m, n, generator=g) * 3 + 0.5).to(cuda)  # a residual stream with a mean offset
+    y, yb, st = ops.linear_bf16_ln_produce(a, w, bias, r)
+    with ops.tuning(cuda.index, lp_cfg=3):
+        y_ref = ops.linear_bf16(a, w, bias, residual=r)
+    assert torch.equal(y.view(torch.int32), y_ref.view(torch.int32))
+    assert torch.equal(yb.view(torch.int16), y.bfloat16().view(torch.int16))
+    xb, st2 = ops.ln_partials_bf16(y)
+    assert torch.equal(xb.view(torch.int16), yb.view(torch.int16))
+    yd = y.double().cpu().view(m, n // 256, 256)
+    mt = yd.mean(-1)
+    m2 = ((yd - mt[..., None]) ** 2).sum(-1)
+    for s in (st, st2):
+        s = s.double().cpu()
+        assert (s[..., 0] - mt).abs().max() <= 1e-6 * (1 + mt.abs().max())
+        assert ((s[..., 1] - m2).abs() / m2).max() <= 1e-5
+    torch.testing.assert_close(st, st2, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("act", [0, 2])
+def test_linear_bf16_ln_fold_vs_float64(cuda, act):
+    """The consumer side: act(LayerNorm(x) W^T + b) with the LayerNorm folded
+    into the GEMM epilogue (bf16(x) rows, W o gamma, the row statistics from
+    the partials) against float64, next to the unfused LayerNorm -> bf16 ->
+    GEMM path: the same error scale (bf16 operand rounding), on rows with a
+    mean offset and heavy channels (|x| up to 60x the rest)."""
+    g = torch.Generator().manual_seed(4 + act)
+    m, k, n = 2 * 197 + 3, 768, 3072 if act else 2304
+    x = torch.randn(m, k, generator=g) + 0.7
+    x[:, :4] *= 60.0  # a few massive-activation channels, as CLIP residual streams have
+    w = torch.randn(n, k, generator=g) / k ** 0.5
+    b = torch.randn(n, generator=g) * 0.1
+    gam = 1.0 + 0.2 * torch.randn(k, generator=g)
+    bet = 0.1 * torch.randn(k, generator=g)
+    xd = x.to(cuda)
+    xb, st = ops.ln_partials_bf16(xd)
+    wf, cs, bf = ops.ln_fold_weights(w.to(cuda), b.to(cuda), gam.to(cuda), bet.to(cuda))
+    y_fold = ops.linear_bf16_ln_fold(xb, st, wf, cs, bf, act=act).float().cpu().double()
+    y_ln = ops.linear_bf16(ops.layernorm_bf16(xd, gam.to(cuda), bet.to(cuda)), w.bfloat16().to(cuda), b.to(cuda),
+                           act=act, out_bf16=True).float().cpu().double()
+    ref = torch.nn.functional.layer_norm(x.double(), (k,), gam.double(), bet.double(), 1e-5) @ w.double().t() + b.double()
+    if act == 2:
+        ref = ref * torch.sigmoid(1.702 * ref)
+    e_fold = (y_fold - ref).abs()
+    e_ln = (y_ln - ref).abs()
+    scale = ref.abs().mean()
+    print(f"act {act}: fold max {e_fold.max().item() / scale:.3e} mean {e_fold.mean().item() / scale:.3e} | "
+          f"LayerNorm path max {e_ln.max().item() / scale:.3e} mean {e_ln.mean().item() / scale:.3e} (x mean |ref|)")
+    # bf16 output rounding alone is 2^-9 relative; the operand roundings add a few times that
+    assert e_fold.mean() <= 2.0 * e_ln.mean() + 1e-6
+    assert e_fold.max() <= 2.0 * e_ln.max() + 1e-6
+
+
+def test_vit_bf16_ln_fold_matches_unfused(cuda):
+    """The whole ViT-B/16 bf16 forward with the ln_1 / ln_2 fold against the
+    same network with LayerNorm passes: descriptors within the C4 bar of each
+    other (cosine >= 0.99999) and of the fp32 oracle (>= 0.9999)."""
+    from research_image_retrieval_amd import weights as W
+    sd = W.synthetic_vit_state_dict(out_dim=512, seed=0)
+    net = VisionTransformer(224, 16, 768, 12, 12, 512, state_dict=sd, device=cuda, dtype="bf16")
+    assert net.ln_fold
+    rs = np.random.RandomState(7)
+    imgs = torch.from_numpy(rs.randint(0, 256, size=(6, 224, 224, 3), dtype=np.uint8))
+    d_fold = net.forward_test_u8(imgs.to(cuda)).cpu().double()
+    net.ln_fold = False
+    d_ln = net.forward_test_u8(imgs.to(cuda)).cpu().double()
+    cos = (d_fold * d_ln).sum(1)
+    with torch.no_grad():
+        ref = torch.cat([torch.nn.functional.normalize(
+            embed_ref.vit_forward(embed_ref.normalize_u8(imgs[i:i + 1]), sd, 16, 768, 12, 12), dim=-1)
+            for i in range(2)]).double()
+    cos_ref = (d_fold[:2] * ref).sum(1)
+    print(f"fold vs LayerNorm passes: min cosine {cos.min().item():.8f}; fold vs fp32 oracle {cos_ref.min().item():.8f}")
+    assert float(cos.min()) >= 0.99999
+    assert float(cos_ref.min()) >= 0.9999
