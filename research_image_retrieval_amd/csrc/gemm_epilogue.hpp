@@ -61,7 +61,8 @@ inline int ep_flags(const GemmArgs& g) {
 // Row m's LayerNorm mean and 1/sqrt(var + eps) from the producer's per-tile
 // partials (mean_t, M2_t over n_t = min(256, d - 256 t) columns), combined as
 // Chan et al.: mean = sum n_t mean_t / d, M2 = sum M2_t + n_t (mean_t - mean)^2
-// (biased variance M2 / d, as nn.LayerNorm).
+// (biased variance M2 / d, as nn.LayerNorm).  The consumer GEMM computes its
+// tile's rows once, before its k-loop, into LDS (ln_tile_stats).
 __device__ __forceinline__ void ln_row_stats(const float* st, long long m, int d, float eps, float& mean,
                                              float& rstd) {
   const int T = (d + 255) >> 8;
@@ -127,10 +128,11 @@ __device__ __forceinline__ int h2_exp(float amax) {
 template <int FL, int P, int ITERS, int NT, int C4, int CS, int BI>
 __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const float* ct, const f32x4 (&bias_v)[BI],
                                            const f32x4 (&res)[ITERS], int tid, int mb, int n0, const f32x4 (&sc_v)[BI],
-                                           float& am, const f32x4& cs_v) {
+                                           float& am, const f32x4& cs_v, const float* ln_l = nullptr) {
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
-  constexpr int GR = ITERS < 4 ? ITERS : (P == 1 ? 8 : 4);
   constexpr bool FIXED = FL >= 0;
+  // (the LayerNorm fold's epilogue holds two more values per row: fewer LDS reads ahead)
+  constexpr int GR = ITERS < 4 ? ITERS : (FIXED && (FL & EP_LNFOLD) != 0) ? 2 : (P == 1 ? 8 : 4);
   // EP_STATS: one row of the 256-column tile per wave and iteration
   static_assert(!(FIXED && (FL & (EP_STATS | EP_LNFOLD))) || (BI == 1 && C4 == 64), "LayerNorm fold: 256-column tiles");
   const bool has_bias = FIXED ? (FL & EP_BIAS) != 0 : g.bias != nullptr;
@@ -171,9 +173,9 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
     f32x4 v = cv[it];
     if constexpr (FIXED && (FL & EP_SCALE) != 0) v *= sc_v[BI == 1 ? 0 : it];
     if constexpr (FIXED && (FL & EP_LNFOLD) != 0) {
-      float mean, rstd;
-      ln_row_stats(g.stats_in, m, g.stats_k, g.ln_eps, mean, rstd);
-      v = (v - mean * cs_v) * rstd;
+      // the row's (mean, rstd), staged in LDS before the k-loop (slab-relative)
+      const float2 mr = *reinterpret_cast<const float2*>(ln_l + 2 * (m - mb));
+      v = (v - mr.x * cs_v) * mr.y;
     }
     if (has_bias) v += bias_v[BI == 1 ? 0 : it];
     if (has_res) v += res[it];
@@ -202,6 +204,7 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
       const float mt = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / 256.0f);
       const f32x4 dv = v - mt;
       const float m2 = wave_sum((dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]));
+      // (wave-uniform: lane 0 stores)
       if ((threadIdx.x & 63) == 0) {
         const int T = (g.N + 255) >> 8;
         *reinterpret_cast<float2*>(g.stats_out + ((long long)m * T + (n0 >> 8)) * 2) = float2{mt, m2};
@@ -219,7 +222,7 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
 // barrier (the LDS is free).
 template <int WM, int WN, int FM, int FN, int CAPF, bool MF16 = false, int FL = -1>
 __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, const f32x16 (&acc)[FM][FN], float* lds,
-                                               int m0, int n0, float a_isc = 1.f) {
+                                               int m0, int n0, float a_isc = 1.f, const float* ln_lds = nullptr) {
   constexpr int NT = 64 * WM * WN;
   constexpr int WTM = 32 * FM, WTN = 32 * FN;
   constexpr int BM = WTM * WM, BN = WTN * WN;
@@ -327,7 +330,7 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
       }
       if constexpr (FL >= 0 && (FL & EP_LNFOLD) != 0) asm volatile("" : "+v"(cs_v));
       store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, CS, BI>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0, sc_v, am,
-                                                                 cs_v);
+                                                                 cs_v, ln_lds ? ln_lds + 2 * rbase : nullptr);
     } else {
       for (int idx = tid; idx < SLAB * C4; idx += NT) {
         const int row = idx / C4, c4 = idx - row * C4;

@@ -134,7 +134,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   static_assert(BM % ROWS_PER_PASS == 0 && BN % ROWS_PER_PASS == 0, "staging passes must tile the block");
   constexpr int BUF = (BM + BN) * BK;  // floats per LDS buffer
   static_assert(!PF || (GL && !MF16 && EMODE != E_STORE), "PF: LDS-DMA sweep tiles");
-  __shared__ __attribute__((aligned(16))) float lds[2 * BUF + (PF ? 64 : 0)];
+  // EP_LNFOLD: the tile's rows' LayerNorm (mean, rstd) beside the stages
+  constexpr bool LNF = EPI >= 0 && (EPI & EP_LNFOLD) != 0;
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF + (PF ? 64 : 0) + (LNF ? 2 * BM : 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -358,6 +360,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   }
 
   const int lr = lane & 31, lh = lane >> 5;
+
+  // EP_LNFOLD: each of the tile's rows combines its producer's partials once,
+  // before the k-loop (the prologue's barrier publishes them to the epilogue)
+  if constexpr (LNF) {
+    if (tid < BM) {
+      float mean = 0.f, rstd = 0.f;
+      if (m0 + tid < g.M) ln_row_stats(g.stats_in, m0 + tid, g.stats_k, g.ln_eps, mean, rstd);
+      *reinterpret_cast<float2*>(lds + 2 * BUF + 2 * tid) = float2{mean, rstd};
+    }
+  }
 
   // bf16 16x16x32 with LDS-DMA: the barrier of k-tile kt sits inside its last
   // k-step, after that step's fragments are in registers: wait for tile kt+1's
@@ -819,7 +831,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   }
   }
 
-  if constexpr (EMODE == E_STORE) epilogue_store<WM, WN, FM, FN, 2 * BUF, (bool)MF16, EPI>(g, Cb, acc, lds, m0, n0);
+  if constexpr (EMODE == E_STORE)
+    epilogue_store<WM, WN, FM, FN, 2 * BUF, (bool)MF16, EPI>(g, Cb, acc, lds, m0, n0, 1.f, LNF ? lds + 2 * BUF : nullptr);
 }
 
 template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0,

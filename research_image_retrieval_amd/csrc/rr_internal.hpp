@@ -1,6 +1,8 @@
 // rr_internal.hpp — shared declarations for librr (gfx950 only).
 #pragma once
 
+#include <type_traits>
+
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include <string>
@@ -259,11 +261,21 @@ struct GemmArgs {
 //   range stream the same rows at about the same time.  The grid is
 //   tile_grid(...) blocks; the padding blocks get false (exit before any
 //   barrier).
-// 64-lane butterfly sum (the same order on every lane and every call)
+// 64-lane sum, returned wave-uniform: DPP row_shr 1/2/4/8 sums each 16-lane
+// row into its lane 15 (out-of-row sources read 0), then the four rows'
+// lanes 15, 31, 47, 63 are added in that order.  VALU-only (no LDS
+// crossbar), and the same order on every call.
 __device__ __forceinline__ float wave_sum(float x) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) x += __shfl_xor(x, o);
-  return x;
+  auto shr = [](float v, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), decltype(ctrl)::value, 0xf, 0xf, true));
+  };
+  x += shr(x, std::integral_constant<int, 0x111>{});  // row_shr:1
+  x += shr(x, std::integral_constant<int, 0x112>{});  // row_shr:2
+  x += shr(x, std::integral_constant<int, 0x114>{});  // row_shr:4
+  x += shr(x, std::integral_constant<int, 0x118>{});  // row_shr:8
+  const int xi = __float_as_int(x);
+  return (__int_as_float(__builtin_amdgcn_readlane(xi, 15)) + __int_as_float(__builtin_amdgcn_readlane(xi, 31))) +
+         (__int_as_float(__builtin_amdgcn_readlane(xi, 47)) + __int_as_float(__builtin_amdgcn_readlane(xi, 63)));
 }
 
 __host__ __device__ inline long long tile_grid(int order, long long tiles_m, long long tiles_n) {
