@@ -46,12 +46,26 @@ def wall(fn, reps=2):
     return (time.perf_counter() - t) / reps * 1e3
 
 
+def split(c):
+    """spec -> (rr_set_tuning keys, extractor attributes: keys that are not
+    tuning keys, e.g. ln_fold=0 on the ViT)"""
+    kv = parse(c)
+    return ({k: v for k, v in kv.items() if k in ops._TUNE_KEYS},
+            {k: v for k, v in kv.items() if k not in ops._TUNE_KEYS})
+
+
 if EMB:
     res = {c: [] for c in EMB}
     for _ in range(ROUNDS):
         for c in EMB:
-            with ops.tuning(0, **parse(c)):
+            tk, attrs = split(c)
+            saved = {k: getattr(net, k) for k in attrs}
+            for k, v in attrs.items():
+                setattr(net, k, bool(v) if isinstance(saved[k], bool) else v)
+            with ops.tuning(0, **tk):
                 res[c].append(wall(lambda: net.forward_test_u8(imgs)))
+            for k, v in saved.items():
+                setattr(net, k, v)
     for c in EMB:
         print(f"embed {c:40s} median {statistics.median(res[c]):8.3f} ms  all {['%.2f' % v for v in res[c]]}",
               flush=True)
