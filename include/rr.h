@@ -50,7 +50,7 @@ typedef struct rr_handle_s* rr_handle_t;
  * f16x2 entries rr_conv2d_h2 / rr_bottleneck_out_h2 / rr_stem_pool_h2 /
  * rr_split2_f16 / rr_amax_f32 were added (no existing entry changed).  Bindings compare
  * rr_abi_version() with the RR_ABI_VERSION they were written against.     */
-#define RR_ABI_VERSION 3
+#define RR_ABI_VERSION 4
 int rr_abi_version(void);
 
 /* ---- handle ------------------------------------------------------------ */

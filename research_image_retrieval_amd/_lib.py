@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(_HERE, "librr.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_EWORKSPACE, RR_EOVERFLOW = 0, -1, -2, -3, -4
-ABI_VERSION = 3  # RR_ABI_VERSION of include/rr.h these signatures follow
+ABI_VERSION = 4  # RR_ABI_VERSION of include/rr.h these signatures follow
 AMAX_SLOTS = 64  # RR_AMAX_SLOTS
 
 # timing classes (rr_timing_enable / rr_timing_collect)
