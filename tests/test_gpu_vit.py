@@ -251,3 +251,47 @@ def test_vit_bf16_ln_fold_matches_unfused(cuda):
     print(f"fold vs LayerNorm passes: min cosine {cos.min().item():.8f}; fold vs fp32 oracle {cos_ref.min().item():.8f}")
     assert float(cos.min()) >= 0.99999
     assert float(cos_ref.min()) >= 0.9999
+
+
+def test_linear_bf16_ln_argument_checks_and_edges(cuda):
+    """rr_linear_bf16_ln: exactly one of stats_in / stats_out, the producer's
+    n % 256 and residual requirements, the consumer's k % 64 and bf16 output
+    (RR_EINVAL otherwise); m = 0 is a no-op; a single row works."""
+    import ctypes
+    from research_image_retrieval_amd import _lib
+    L, h = _lib.lib(), _lib.handle(cuda.index)
+    m, k, n = 1, 768, 768
+    x = torch.randn(m, k, device=cuda).bfloat16()
+    w = (torch.randn(n, k, device=cuda) / k ** 0.5).bfloat16()
+    bias = torch.randn(n, device=cuda)
+    r = torch.randn(m, n, device=cuda)
+    y = torch.empty(m, n, device=cuda)
+    yb = torch.empty(m, n, device=cuda, dtype=torch.bfloat16)
+    st = torch.empty(m, n // 256, 2, device=cuda)
+    p = lambda t: ctypes.c_void_p(t.data_ptr()) if t is not None else None  # noqa: E731
+    s = torch.cuda.current_stream(cuda).cuda_stream
+    # neither / both stats pointers
+    assert L.rr_linear_bf16_ln(h, p(x), m, k, p(w), p(bias), n, p(r), 0, 0, p(y), None, None, 0.0, None, None,
+                               s) == _lib.RR_EINVAL
+    assert L.rr_linear_bf16_ln(h, p(x), m, k, p(w), p(bias), n, p(r), 0, 0, p(y), p(st), p(bias), 1e-5, p(st), p(yb),
+                               s) == _lib.RR_EINVAL
+    # producer without a residual / with n % 256 != 0
+    assert L.rr_linear_bf16_ln(h, p(x), m, k, p(w), p(bias), n, None, 0, 0, p(y), None, None, 0.0, p(st), p(yb),
+                               s) == _lib.RR_EINVAL
+    assert L.rr_linear_bf16_ln(h, p(x), m, k, p(w), p(bias), 640, p(r), 0, 0, p(y), None, None, 0.0, p(st), p(yb),
+                               s) == _lib.RR_EINVAL
+    # consumer with fp32 output
+    cs = w.float().sum(1)
+    assert L.rr_linear_bf16_ln(h, p(x), m, k, p(w), p(bias), n, None, 0, 0, p(y), p(st), p(cs), 1e-5, None, None,
+                               s) == _lib.RR_EINVAL
+    # m = 0: nothing to do
+    assert L.rr_linear_bf16_ln(h, p(x), 0, k, p(w), p(bias), n, p(r), 0, 0, p(y), None, None, 0.0, p(st), p(yb),
+                               s) == 0
+    # one row, producer then consumer
+    y1, yb1, st1 = ops.linear_bf16_ln_produce(x, w, bias, r)
+    assert torch.equal(yb1.view(torch.int16), y1.bfloat16().view(torch.int16))
+    gam, bet = torch.ones(n, device=cuda), torch.zeros(n, device=cuda)
+    wf, csum, bf = ops.ln_fold_weights(w.float(), bias, gam, bet)
+    out = ops.linear_bf16_ln_fold(yb1, st1, wf, csum, bf).float()
+    ref = ops.linear_bf16(ops.layernorm_bf16(y1, gam, bet), w, bias).float()
+    assert (out - ref).abs().max().item() <= 0.05 * ref.abs().mean().item()
