@@ -108,7 +108,8 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     (the L2 prefetch of RR_TUNE_SWEEP_PF = 1 runs without it)
  *   RR_TUNE_CONV_IL:  the f16x2 256x256 conv tile (RR_TUNE_S3_CFG 12): 1 = the next
  *                     k-tiles' B DMA and A loads issued one group at a time among the
- *                     MFMAs, 0 = one burst at the top of the k-tile; -1 = the library's pick (0)
+ *                     MFMAs, 2 = the same for the GEMMs without a residual epilogue only,
+ *                     0 = one burst at the top of the k-tile; -1 = the library's pick (0)
  *   RR_TUNE_HALO_MF:  the f16x2 halo-staged 3x3 tiles on v_mfma_f32_16x16x32_f16 (1) or
  *                     v_mfma_f32_32x32x16_f16 (0); -1 = the library's pick (RR_TUNE_S3_CFG
  *                     13 / 14 override it)

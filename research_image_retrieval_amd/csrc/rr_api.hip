@@ -167,7 +167,7 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.sweep_il = value;
       return RR_OK;
     case RR_TUNE_CONV_IL:
-      if (!in({-1, 0, 1})) break;
+      if (!in({-1, 0, 1, 2})) break;
       h->tune.conv_il = value;
       return RR_OK;
     case RR_TUNE_HALO_MF:

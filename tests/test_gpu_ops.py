@@ -123,7 +123,7 @@ def test_handle_device_and_tuning_validation(cuda):
     assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_PF, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_MF16, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_IL, 2) == _lib.RR_EINVAL
-    assert L.rr_set_tuning(h, _lib.TUNE_CONV_IL, 2) == _lib.RR_EINVAL
+    assert L.rr_set_tuning(h, _lib.TUNE_CONV_IL, 3) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_HALO_MF, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_LP_IL, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG_RES, 15) == _lib.RR_EINVAL
