@@ -122,12 +122,15 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
     batch-1 extraction (utils/helpfunc.py:18-48 semantics) through the oracle's
     torch-CPU restatement of ResNet->GeM->whiten->L2->PCA-w->L2, then the
     ranker of iris_evaluate.py:383-386 (torch.mm + full np.argsort) against a
-    400k-row gallery sample, scaled to the full gallery."""
+    400k-row gallery sample, scaled to the full gallery.  The same extraction
+    is also timed at batch 32 ("timed at batch 1 ... and
+    batch 32"): value_b32 / embed_s_per_image_b32."""
     from oracle import embed_ref
     affinity, quota, threads = host_threads()
     default_threads = torch.get_num_threads()
     torch.set_num_threads(threads)
-    n_img, n_q, n_g = 192, 64, 400_000  # ~10-15 s of CPU work on the box's 16-core share
+    n_img, n_q, n_g = 160, 64, 400_000  # ~10-15 s of CPU work on the box's 16-core share
+    n_b32 = 2  # timed batches of 32 images (after one untimed batch)
     sd = W.synthetic_resnet_state_dict(arch, seed)
     ww, wb = W.synthetic_linear(2048, 2048, seed + 1)
     pw, pb = W.synthetic_linear(2048, 2048, seed + 5, scale=1.0 / np.sqrt(2048))
@@ -143,6 +146,13 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
             f = embed_ref.gem_net_forward_test(x, sd, layers, ww, wb)
             embed_ref.pcaw_apply(f, pw, pb)
         t_embed = (time.perf_counter() - t0) / n_img
+        imgs32 = torch.from_numpy(rs.randint(0, 256, size=(32, 224, 224, 3), dtype=np.uint8))
+        for it in range(n_b32 + 1):
+            if it == 1:
+                t0 = time.perf_counter()
+            f = embed_ref.gem_net_forward_test(embed_ref.normalize_u8(imgs32), sd, layers, ww, wb)
+            embed_ref.pcaw_apply(f, pw, pb)
+        t_embed32 = (time.perf_counter() - t0) / (32 * n_b32)
         gen = torch.Generator().manual_seed(7)
         gal = torch.nn.functional.normalize(torch.randn(n_g, d, generator=gen), dim=1)
         q = torch.nn.functional.normalize(torch.randn(n_q, d, generator=gen), dim=1)
@@ -171,9 +181,11 @@ def cpu_baseline(arch, n_total, d, k, seed=0):
             "affinity_cpus": affinity, "granted_cpus": quota, "torch_default_threads": default_threads,
             "sample": f"{n_img} images embedded at batch 1 (224x224, {arch}-GeM+PCA-w, fp32) + {n_q} queries "
                       f"ranked against a {n_g}-row x {d} gallery sample (torch.mm + full np.argsort), "
-                      f"rank time scaled x{scale:.0f} to {n_total} rows",
+                      f"rank time scaled x{scale:.0f} to {n_total} rows; batch-32 figures: {n_b32} timed batches "
+                      f"of 32 images after one untimed batch, same ranker time",
             "embed_s_per_image": t_embed, "rank_s_per_query_argsort": t_rank, "rank_s_per_query_topk": t_rank_topk,
-            "value_with_topk": 1.0 / (t_embed + t_rank_topk), "cpu_model": model}
+            "value_with_topk": 1.0 / (t_embed + t_rank_topk),
+            "embed_s_per_image_b32": t_embed32, "value_b32": 1.0 / (t_embed32 + t_rank), "cpu_model": model}
 
 
 # ---- config C2: ResNet50-GeM 512-d at imsize 1024 over a ROxford5k-shaped set ----
@@ -468,9 +480,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--batch", type=int, default=1280,
-                    help="images per GPU per step (measured C3 images/s on one MI355X, same box: 320: 8634, "
-                         "640: 8985, 960: 9109, 1280: 9206 -- larger batches amortise the gallery sweep and fill "
-                         "the conv grids' last rounds better)")
+                    help="images per GPU per step (1280 = the BASELINE C3 batch; a larger batch amortises the "
+                         "gallery sweep over more queries and fills the conv grids' last rounds better: round 2's "
+                         "sweep on one box, profiles/r02l_batch_sweep.jsonl, was flat above 1280)")
     ap.add_argument("--gallery", type=int, default=1_600_000)
     ap.add_argument("--gallery-kind", choices=("gaussian", "clustered"), default="gaussian",
                     help="gaussian: isotropic rows; clustered: 81,313 landmark-like classes (the prefilter's "
@@ -490,8 +502,9 @@ def main():
                          "fp32 rescoring (bit-identical results)")
     ap.add_argument("--conv-math", choices=("h2", "s3", "f32"), default="h2",
                     help="ResNet trunk convs: h2 = fp32-accurate f16x2 split on the fp16 matrix cores, 3 MFMA "
-                         "products per fp32 product (tests/test_gpu_h2.py); s3 = 3-way bf16 split, 6 products "
-                         "(tests/test_gpu_s3.py); both with error vs float64 <= the exact-fp32 core's; "
+                         "products per fp32 product (tested bar vs float64, tests/test_gpu_h2.py: per conv mean "
+                         "error <= 1.05x and max <= 1.25x the exact-fp32 core's); s3 = 3-way bf16 split, 6 "
+                         "products (tests/test_gpu_s3.py); "
                          "f32 = exact fp32 MFMA")
     ap.add_argument("--ws-budget-gb", type=float, default=4.0,
                     help="ranker workspace budget per rank (bounded candidate buffers, overflowed queries re-run; "

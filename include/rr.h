@@ -48,9 +48,15 @@ typedef struct rr_handle_s* rr_handle_t;
  * arguments under the same name (a caller built against an older header would
  * pass shifted arguments): 2 = rr_alpha_qe gained n_rows (round 2); 3 = the
  * f16x2 entries rr_conv2d_h2 / rr_bottleneck_out_h2 / rr_stem_pool_h2 /
- * rr_split2_f16 / rr_amax_f32 were added (no existing entry changed).  Bindings compare
- * rr_abi_version() with the RR_ABI_VERSION they were written against.     */
-#define RR_ABI_VERSION 4
+ * rr_split2_f16 / rr_amax_f32 were added (no existing entry changed); 4 =
+ * rr_linear_bf16_ln / rr_ln_partials_bf16 were added (round 4; the ViT
+ * LayerNorm fold); 5 = rr_bottleneck_seam_h2 was added and the tuning keys
+ * RR_TUNE_SWEEP_ORDER (6), RR_TUNE_SWEEP_PF (7) and RR_TUNE_LP_IL (12) and the
+ * lp_cfg value 6 were retired (round 5: they lost their A/Bs; rr_set_tuning
+ * now returns RR_EINVAL for them, and their numbers are not reused).
+ * Bindings compare rr_abi_version() with the RR_ABI_VERSION they were
+ * written against.                                                          */
+#define RR_ABI_VERSION 5
 int rr_abi_version(void);
 
 /* ---- handle ------------------------------------------------------------ */
@@ -81,9 +87,7 @@ int rr_get_device(rr_handle_t h, int* device);
  *   RR_TUNE_LP_CFG:   bf16/fp8 core, 1 (128x128), 2 (256x64), 3 (256x256),
  *                     4 (256x320 for bf16 filter / score sweeps, 256x256 otherwise),
  *                     5 (bf16 sweeps with K % 128 == 0, fp8 sweeps with K % 256 == 0:
- *                     256x256 8-phase pipeline; otherwise as 3), 6 (filter sweeps,
- *                     bf16 with K % 32 == 0 or fp8 with K % 128 == 0: gallery rows in
- *                     VGPRs, query panel in LDS, sweep_v.hip; otherwise the pick)
+ *                     256x256 8-phase pipeline; otherwise as 3)
  *   RR_TUNE_S3_CFG:   split cores (bf16x3 and f16x2), 1..14 (gemm_s3.hip tile table;
  *                     9..14 f16x2 only; 13 = the halo-staged stride-1 3x3 tile on
  *                     v_mfma_f32_32x32x16_f16, 14 = the same on v_mfma_f32_16x16x32_f16
@@ -91,31 +95,20 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     7 also selects the implicit-GEMM fused stem over the halo stem)
  *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of
  *                     ~1 us for every other resident block (-1 = the library's pick)
- *   RR_TUNE_SWEEP_ORDER: bf16 / fp8 filter sweeps' block -> tile order: 0 = each XCD a
- *                     contiguous range of gallery tiles against every query panel;
- *                     2 / 4 / 8 = the XCDs split into that many query-panel groups x
- *                     8 / value gallery ranges (when the panels divide evenly);
- *                     -1 = the library's pick
- *   RR_TUNE_SWEEP_PF: the 256x320 bf16 filter sweep: 1 = touch each gallery row's
- *                     line of k-tile kt + 2 while kt computes (L2 prefetch, DMA left in
- *                     flight across the barrier), 0 = off, -1 = the library's pick
  *   RR_TUNE_SWEEP_MF16: the 256x320 bf16 filter sweep on v_mfma_f32_16x16x32_bf16 (1)
  *                     or v_mfma_f32_32x32x16_bf16 (0); -1 = the library's pick (0)
  *   RR_TUNE_SWEEP_IL: the bf16 / fp8 filter sweeps: 1 = the next k-tile's LDS-DMA
  *                     issued chunk by chunk among the k-tile's first MFMAs, 0 = one
  *                     burst at the top of the k-tile; -1 = the library's pick (1 for the
  *                     256x320 bf16 and the fp8 sweeps, 0 for the 256x256 bf16 one)
- *                     (the L2 prefetch of RR_TUNE_SWEEP_PF = 1 runs without it)
  *   RR_TUNE_CONV_IL:  the f16x2 256x256 conv tile (RR_TUNE_S3_CFG 12): 1 = the next
  *                     k-tiles' B DMA and A loads issued one group at a time among the
- *                     MFMAs, 2 = the same for the GEMMs without a residual epilogue only,
- *                     0 = one burst at the top of the k-tile; -1 = the library's pick (0)
+ *                     MFMAs, 0 = one burst at the top of the k-tile; 1 also selects the
+ *                     halo-staged 3x3 tile's 16x16x32 form with its B DMA spread the
+ *                     same way; -1 = the library's pick (0)
  *   RR_TUNE_HALO_MF:  the f16x2 halo-staged 3x3 tiles on v_mfma_f32_16x16x32_f16 (1) or
  *                     v_mfma_f32_32x32x16_f16 (0); -1 = the library's pick (RR_TUNE_S3_CFG
  *                     13 / 14 override it)
- *   RR_TUNE_LP_IL:    the bf16 256x256 stored-C / score tile (lp_cfg 3, the ViT linears):
- *                     1 = the next k-tile's LDS-DMA issued chunk by chunk among the MFMAs
- *                     after the k-tile barrier, 0 = one burst; -1 = the library's pick (0)
  *   RR_TUNE_S3_CFG_RES: as RR_TUNE_S3_CFG, for the split-core GEMMs with a residual
  *                     epilogue only (0 = RR_TUNE_S3_CFG's choice)
  * Any other key or value: RR_EINVAL. */
@@ -124,13 +117,12 @@ int rr_get_device(rr_handle_t h, int* device);
 #define RR_TUNE_LP_CFG 3
 #define RR_TUNE_S3_CFG 4
 #define RR_TUNE_S3_STAGGER 5
-#define RR_TUNE_SWEEP_ORDER 6
-#define RR_TUNE_SWEEP_PF 7
+/* 6, 7: retired (ABI 5) */
 #define RR_TUNE_SWEEP_MF16 8
 #define RR_TUNE_SWEEP_IL 9
 #define RR_TUNE_CONV_IL 10
 #define RR_TUNE_HALO_MF 11
-#define RR_TUNE_LP_IL 12
+/* 12: retired (ABI 5) */
 #define RR_TUNE_S3_CFG_RES 13
 int rr_set_tuning(rr_handle_t h, int key, int value);
 
@@ -444,7 +436,7 @@ int rr_linear_bf16(rr_handle_t h, const void* x, int m, int k, const void* w,
  * / ln_2 of :188-190) folded into the GEMMs, so no LayerNorm pass reads the
  * fp32 residual stream.  Exactly one of stats_in / stats_out is set:
  *  - stats_out (the out-proj / c_proj GEMMs: bias, residual, fp32 y, act 0,
- *    n % 256 == 0): besides y, writes xb_out [m][n] = bf16(y) (RNE) and per row
+ *    n % 256 == 0, k % 64 == 0): besides y, writes xb_out [m][n] = bf16(y) (RNE) and per row
  *    and 256-column tile t the LayerNorm partials of y: stats_out [m][n/256][2]
  *    = (mean_t, M2_t = sum (y - mean_t)^2 over the tile's 256 columns).
  *  - stats_in (the in-proj / c_fc GEMMs: bias, bf16 y, k % 64 == 0): x holds
@@ -454,8 +446,11 @@ int rr_linear_bf16(rr_handle_t h, const void* x, int m, int k, const void* w,
  *      y = act(rstd_m (x.w^T - mean_m colsum) + bias),
  *    mean_m / rstd_m = 1 / sqrt(var + eps) from the partials (biased
  *    variance, combined as Chan et al.).  Equal to LayerNorm -> bf16 ->
- *    rr_linear_bf16 up to where bf16 rounding falls (bf16(y) instead of
- *    bf16(LayerNorm(y))): tests/test_gpu_vit.py.                            */
+ *    rr_linear_bf16 up to where bf16 rounding falls: the operand is bf16(y),
+ *    not bf16(LayerNorm(y)), so each element's rounding error is 2^-9 |y_k|
+ *    instead of 2^-9 |y_k - mean| and the fold's error grows with the rows'
+ *    |mean| / std (tests/test_gpu_vit.py measures a mean offset of 20 std:
+ *    test_linear_bf16_ln_fold_large_mean).                                  */
 int rr_linear_bf16_ln(rr_handle_t h, const void* x, int m, int k, const void* w,
                       const float* bias, int n, const float* residual, int act,
                       int out_bf16, void* y, const float* stats_in,

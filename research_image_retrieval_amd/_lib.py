@@ -16,15 +16,16 @@ LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(_HERE, "librr.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_EWORKSPACE, RR_EOVERFLOW = 0, -1, -2, -3, -4
-ABI_VERSION = 4  # RR_ABI_VERSION of include/rr.h these signatures follow
+ABI_VERSION = 5  # RR_ABI_VERSION of include/rr.h these signatures follow
 AMAX_SLOTS = 64  # RR_AMAX_SLOTS
 
 # timing classes (rr_timing_enable / rr_timing_collect)
 TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM, TIME_COSINE_SEED, TIME_ATTN = 0, 1, 2, 3, 4, 5
 # rr_set_tuning keys
-TUNE_GEMM_CFG, TUNE_GEMM_BK, TUNE_LP_CFG, TUNE_S3_CFG, TUNE_S3_STAGGER, TUNE_SWEEP_ORDER, TUNE_SWEEP_PF, \
-    TUNE_SWEEP_MF16, TUNE_SWEEP_IL, TUNE_CONV_IL, TUNE_HALO_MF, TUNE_LP_IL, TUNE_S3_CFG_RES = \
-    1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13
+# (6, 7 and 12 -- sweep_order, sweep_pf, lp_il -- were retired in ABI 5)
+TUNE_GEMM_CFG, TUNE_GEMM_BK, TUNE_LP_CFG, TUNE_S3_CFG, TUNE_S3_STAGGER, \
+    TUNE_SWEEP_MF16, TUNE_SWEEP_IL, TUNE_CONV_IL, TUNE_HALO_MF, TUNE_S3_CFG_RES = \
+    1, 2, 3, 4, 5, 8, 9, 10, 11, 13
 
 _lib = None
 _lock = threading.RLock()

@@ -62,8 +62,7 @@ __global__ __launch_bounds__(512, 1) void gemm_8p_kernel(GemmArgs g, int tiles_n
 
   // XCD-aware block -> tile order (rr_internal.hpp tile_coords)
   int tm, tn;
-  if (!tile_coords(g.tile_order, blockIdx.x, gridDim.x, (g.M + 255) / 256, tiles_n, tm, tn))
-    return;  // a padding block of a reordered grid, before any barrier
+  tile_coords(blockIdx.x, gridDim.x, tiles_n, tm, tn);
   const int m0 = tm * 256, n0 = tn * 256;
   const int nk = g.K / EPR;  // even (K % (2 EPR) == 0, checked on the host)
 
@@ -351,7 +350,7 @@ bool gemm_8p_eligible(const GemmArgs& g, int dt) {
 
 hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s, int dt) {
   const long long tiles_m = (g.M + 255) / 256, tiles_n = (g.N + 255) / 256;
-  const long long nblk = tile_grid(g.tile_order, tiles_m, tiles_n);
+  const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
   if (emode == E_FILTER && dt == DT_FP8)

@@ -101,12 +101,6 @@ __device__ __forceinline__ void interleave2() {
 // 16x16 shape holds a higher clock on random operands, MI355X_MICROARCH.md
 // 'DVFS give-back' item 7).  Register r of tile (i, j) then maps through
 // acc_row / acc_col<true> (gemm_epilogue.hpp) instead of the 32x32 map.
-// PF (LDS-DMA, non-MF16 tiles, EMODE != E_STORE; the long-K gallery sweeps):
-// the A rows' (gallery's) 128-B line of k-tile kt + 2 is touched by one
-// 4-byte LDS-DMA per row into a dummy LDS word while tile kt computes, so
-// the HBM fetch has two k-tiles of lead time and the real DMA of kt + 2 hits
-// L2; that DMA stays in flight across the k-tile's barrier (counted vmcnt and
-// a raw s_barrier instead of __syncthreads' vmcnt(0)).
 // IL (LDS-DMA bf16 filter sweeps): the next k-tile's DMA is not issued as one
 // burst at the top of the k-tile but chunk by chunk among the first SPAN
 // MFMAs (18 of 40 on 32x32x16, 36 of 80 on 16x16x32): a burst of 9
@@ -114,7 +108,7 @@ __device__ __forceinline__ void interleave2() {
 // and stalls the waves' MFMAs behind it (tools/fetch_ceiling.hip, r04e:
 // 0.481 -> 0.525 of peak on the bare 32x32x16 sweep loop).
 template <int WM, int WN, int FM, int FN, int AMODE, int EMODE, int BK, int DT, int MINB, int GL, int MF16 = 0,
-          int EPI = -1, int PF = 0, int IL = 0>
+          int EPI = -1, int IL = 0>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, int tiles_n) {
   using ET = typename ElemT<DT>::T;
   static_assert(!MF16 || DT == DT_BF16, "MF16: bf16 only");
@@ -133,10 +127,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for block");
   static_assert(BM % ROWS_PER_PASS == 0 && BN % ROWS_PER_PASS == 0, "staging passes must tile the block");
   constexpr int BUF = (BM + BN) * BK;  // floats per LDS buffer
-  static_assert(!PF || (GL && !MF16 && EMODE != E_STORE), "PF: LDS-DMA sweep tiles");
   // EP_LNFOLD: the tile's rows' LayerNorm (mean, rstd) beside the stages
   constexpr bool LNF = EPI >= 0 && (EPI & EP_LNFOLD) != 0;
-  __shared__ __attribute__((aligned(16))) float lds[2 * BUF + (PF ? 64 : 0) + (LNF ? 2 * BM : 0)];
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF + (LNF ? 2 * BM : 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -145,8 +138,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
 
   // XCD-aware block -> tile order (rr_internal.hpp tile_coords)
   int tm, tn;
-  if (!tile_coords(g.tile_order, blockIdx.x, gridDim.x, (g.M + BM - 1) / BM, tiles_n, tm, tn))
-    return;  // a padding block of a reordered grid, before any barrier
+  tile_coords(blockIdx.x, gridDim.x, tiles_n, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   const int slot = tid % SLOTS;
@@ -296,7 +288,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   // IL: chunk c (A rows, then B rows) of glds_tile(kt, buf), due before MFMA
   // number idx; past the last k-tile it re-fetches the last one (an L2 hit)
   // into the drained buffer, so every iteration issues the same DMAs
-  static_assert(!IL || (GL && DT != DT_F32 && !PF && (MF16 == 1 || EMODE == E_FILTER)),
+  static_assert(!IL || (GL && DT != DT_F32 && (MF16 == 1 || EMODE == E_FILTER)),
                 "IL: LDS-DMA bf16 / fp8 filter sweeps, or the PIPE16 tiles");
   constexpr int NCH = A_CH + B_CH;
   // (PIPE16: the chunks go among the last k-step's MFMAs, one every
@@ -475,21 +467,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     if constexpr (IL) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the last spread DMA
     __syncthreads();  // every wave's last reads done: the epilogue reuses the LDS
   } else {
-  // PF: waves 0 .. BM/64 - 1 each touch 64 A rows (one per lane)
-  const ET* pf_src = reinterpret_cast<const ET*>(g.A) +
-                     (long long)min(m0 + (PF ? (wave % (BM / 64)) * 64 + lane : 0), g.M - 1) * g.lda + koff;
-  const bool pf_wave = PF && wave < BM / 64;
-  auto prefetch = [&](int kt) {
-    if constexpr (PF) {
-      if (pf_wave && kt < nk)
-        __builtin_amdgcn_global_load_lds((const void*)(pf_src + (long long)kt * EPR),
-                                         (__attribute__((address_space(3))) void*)(lds + 2 * BUF), 4, 0, 0);
-    }
-  };
   if constexpr (GL) {
     glds_tile(0, 0);
     __syncthreads();
-    prefetch(1);
   } else {
     load_tile(0);
     store_tile(0);
@@ -502,7 +482,6 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
       if constexpr (GL) glds_tile(kt + 1, cur ^ 1);
       else load_tile(kt + 1);
     }
-    prefetch(kt + 2);
     const float* la = lds + cur * BUF;
     const float* lb = la + BM * BK;
     if constexpr (DT == DT_F32) {
@@ -690,19 +669,8 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
     if constexpr (!GL) {
       if (kt + 1 < nk) store_tile(cur ^ 1);
     }
-    if constexpr (PF) {
-      // every DMA of tile kt + 1 has landed; only this iteration's prefetch
-      // (the wave's youngest VMEM op) may still be in flight
-      if (pf_wave && kt + 2 < nk) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-    } else {
-      __syncthreads();  // with GL: also the vmcnt(0) that retires the DMA
-    }
+    __syncthreads();  // with GL: also the vmcnt(0) that retires the DMA
   }
-  if constexpr (PF) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if constexpr (MF16) {
 #pragma unroll
@@ -836,16 +804,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
 }
 
 template <int WM, int WN, int FM, int FN, int AM, int EM, int BK, int DT, int MINB, int GL = 0, int MF16 = 0,
-          int EPI = -1, int PF = 0, int IL = 0>
+          int EPI = -1, int IL = 0>
 static hipError_t launch_t1(const GemmArgs& g, hipStream_t s) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
   const long long tiles_m = (g.M + BM - 1) / BM;
   const long long tiles_n = (g.N + BN - 1) / BN;
-  const long long nblk = tile_grid(g.tile_order, tiles_m, tiles_n);
+  const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
   const unsigned splits = g.k_split > 0 ? (unsigned)((g.K + g.k_split - 1) / g.k_split) : 1u;
-  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EPI, PF, IL>), dim3((unsigned)nblk, splits),
+  hipLaunchKernelGGL((gemm_kernel<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EPI, IL>), dim3((unsigned)nblk, splits),
                      dim3(64 * WM * WN), 0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
@@ -858,28 +826,28 @@ static hipError_t launch_t(const GemmArgs& g, hipStream_t s) {
   if constexpr (EM == E_STORE && DT == DT_BF16) {
     switch (ep_flags(g)) {
       case EP_BIAS | EP_BF16:
-        return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_BF16, 0, IL>(g, s);
-      case EP_BIAS | EP_RES: return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_RES, 0, IL>(g, s);
+        return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_BF16, IL>(g, s);
+      case EP_BIAS | EP_RES: return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_RES, IL>(g, s);
       case EP_BIAS | EP_GELU | EP_BF16:
-        return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_GELU | EP_BF16, 0, IL>(g, s);
+        return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_GELU | EP_BF16, IL>(g, s);
       default: break;
     }
     // the ViT LayerNorm fold (256-column tiles only; rr_linear_bf16_ln forces lp_cfg 3)
     if constexpr (32 * FN * WN == 256 && MF16 == 1) {
       switch (ep_flags(g)) {
         case EP_BIAS | EP_RES | EP_STATS:
-          return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_RES | EP_STATS, 0, IL>(g, s);
+          return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_RES | EP_STATS, IL>(g, s);
         case EP_BIAS | EP_BF16 | EP_LNFOLD:
-          return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_BF16 | EP_LNFOLD, 0, IL>(g, s);
+          return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_BF16 | EP_LNFOLD, IL>(g, s);
         case EP_BIAS | EP_GELU | EP_BF16 | EP_LNFOLD:
-          return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_GELU | EP_BF16 | EP_LNFOLD, 0,
+          return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, EP_BIAS | EP_GELU | EP_BF16 | EP_LNFOLD,
                            IL>(g, s);
         default: break;
       }
     }
     if (g.stats_out != nullptr || g.stats_in != nullptr) return hipErrorInvalidValue;
   }
-  return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, -1, 0, IL>(g, s);
+  return launch_t1<WM, WN, FM, FN, AM, EM, BK, DT, MINB, GL, MF16, -1, IL>(g, s);
 }
 
 // k-tile depth.  Measured on MI355X (same device, interleaved A/B): BK = 16
@@ -987,18 +955,10 @@ static hipError_t launch_lp_cfg(const GemmArgs& g, hipStream_t s, int cfg);
 template <int EM, int DT>
 static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s::Tuning& tu) {
   constexpr int EPR = DT == DT_BF16 ? 64 : 128;  // elements per 128-B k-tile row
-  if constexpr (EM == E_FILTER && DT != DT_F32) {
-    if (tu.lp_cfg == 6 && sweep_v_eligible(g, DT)) return launch_sweep_v(g, s, DT);
-  }
   int cfg = pick_lp(g, EM, DT == DT_BF16, tu);
   if (g.stats_out != nullptr || g.stats_in != nullptr) cfg = 3;  // the LayerNorm fold: 256-column tiles
   if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles
   if constexpr (EM == E_FILTER) {
-    // panel-grouped XCD order for the filter sweeps (tile_coords), when the
-    // picked tile's query panels split evenly into the groups
-    const int ord = tu.sweep_order < 0 ? 0 : tu.sweep_order;
-    const int bn = (cfg == 4 && DT == DT_BF16) ? 320 : (cfg >= 3 ? 256 : (cfg == 2 ? 64 : 128));
-    const long long tn = ((long long)g.N + bn - 1) / bn;
     // the 256x320 bf16 tile's default: v_mfma_f32_32x32x16_bf16 with the next
     // k-tile's DMA spread among the MFMAs (sweep_il).  On the C3 bench's own
     // descriptors (tools/e2e_ab.py, profiles/r04j_e2e_ab.txt): 7.15 -> 6.81
@@ -1006,18 +966,11 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
     // it won on synthetic near-parallel queries (r04f_sweep_il_ab.txt).
     // Bit-identical rankings in every form.
     GemmArgs g2 = g;
-    if (ord > 0 && tn % ord == 0) g2.tile_order = ord;
-    g2.l2_prefetch = tu.sweep_pf > 0;
     g2.mf16_sweep = tu.sweep_mf16 > 0;
     // (sweep_il = 1 spreads every filter sweep's DMA, the 256x256 bf16 one
     // too; the default: the 256x320 bf16 and the fp8 sweeps -- C5's fp8
     // sweeps 7.70 -> 7.53 ms per step on the bench, profiles/r04k_c5_*.json)
     g2.issue_spread = tu.sweep_il > 0 || (tu.sweep_il < 0 && ((cfg == 4 && DT == DT_BF16) || DT == DT_FP8));
-    return launch_lp_cfg<EM, DT>(g2, s, cfg);
-  }
-  if (tu.lp_il > 0) {  // the 256x256 bf16 tile of the stored-C / score GEMMs (ViT linears)
-    GemmArgs g2 = g;
-    g2.issue_spread = 1;
     return launch_lp_cfg<EM, DT>(g2, s, cfg);
   }
   return launch_lp_cfg<EM, DT>(g, s, cfg);
@@ -1035,18 +988,18 @@ static hipError_t launch_lp_cfg(const GemmArgs& g, hipStream_t s, int cfg) {
   switch (cfg) {
     case 2: return launch_t<4, 1, 2, 2, A_DENSE, EM, 32, DT, 2, 0, MF>(g, s);
     case 3:
-      // (the next k-tile's DMA spread among the MFMAs: lp_il for the bf16
-      // stored-C tile, sweep_il for the fp8 filter sweeps)
-      if constexpr (DT == DT_BF16 || (DT == DT_FP8 && EM == E_FILTER)) {
+      // (the next k-tile's DMA spread among the MFMAs: sweep_il, the filter
+      // sweeps; on the ViT linears' stored-C tile it made the C4 embed slower,
+      // 61.3 -> 62.4 ms, profiles/r04k_e2e_c4_il.txt, and was removed)
+      if constexpr (EM == E_FILTER && DT != DT_F32) {
         if (g.issue_spread) return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF, 1>(g, s);
       }
       return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);
     case 4:  // bf16 sweeps only (fp8: the 256x256 tile; its 256x320 form spills the dequantisation)
       if constexpr (EM == E_FILTER && DT == DT_BF16) {
-        if (g.l2_prefetch) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0, -1, 1>(g, s);
-        if (g.mf16_sweep && g.issue_spread) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 2, -1, 0, 1>(g, s);
+        if (g.mf16_sweep && g.issue_spread) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 2, -1, 1>(g, s);
         if (g.mf16_sweep) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 2>(g, s);
-        if (g.issue_spread) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0, -1, 0, 1>(g, s);
+        if (g.issue_spread) return launch_t1<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0, -1, 1>(g, s);
       }
       if constexpr (EM != E_STORE && DT == DT_BF16) return launch_t<4, 2, 2, 5, A_DENSE, EM, 32, DT, 1, 1, 0>(g, s);
       else if constexpr (EM != E_STORE) return launch_t<2, 4, 4, 2, A_DENSE, EM, 32, DT, 1, 1, MF>(g, s);

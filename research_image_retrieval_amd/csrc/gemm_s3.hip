@@ -2233,10 +2233,11 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
       // conv_il (opt-in): every R101 layer the 256x256 tile serves ran 1-3 %
       // faster alone at 1280 images (256->1024 0.681 -> 0.668 ms; profiles/
       // r04g_h2_cfg_il.txt, r04h_h2_cfg_il.txt), but the bench's whole embed
-      // ran 0.5 % slower with it (71.77 -> 72.11 ms, r04j_e2e_ab.txt)
-      // (conv_il 2: only the GEMMs without a residual epilogue)
+      // ran 0.5 % slower with it (71.77 -> 72.11 ms, r04j_e2e_ab.txt; limited
+      // to the GEMMs without a residual, 1.0 % slower, r04s_e2e_conv_il.txt).
+      // It also selects the halo tile's 16x16x32 form with its B DMA spread.
       GemmArgs g2 = g;
-      g2.issue_spread = h->tune.conv_il == 1 || (h->tune.conv_il == 2 && g.residual == nullptr);
+      g2.issue_spread = h->tune.conv_il == 1;
       g2.halo_mf = h->tune.halo_mf;
       e = amode == A_DENSE ? launch_h2_am<A_DENSE>(g2, s, f, n_cu, st)
           : amode == A_CONV ? launch_h2_am<A_CONV>(g2, s, f, n_cu, st)

@@ -139,7 +139,7 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.gemm_bk = value;
       return RR_OK;
     case RR_TUNE_LP_CFG:
-      if (value < 0 || value > 6) break;
+      if (value < 0 || value > 5) break;
       h->tune.lp_cfg = value;
       return RR_OK;
     case RR_TUNE_S3_CFG:
@@ -150,14 +150,6 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       if (value < -1 || value > 200) break;
       h->tune.s3_stagger = value;
       return RR_OK;
-    case RR_TUNE_SWEEP_ORDER:
-      if (!in({-1, 0, 2, 4, 8})) break;
-      h->tune.sweep_order = value;
-      return RR_OK;
-    case RR_TUNE_SWEEP_PF:
-      if (!in({-1, 0, 1})) break;
-      h->tune.sweep_pf = value;
-      return RR_OK;
     case RR_TUNE_SWEEP_MF16:
       if (!in({-1, 0, 1})) break;
       h->tune.sweep_mf16 = value;
@@ -167,16 +159,12 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.sweep_il = value;
       return RR_OK;
     case RR_TUNE_CONV_IL:
-      if (!in({-1, 0, 1, 2})) break;
+      if (!in({-1, 0, 1})) break;
       h->tune.conv_il = value;
       return RR_OK;
     case RR_TUNE_HALO_MF:
       if (!in({-1, 0, 1})) break;
       h->tune.halo_mf = value;
-      return RR_OK;
-    case RR_TUNE_LP_IL:
-      if (!in({-1, 0, 1})) break;
-      h->tune.lp_il = value;
       return RR_OK;
     case RR_TUNE_S3_CFG_RES:
       if (value < 0 || value > 14) break;
@@ -378,9 +366,11 @@ int rr_linear_bf16_ln(rr_handle_t h, const void* x, int m, int k, const void* w,
     return set_error(h, RR_EINVAL, "rr_linear_bf16_ln: exactly one of stats_in (fold) and stats_out (produce)");
   if (stats_out) {
     // the producer: the residual GEMM (fp32 output) writing the bf16 copy and the partials
-    if (!xb_out || !residual || !bias || act != 0 || out_bf16 || (n % 256) || ((uintptr_t)xb_out & 15) ||
+    // (k % 64: the 256x256 tile with the partials epilogue stages whole 64-deep k-tiles)
+    if (!xb_out || !residual || !bias || act != 0 || out_bf16 || (n % 256) || (k % 64) || ((uintptr_t)xb_out & 15) ||
         ((uintptr_t)stats_out & 7))
-      return set_error(h, RR_EINVAL, "rr_linear_bf16_ln: stats_out needs bias, residual, fp32 output, n % 256 == 0");
+      return set_error(h, RR_EINVAL,
+                       "rr_linear_bf16_ln: stats_out needs bias, residual, fp32 output, n % 256 == 0, k % 64 == 0");
   } else {
     // the consumer: bias, bf16 output, K in whole 64-deep k-tiles
     if (!colsum || !bias || residual || !out_bf16 || (k % 64) || (n & 3) || ((uintptr_t)colsum & 15) ||

@@ -13,21 +13,19 @@
 struct rr_handle_s {
   int device = 0;
   std::string last_error;
-  // kernel-config overrides (rr_set_tuning; 0 = the built-in pick): tests
-  // and tools force each tile config through these, the product path never does
+  // kernel-config overrides (rr_set_tuning): tests and tools force each tile
+  // config through these; the product path never sets them, and their
+  // defaults (0 / -1) select the library's own picks
   struct Tuning {
     int gemm_cfg = 0;  // fp32 core: 22, 41 or 88
     int gemm_bk = 0;   // fp32 core k-tile depth: 16 or 32
-    int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 / fp8 sweeps), 6 = gallery-in-VGPR bf16 / fp8 filter sweep (sweep_v.hip)
-    int s3_cfg = 0;    // split cores: 1..13 (gemm_s3.hip tile table; 9-13 f16x2 only)
+    int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 / fp8 sweeps)
+    int s3_cfg = 0;    // split cores: 1..14 (gemm_s3.hip tile table; 9-14 f16x2 only)
     int s3_stagger = -1;  // split-bf16 core round stagger in ~1 us sleeps (-1: the library's pick)
-    int sweep_order = -1;  // bf16 / fp8 filter sweeps: block -> tile order (tile_coords); -1: the library's pick
-    int sweep_pf = -1;     // bf16 256x320 filter sweep: L2 prefetch of the gallery two k-tiles ahead; -1: the pick
     int sweep_mf16 = -1;   // bf16 256x320 filter sweep on v_mfma_f32_16x16x32_bf16 (1) or 32x32x16 (0); -1: the pick (0)
     int sweep_il = -1;     // bf16 256x320 filter sweep: next k-tile's DMA spread among the MFMAs (1) or one burst (0); -1: the pick (1)
-    int conv_il = -1;      // f16x2 256x256 conv tile (s3_cfg 12): next k-tiles' loads spread among the MFMAs (1) or one burst (0); -1: the pick (0)
+    int conv_il = -1;      // f16x2 256x256 conv tile (s3_cfg 12) and halo 16x16x32 tile: next k-tiles' loads spread among the MFMAs (1) or one burst (0); -1: the pick (0)
     int halo_mf = -1;      // f16x2 halo 3x3 tiles on v_mfma_f32_16x16x32_f16 (1) or 32x32x16 (0); -1: the pick (the 256x256 tile 1, the others 0)
-    int lp_il = -1;        // bf16 256x256 stored-C / score tile (the ViT linears): next k-tile's DMA spread among the MFMAs (1) or one burst (0); -1: the pick (0)
     int s3_cfg_res = 0;    // split cores: forced tile config for the GEMMs with a residual epilogue only (0: s3_cfg's)
   } tune;
   int n_cu = 0;  // compute units of the handle's device (device_cu_count)
@@ -239,28 +237,12 @@ struct GemmArgs {
   const float* colsum = nullptr;
   int stats_k = 0;
   float ln_eps = 0.f;
-  // block -> tile order of the low-precision filter sweeps (tile_coords)
-  int tile_order = 0;
-  // the 256x320 bf16 filter sweep's L2 prefetch of A (gemm_kernel PF), and
-  // its 16x16x32 MFMA form (gemm_kernel MF16 = 2)
-  int l2_prefetch = 0;
+  // the 256x320 bf16 filter sweep's 16x16x32 MFMA form (gemm_kernel MF16 = 2)
   int mf16_sweep = 0;
   int issue_spread = 0;
   int halo_mf = -1;
 };
 
-// Block -> (tm, tn) of a tiles_m x tiles_n grid (tm: A / gallery-row tiles,
-// tn: B / query-panel tiles).  Blocks b, b + 8, ... share an XCD (dispatch is
-// round-robin over the 8 XCDs; used for speed only, never for correctness).
-// order 0: the bijective XCD remap: each XCD a contiguous range of tile ids,
-//   tn fastest (an XCD sweeps its rows against every panel).
-// order NP (2, 4 or 8, tiles_n % NP == 0): the 8 XCD slots are NP panel
-//   groups x 8 / NP row ranges; slot x sweeps rows [(x / NP) R, +R) against
-//   panels (x % NP) tiles_n / NP .. +tiles_n / NP - 1, R = ceil(tiles_m NP / 8):
-//   an XCD keeps tiles_n / NP panels L2-resident, and the NP slots of a row
-//   range stream the same rows at about the same time.  The grid is
-//   tile_grid(...) blocks; the padding blocks get false (exit before any
-//   barrier).
 // 64-lane sum, returned wave-uniform: DPP row_shr 1/2/4/8 sums each 16-lane
 // row into its lane 15 (out-of-row sources read 0), then the four rows'
 // lanes 15, 31, 47, 63 are added in that order.  VALU-only (no LDS
@@ -278,24 +260,17 @@ __device__ __forceinline__ float wave_sum(float x) {
          (__int_as_float(__builtin_amdgcn_readlane(xi, 47)) + __int_as_float(__builtin_amdgcn_readlane(xi, 63)));
 }
 
-__host__ __device__ inline long long tile_grid(int order, long long tiles_m, long long tiles_n) {
-  if (order <= 0) return tiles_m * tiles_n;
-  const long long nr = 8 / order, r = (tiles_m + nr - 1) / nr;
-  return 8 * r * (tiles_n / order);
-}
-__device__ __forceinline__ bool tile_coords(int order, int bid, int nwg, int tiles_m, int tiles_n, int& tm, int& tn) {
-  if (order <= 0) {
-    const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-    tn = wgid % tiles_n;
-    tm = wgid / tiles_n;
-    return true;
-  }
-  const int nr = 8 / order, tpg = tiles_n / order, x = bid & 7, j = bid >> 3;
-  const int r = (tiles_m + nr - 1) / nr;
-  tm = (x / order) * r + j / tpg;
-  tn = (x % order) * tpg + j % tpg;
-  return tm < tiles_m;
+// Block -> (tm, tn) of a tiles_m x tiles_n grid, the bijective XCD remap:
+// blocks b, b + 8, ... share an XCD (dispatch is round-robin over the 8 XCDs;
+// used for speed only, never for correctness), and each XCD gets a contiguous
+// range of tile ids, tn fastest (an XCD sweeps its rows against every panel).
+// (Round 4 measured panel-grouped orders on the filter sweeps: +-1 %, not kept,
+// profiles/r04b_sweep_order_ab.txt.)
+__device__ __forceinline__ void tile_coords(int bid, int nwg, int tiles_n, int& tm, int& tn) {
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  tn = wgid % tiles_n;
+  tm = wgid / tiles_n;
 }
 
 int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStream_t s, int timer_cls,
@@ -317,10 +292,6 @@ int launch_split2h(rr_handle_s* h, const float* w, int rows, int k, int kpad, ui
 // max |x| over x[n] into the RR_AMAX_SLOTS words at slots (atomic max)
 int launch_amax(rr_handle_s* h, const float* x, long long n, uint32_t* slots, hipStream_t s);
 
-// bf16 / fp8 filter sweep with the gallery in VGPRs (sweep_v.hip): dense A/B,
-// K % 32 (bf16) or % 128 (fp8) == 0, unscaled bf16 rows
-bool sweep_v_eligible(const GemmArgs& g, int dt);
-hipError_t launch_sweep_v(const GemmArgs& g, hipStream_t s, int dt);
 // 256x256 8-phase pipeline (gemm_8p.hip), bf16 or fp8 (16x16x128 block-scaled
 // MFMA): dense A/B, K a multiple of two k-tiles
 bool gemm_8p_eligible(const GemmArgs& g, int dt);

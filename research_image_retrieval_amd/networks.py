@@ -366,12 +366,18 @@ class VisionTransformer(_Extractor):
             # residual GEMMs' epilogues write the bf16 rows and the row
             # statistics, so no LayerNorm pass re-reads the fp32 stream
             xb, st = ops.ln_partials_bf16(x)
-            for blk in self.blocks:
+            for li, blk in enumerate(self.blocks):
                 qkv = ops.linear_bf16_ln_fold(xb, st, *blk["qkv.fold"])
                 a = ops.attention_bf16(qkv, b, self.seq, self.heads)
                 x, xb, st = ops.linear_bf16_ln_produce(a, blk["attn.out_proj.weight.bf16"], blk["attn.out_proj.bias"], x)
                 y = ops.linear_bf16_ln_fold(xb, st, *blk["fc.fold"], act=2)
-                x, xb, st = ops.linear_bf16_ln_produce(y, blk["mlp.c_proj.weight.bf16"], blk["mlp.c_proj.bias"], x)
+                if li + 1 < len(self.blocks):
+                    x, xb, st = ops.linear_bf16_ln_produce(y, blk["mlp.c_proj.weight.bf16"], blk["mlp.c_proj.bias"], x)
+                else:
+                    # the last block's output feeds only ln_post (fp32 CLS rows):
+                    # no bf16 copy or partials (they would be ~390 MB per
+                    # 1280-image step that nothing reads)
+                    x = ops.linear_bf16(y, blk["mlp.c_proj.weight.bf16"], blk["mlp.c_proj.bias"], residual=x)
             cls = ops.layernorm(x, *self.ln_post, rows=b, row_stride=self.seq * self.width)
             return ops.linear(cls, self.proj_t)
         for blk in self.blocks:

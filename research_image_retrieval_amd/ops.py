@@ -518,12 +518,11 @@ def topk_merge(part_scores, part_idx, k_out):
 
 
 _TUNE_KEYS = {"gemm_cfg": _lib.TUNE_GEMM_CFG, "gemm_bk": _lib.TUNE_GEMM_BK, "lp_cfg": _lib.TUNE_LP_CFG,
-              "s3_cfg": _lib.TUNE_S3_CFG, "s3_stagger": _lib.TUNE_S3_STAGGER, "sweep_order": _lib.TUNE_SWEEP_ORDER,
-              "sweep_pf": _lib.TUNE_SWEEP_PF, "sweep_mf16": _lib.TUNE_SWEEP_MF16,
+              "s3_cfg": _lib.TUNE_S3_CFG, "s3_stagger": _lib.TUNE_S3_STAGGER, "sweep_mf16": _lib.TUNE_SWEEP_MF16,
               "sweep_il": _lib.TUNE_SWEEP_IL, "conv_il": _lib.TUNE_CONV_IL,
-              "halo_mf": _lib.TUNE_HALO_MF, "lp_il": _lib.TUNE_LP_IL, "s3_cfg_res": _lib.TUNE_S3_CFG_RES}
-_TUNE_DEFAULT = {"s3_stagger": -1, "sweep_order": -1, "sweep_pf": -1, "sweep_mf16": -1, "sweep_il": -1,
-                 "conv_il": -1, "halo_mf": -1, "lp_il": -1}  # the library's own pick (0 elsewhere)
+              "halo_mf": _lib.TUNE_HALO_MF, "s3_cfg_res": _lib.TUNE_S3_CFG_RES}
+_TUNE_DEFAULT = {"s3_stagger": -1, "sweep_mf16": -1, "sweep_il": -1,
+                 "conv_il": -1, "halo_mf": -1}  # the library's own pick (0 elsewhere)
 
 
 class tuning:

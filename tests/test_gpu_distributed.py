@@ -13,7 +13,7 @@ import torch.multiprocessing as mp
 pytestmark = pytest.mark.gpu
 
 
-def _worker(rank, world, port, q_all, g_all, k, sizes, prefilter, out):
+def _worker(rank, world, port, q_all, g_all, k, sizes, prefilter, out, dtype="fp32"):
     import sys
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from research_image_retrieval_amd.distributed import ShardedGallery, shard_bounds
@@ -21,7 +21,7 @@ def _worker(rank, world, port, q_all, g_all, k, sizes, prefilter, out):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     dev = torch.device("cuda:0")
     lo, hi = shard_bounds(g_all.shape[0], world, rank)
-    sg = ShardedGallery(g_all[lo:hi].contiguous().to(dev), lo, prefilter=prefilter)
+    sg = ShardedGallery(g_all[lo:hi].contiguous().to(dev), lo, prefilter=prefilter, dtype=dtype)
     qlo = sum(sizes[:rank])
     s, i = sg.search(q_all[qlo:qlo + sizes[rank]].contiguous().to(dev), k)
     out[rank] = (s.cpu().numpy(), i.cpu().numpy())
@@ -52,6 +52,36 @@ def test_sharded_search_real_kernels_world2(prefilter):
     s_o, i_o = oracle.cosine_topk(q, g, k)
     assert np.array_equal(i, i_o) and np.array_equal(s, s_o)
     assert list(i[0, :2]) == [10, 60_000]
+
+
+@pytest.mark.parametrize("n,d", [(90_001, 512), (33_333, 256)])
+def test_sharded_search_bf16_real_kernels_world2(cuda, n, d):
+    """C4's N > 1 ranker: ShardedGallery(dtype="bf16") -- the all-gathered
+    queries quantised and swept against each rank's bf16 shard
+    (quantize_rows + cosine_topk_lp), the partial lists all-to-all'd and
+    merged -- equals GallerySearcher(dtype="bf16") on the whole gallery bit
+    for bit, with a tie planted across the shard boundary."""
+    from test_distributed_gloo import _free_port
+    from research_image_retrieval_amd.search import GallerySearcher
+    rs = np.random.RandomState(n + d)
+    q = rs.standard_normal((11, d)).astype(np.float32)
+    g = rs.standard_normal((n, d)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    g /= np.linalg.norm(g, axis=1, keepdims=True)
+    g[n - 7] = g[12]  # exact tie across the shard boundary
+    q[2] = g[12]
+    k = 100
+    sizes = [5, 6]
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_worker, args=(2, _free_port(), torch.from_numpy(q), torch.from_numpy(g), k, sizes, False,
+                                      out, "bf16"), nprocs=2, join=True, start_method="spawn")
+    s = np.concatenate([out[0][0], out[1][0]])
+    i = np.concatenate([out[0][1], out[1][1]])
+    srch = GallerySearcher(torch.from_numpy(g), device=cuda, normalize=False, dtype="bf16")
+    s_ref, i_ref = srch.topk(torch.from_numpy(q), k, normalize=False)
+    assert np.array_equal(i, i_ref.cpu().numpy()) and np.array_equal(s, s_ref.cpu().numpy())
+    assert list(i[2, :2]) == [12, n - 7]
 
 
 def _qe_worker(rank, world, port, q_all, g_all, k, sizes, dtype, out):

@@ -121,7 +121,7 @@ def test_conv2d_h2_vs_float64(cuda, b, h, w, cin, cout, k, s, p, res):
     es3 = _rel_err(y_s3[live], ref[live], scale[live])
     print(f"conv {b}x{h}x{w}x{cin}->{cout} k{k}s{s}: h2 max {eh2[0]:.3g} mean {eh2[1]:.3g} | "
           f"s3 max {es3[0]:.3g} mean {es3[1]:.3g} | f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
-    # mean error at or below the exact-fp32 core's; max within 1.25x of it: the
+    # mean error at most 1.05x the exact-fp32 core's (+1e-9); max within 1.25x of it: the
     # one-accumulator tiles the library picks for K >= 256, N % 256 == 0
     # (configs 10-12) round the a0b1 + a1b0 terms against the running sum, three
     # roundings per product instead of one, measured up to 1.2x the exact core's
@@ -169,7 +169,7 @@ def test_stem_h2_vs_float64(cuda, b, h, w):
     eh2 = _rel_err(y_h2[live], ref[live], scale[live])
     ef32 = _rel_err(y_f32[live], ref[live], scale[live])
     print(f"stem {b}x{h}x{w}: h2 max {eh2[0]:.3g} mean {eh2[1]:.3g} | f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
-    # mean error at or below the exact-fp32 core's; max within 1.25x of it: the
+    # mean error at most 1.05x the exact-fp32 core's (+1e-9); max within 1.25x of it: the
     # one-accumulator tiles the library picks for K >= 256, N % 256 == 0
     # (configs 10-12) round the a0b1 + a1b0 terms against the running sum, three
     # roundings per product instead of one, measured up to 1.2x the exact core's

@@ -145,23 +145,6 @@ def test_prefilter_query_panels_of_256(cuda, nq):
     assert i[3, 0] == 77_777
 
 
-@pytest.mark.parametrize("nq,n,d", [(1280, 70_001, 2048), (300, 50_000, 256), (17, 9_999, 512)])
-def test_prefilter_gallery_in_vgpr_sweep(cuda, nq, n, d):
-    """The gallery-in-VGPR bf16 filter sweep (sweep_v.hip, lp_cfg 6: 256x256
-    blocks, query panel in LDS) inside the prefilter ranker: bit-identical to
-    the exhaustive fp32 ranker on ragged gallery tiles, padded query panels
-    and a planted exact match."""
-    rs = np.random.RandomState(nq + n)
-    g = rs.standard_normal((n, d)).astype(np.float32)
-    q = rs.standard_normal((nq, d)).astype(np.float32)
-    g[n - 1] = q[nq - 1]
-    g /= np.linalg.norm(g, axis=1, keepdims=True)
-    q /= np.linalg.norm(q, axis=1, keepdims=True)
-    with ops.tuning(cuda.index, lp_cfg=6):
-        s, i = _prefilter_vs_exhaustive(cuda, q, g, 100)
-    assert i[nq - 1, 0] == n - 1
-
-
 def test_prefilter_bitexact_ties_and_clusters(cuda):
     """Exact ties (duplicate rows on both sides of the seed boundary), planted
     near-duplicates, and a dense cluster where thousands of rows score within
@@ -294,59 +277,6 @@ def test_bounded_workspace_overflow_recovery(cuda):
     s3, i3 = ops.cosine_topk_lp(qb, None, gb, None, k, "bf16")
     s4, i4 = ops.cosine_topk_lp(qb, None, gb, None, k, "bf16", max_workspace_bytes=budget)
     assert torch.equal(i3, i4) and torch.equal(s3, s4)
-
-
-@pytest.mark.parametrize("order", [2, 4, 8])
-def test_prefilter_sweep_tile_orders_bit_identical(cuda, order):
-    """The filter sweep's panel-grouped XCD block orders (rr_set_tuning
-    sweep_order; 8 does not divide 4 panels of 320 and falls back to the
-    default): the same bits as the default order, with a ragged last gallery
-    tile and planted matches in the first and last rows."""
-    rs = np.random.RandomState(order)
-    d, nq, n = 2048, 1280, 90_001
-    g = rs.standard_normal((n, d)).astype(np.float32)
-    q = rs.standard_normal((nq, d)).astype(np.float32)
-    g[0], g[n - 1] = q[5], q[nq - 1]
-    g /= np.linalg.norm(g, axis=1, keepdims=True)
-    q /= np.linalg.norm(q, axis=1, keepdims=True)
-    qd, gd = torch.from_numpy(q).to(cuda), torch.from_numpy(g).to(cuda)
-    gbf, _ = ops.quantize_rows(gd, "bf16")
-    bound = ops.prefilter_gallery_bound(gd, gbf)
-    s0, i0 = ops.cosine_topk_prefilter(qd, gd, gbf, bound, 100)
-    with ops.tuning(cuda.index, sweep_order=order):
-        s1, i1 = ops.cosine_topk_prefilter(qd, gd, gbf, bound, 100)
-        # the bf16 / fp8 lp rankers' filter sweeps take the same orders
-        for dt in ("bf16", "fp8"):
-            ql, qs = ops.quantize_rows(qd, dt)
-            gl, gs = ops.quantize_rows(gd, dt)
-            with ops.tuning(cuda.index, sweep_order=0):
-                a = ops.cosine_topk_lp(ql, qs, gl, gs, 100, dt)
-            b = ops.cosine_topk_lp(ql, qs, gl, gs, 100, dt)
-            assert torch.equal(a[1], b[1]) and torch.equal(a[0], b[0]), dt
-    assert torch.equal(i0, i1) and torch.equal(s0.view(torch.int32), s1.view(torch.int32))
-    assert int(i1[5, 0]) == 0 and int(i1[nq - 1, 0]) == n - 1
-
-
-def test_prefilter_sweep_l2_prefetch_bit_identical(cuda):
-    """The 256x320 bf16 sweep with the gallery's L2 prefetch two k-tiles
-    ahead (rr_set_tuning sweep_pf; DMA in flight across the raw barrier):
-    the same bits as without, ragged last tile, planted matches."""
-    rs = np.random.RandomState(77)
-    d, nq, n = 2048, 1280, 70_001
-    g = rs.standard_normal((n, d)).astype(np.float32)
-    q = rs.standard_normal((nq, d)).astype(np.float32)
-    g[3], g[n - 1] = q[0], q[nq - 1]
-    g /= np.linalg.norm(g, axis=1, keepdims=True)
-    q /= np.linalg.norm(q, axis=1, keepdims=True)
-    qd, gd = torch.from_numpy(q).to(cuda), torch.from_numpy(g).to(cuda)
-    gbf, _ = ops.quantize_rows(gd, "bf16")
-    bound = ops.prefilter_gallery_bound(gd, gbf)
-    out = {}
-    for pf in (0, 1):
-        with ops.tuning(cuda.index, sweep_pf=pf):
-            out[pf] = ops.cosine_topk_prefilter(qd, gd, gbf, bound, 100)
-    assert torch.equal(out[0][1], out[1][1]) and torch.equal(out[0][0].view(torch.int32), out[1][0].view(torch.int32))
-    assert int(out[1][1][0, 0]) == 3 and int(out[1][1][nq - 1, 0]) == n - 1
 
 
 @pytest.mark.parametrize("il", [0, 1])

@@ -35,6 +35,11 @@ def _rccl_worker(rank, port, q, g, k, out):
         s2, i2 = sg.search(qd, k, counts=[nq])
         res[f"search_pre{int(pre)}"] = bool(torch.equal(i1, i0) and torch.equal(s1, s0) and torch.equal(i2, i0)
                                             and torch.equal(s2, s0))
+    # C4's ranker: the bf16 shard (quantize_rows + cosine_topk_lp inside search)
+    sg = ShardedGallery(gd, 0, dtype="bf16")
+    s5, i5 = sg.search(qd, k, counts=[nq])
+    s6, i6 = GallerySearcher(g, device=dev, normalize=False, dtype="bf16").topk(q, k, normalize=False)
+    res["search_bf16"] = bool(torch.equal(i5, i6) and torch.equal(s5, s6))
     # rows of the global gallery by index, padding slots (-1) zero
     sg = ShardedGallery(gd, 0)
     idx = torch.tensor([[0, -1, g.shape[0] - 1]] * nq, dtype=torch.int64, device=dev)
@@ -53,6 +58,9 @@ def _rccl_worker(rank, port, q, g, k, out):
 
 
 def test_sharded_path_over_rccl_world1():
+    """fp32 / prefilter / bf16 sharded search, gather_rows and the fp8 / fp32
+    alpha-QE re-search over RCCL on a world of one: each equals the
+    single-GPU path bit for bit."""
     from test_distributed_gloo import _free_port
     rs = np.random.RandomState(17)
     d = 256

@@ -108,7 +108,7 @@ def test_f32_core_every_tile_config(cuda, cfg, bk, mode):
     _check(y, ref, scale, 2e-6)
 
 
-@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("cfg", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("dtype", ["bf16", "fp8"])
 def test_lowp_every_tile_config(cuda, cfg, dtype):
     """bf16 / fp8 linears (stored C) and filter sweeps (top-k) on every config:

@@ -139,34 +139,6 @@ def test_vit_bf16_linear_bf16_qkv_matches_fp32_qkv(cuda):
     assert torch.equal(a32, a16)
 
 
-@pytest.mark.parametrize("m,k,n,kind", [
-    (1280 * 197 // 8, 768, 2304, "qkv"),       # bias -> bf16, a few hundred 256x256 tiles
-    (3 * 197 + 5, 768, 768, "res"),            # bias + residual, ragged M
-    (2 * 197, 768, 3072, "gelu"),              # bias + QuickGELU -> bf16
-    (2 * 197, 3072, 768, "res"),               # long K (48 k-tiles)
-])
-def test_linear_bf16_issue_spread_bit_identical(cuda, m, k, n, kind):
-    """lp_il: the bf16 256x256 tile with each k-tile's LDS-DMA spread among the
-    MFMAs after its barrier computes the same products in the same order as
-    with one burst: identical bits on the ViT linears' epilogues."""
-    g = torch.Generator().manual_seed(m + n)
-    x = torch.randn(m, k, generator=g).bfloat16().to(cuda)
-    w = (torch.randn(n, k, generator=g) / k ** 0.5).bfloat16().to(cuda)
-    bias = torch.randn(n, generator=g).to(cuda)
-    r = torch.randn(m, n, generator=g).to(cuda) if kind == "res" else None
-    outs = {}
-    for il in (0, 1):
-        with ops.tuning(cuda.index, lp_cfg=3, lp_il=il):
-            if kind == "qkv":
-                outs[il] = ops.linear_bf16(x, w, bias, out_bf16=True)
-            elif kind == "gelu":
-                outs[il] = ops.linear_bf16(x, w, bias, act=2, out_bf16=True)
-            else:
-                outs[il] = ops.linear_bf16(x, w, bias, residual=r)
-    assert torch.equal(outs[0].view(torch.int16) if outs[0].dtype == torch.bfloat16 else outs[0].view(torch.int32),
-                       outs[1].view(torch.int16) if outs[1].dtype == torch.bfloat16 else outs[1].view(torch.int32))
-
-
 def test_ln_partials_and_produce_epilogue(cuda):
     """The LayerNorm fold's producer side: rr_ln_partials_bf16 and the residual
     GEMM's EP_STATS epilogue give bf16(y) exactly and per-tile (mean, M2)

@@ -1,10 +1,10 @@
 """Interleaved A/B of the exact prefilter ranker's bf16 filter sweep configs
-(rr_set_tuning lp_cfg: 0 = the pick, 6 = sweep_v.hip; or, with PF_KEY=sweep_order,
-the block -> tile orders 0 / 2 / 4 / 8) on the C3 shape
+(rr_set_tuning lp_cfg: 0 = the pick, 4 / 5 forced; or another key with PF_KEY, e.g.
+sweep_il / sweep_mf16) on the C3 shape
 (Q queries x 1.6 M x 2048, top-100): the sweep launch's HIP-event time, its
 fraction of the bf16 dense peak, and the whole ranker's results compared bit
 for bit between configs.
-usage: [PF_KEY=lp_cfg|sweep_order|...] [PF_EXTRA="key=value ..."] PF_CFGS="0 6" PF_Q=1280
+usage: [PF_KEY=lp_cfg|sweep_il|...] [PF_EXTRA="key=value ..."] PF_CFGS="0 5" PF_Q=1280
        python tools/prefilter_ab.py"""
 import json
 import os
@@ -19,7 +19,7 @@ from research_image_retrieval_amd import _lib, ops  # noqa: E402
 
 dev = torch.device("cuda:0")
 Q = int(os.environ.get("PF_Q", "1280"))
-cfgs = [int(c) for c in os.environ.get("PF_CFGS", "0 6").split()]
+cfgs = [int(c) for c in os.environ.get("PF_CFGS", "0 5").split()]
 KEY = os.environ.get("PF_KEY", "lp_cfg")
 # fixed extra tuning for every config, e.g. PF_EXTRA="sweep_mf16=1"
 EXTRA = {kv.split("=")[0]: int(kv.split("=")[1]) for kv in os.environ.get("PF_EXTRA", "").split()}
