@@ -371,6 +371,30 @@ int rr_bottleneck_out_h2(rr_handle_t h, const float* y, const unsigned* y_amax,
                          const float* bias, int cout, float* out,
                          unsigned* out_amax, void* stream);
 
+/* The seam between two bottleneck blocks of a stage on the f16x2 core, as
+ * ONE launch: block i's conv3 with its residual and block i+1's conv1,
+ *   out = ReLU(y2 . W3^T + b3 + res)        [m][4 planes]  (block i's output)
+ *   h1  = ReLU(out . W1^T + b1)             [m][planes]    (block i+1's conv1)
+ * (torchvision Bottleneck / the reference's ResBlock + BottleneckTransform,
+ * networks/backbone.py:305-346), so block i's output is written once and
+ * never read back for the next conv1.  y2: block i's conv2 output [m][planes]
+ * with its max-|x| record y2_amax; res: block i's input [m][4 planes];
+ * w3 / w3_iscale: rr_split2_f16 of conv3's [4 planes][planes] weights; w1 /
+ * w1_iscale: rr_split2_f16 of the next conv1's [planes][4 planes]; b3 / b1
+ * may be NULL.  out_amax / h1_amax (optional, zeroed by the caller): the
+ * max-|x| records of out and h1.  planes = 64, 128 or 256; every pointer
+ * 16-byte aligned.  `out` equals rr_conv2d_h2's conv3 (+ residual, ReLU) bit
+ * for bit where that call runs its 256 x 256 one-accumulator tile (K >= 256);
+ * h1's A operand is split at the running max of each 128-row group's
+ * outputs instead of one scale per tensor, which rounds no differently except
+ * where it keeps more low bits (tests/test_gpu_seam.py).                     */
+int rr_bottleneck_seam_h2(rr_handle_t h, const float* y2, const unsigned* y2_amax,
+                          int m, int planes, const float* res, const void* w3,
+                          const float* w3_iscale, const float* b3, const void* w1,
+                          const float* w1_iscale, const float* b1, float* out,
+                          unsigned* out_amax, float* h1, unsigned* h1_amax,
+                          void* stream);
+
 /* The ResNet stem on the f16x2 core with its max-pool fused: NHWC4 conv
  * (cin == 4, as rr_conv2d_h2) + bias + ReLU, then the 3x3 stride-2 padding-1
  * max-pool, written only pooled: y_pool [b][ph][pw][64] with

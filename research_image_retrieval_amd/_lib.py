@@ -68,6 +68,8 @@ SIGNATURES = {
     "rr_stem_pool_h2": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
     "rr_bottleneck_out_h2": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _vp,
                                   _vp, _vp]),
+    "rr_bottleneck_seam_h2": (_i, [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp]),
     "rr_amax_f32": (_i, [_vp, _vp, _ll, _vp, _vp]),
     "rr_resize_bilinear": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _f, _f, _vp, _vp]),
     "rr_maxpool2d": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),

@@ -69,6 +69,9 @@ class ResNet:
             self.fuse_downsample = True
             # the stem conv + ReLU + max-pool as one launch (ops.stem_pool_h2)
             self.fuse_stem_pool = True
+            # block i's conv3 (+ residual) and block i+1's conv1 as one launch
+            # inside a stage (ops.bottleneck_seam_h2) for planes 64 / 128 / 256
+            self.fuse_seams = False  # measured per release: see DESIGN.md (the seam kernel)
             self.bneck_h2 = {}
             for li in range(len(self.layers)):
                 p = f"layer{li + 1}.0"
@@ -93,7 +96,10 @@ class ResNet:
         its ReLU and the max-pool run as one launch (ops.stem_pool_h2), so the
         stem's full-resolution map never reaches HBM.  A stage's
         first block runs conv3 and its downsample projection as one GEMM
-        (ops.bottleneck_out_h2), so the projected identity never reaches HBM."""
+        (ops.bottleneck_out_h2), so the projected identity never reaches HBM;
+        inside a stage, block i's conv3 and block i+1's conv1 run as one
+        launch (ops.bottleneck_seam_h2, fuse_seams), so block i's output is
+        not read back for that conv1."""
         cv, h2 = self.convs, self.convs_h2
         rec = ops.amax_records(2 + 3 * sum(self.layers), x.device)
         ops.amax_f32(x, rec[0])
@@ -104,16 +110,27 @@ class ResNet:
             x = ops.maxpool2d(x, 3, 2, 1)
         xa, r, x3 = rec[1], 2, None
         for li, nb in enumerate(self.layers):
+            h1 = None  # the next block's conv1 output, when a seam launch produced it
             for bi in range(nb):
                 p = f"layer{li + 1}.{bi}"
                 s1, s2 = W.block_strides(2 if (bi == 0 and li > 0) else 1, self.stride_on)
                 d = f"{p}.downsample.0"
                 fused = bi == 0 and self.fuse_downsample and p in self.bneck_h2
                 idn = ops.conv2d_h2(x, xa, h2[d], cv[d][1], s1 * s2, 0, None, False) if bi == 0 and not fused else x
-                y = ops.conv2d_h2(x, xa, h2[f"{p}.conv1"], cv[f"{p}.conv1"][1], s1, 0, None, True, rec[r])
+                if h1 is None:
+                    y = ops.conv2d_h2(x, xa, h2[f"{p}.conv1"], cv[f"{p}.conv1"][1], s1, 0, None, True, rec[r])
+                else:
+                    y = h1
                 y = ops.conv2d_h2(y, rec[r], h2[f"{p}.conv2"], cv[f"{p}.conv2"][1], s2, 1, None, True, rec[r + 1])
+                # a seam: this block's conv3 with the next (non-entry) block's conv1
+                seam = (self.fuse_seams and 1 <= bi < nb - 1 and h2[f"{p}.conv3"].cin in (64, 128, 256))
+                h1 = None
                 if fused:
                     x = ops.bottleneck_out_h2(y, rec[r + 1], x, xa, self.bneck_h2[p], s1 * s2, rec[r + 2])
+                elif seam:
+                    q = f"layer{li + 1}.{bi + 1}.conv1"
+                    x, h1 = ops.bottleneck_seam_h2(y, rec[r + 1], idn, h2[f"{p}.conv3"], cv[f"{p}.conv3"][1], h2[q],
+                                                   cv[q][1], rec[r + 2], rec[r + 3])
                 else:
                     x = ops.conv2d_h2(y, rec[r + 1], h2[f"{p}.conv3"], cv[f"{p}.conv3"][1], 1, 0, idn, True,
                                       rec[r + 2])

@@ -334,6 +334,39 @@ def bottleneck_out_h2(y, y_amax, x, x_amax, wb, stride, out_amax=None):
     return out
 
 
+def bottleneck_seam_h2(y2, y2_amax, res, c3, b3, c1, b1, out_amax=None, h1_amax=None):
+    """Block i's conv3 (+ residual, ReLU) and block i+1's conv1 (+ ReLU) as one
+    f16x2 launch (rr_bottleneck_seam_h2): y2 [B,H,W,P] (block i's conv2
+    output, record y2_amax), res [B,H,W,4P] (block i's input), c3 / c1 the
+    1x1 H2Conv weights (4P x P and P x 4P).  -> (out [B,H,W,4P], h1
+    [B,H,W,P])."""
+    _f32(y2, "bottleneck_seam_h2 y2")
+    _f32(res, "bottleneck_seam_h2 res")
+    if not isinstance(c3, H2Conv) or not isinstance(c1, H2Conv):
+        raise TypeError("bottleneck_seam_h2: c3 and c1 must be ops.H2Conv")
+    b, h, w, planes = y2.shape
+    if (c3.kh, c3.kw, c3.cin, c3.cout) != (1, 1, planes, 4 * planes) or \
+            (c1.kh, c1.kw, c1.cin, c1.cout) != (1, 1, 4 * planes, planes):
+        raise ValueError("bottleneck_seam_h2: conv3 must be 1x1 P -> 4P and conv1 1x1 4P -> P")
+    if tuple(res.shape) != (b, h, w, 4 * planes):
+        raise ValueError("bottleneck_seam_h2: residual shape mismatch")
+    for t, nm in ((b3, "b3"), (b1, "b1")):
+        if t is not None:
+            _f32(t, "bottleneck_seam_h2 " + nm)
+    for r, nm in ((y2_amax, "y2_amax"), (out_amax, "out_amax"), (h1_amax, "h1_amax")):
+        if r is not None and (r.dtype != torch.int32 or r.numel() != AMAX_SLOTS or not r.is_contiguous()):
+            raise ValueError(f"bottleneck_seam_h2: {nm} must be a contiguous int32 [RR_AMAX_SLOTS] record")
+    dev = _dev(y2)
+    out = torch.empty((b, h, w, 4 * planes), dtype=torch.float32, device=y2.device)
+    h1 = torch.empty((b, h, w, planes), dtype=torch.float32, device=y2.device)
+    hd = _lib.handle(dev)
+    _lib.check(_lib.lib().rr_bottleneck_seam_h2(hd, _ptr(y2), _ptr(y2_amax), b * h * w, planes, _ptr(res),
+                                                _ptr(c3.planes), _ptr(c3.iscale), _ptr(b3), _ptr(c1.planes),
+                                                _ptr(c1.iscale), _ptr(b1), _ptr(out), _ptr(out_amax), _ptr(h1),
+                                                _ptr(h1_amax), _stream(dev)), hd, "rr_bottleneck_seam_h2")
+    return out, h1
+
+
 def resize_bilinear(x_nhwc, out_h, out_w, scale_factor=None):
     """NHWC bilinear resize, align_corners=False.  With ``scale_factor`` the
     source index uses 1/scale_factor, as F.interpolate(scale_factor=s) does."""

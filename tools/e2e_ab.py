@@ -54,18 +54,29 @@ def split(c):
             {k: v for k, v in kv.items() if k not in ops._TUNE_KEYS})
 
 
+def owner(k):
+    """the extractor object holding attribute k: the extractor itself or a
+    nested part (GeMPCAw.net, GeM.backbone: e.g. fuse_seams on the trunk)"""
+    o = net
+    while not hasattr(o, k):
+        o = getattr(o, "net", None) or getattr(o, "backbone", None)
+        if o is None:
+            raise AttributeError(k)
+    return o
+
+
 if EMB:
     res = {c: [] for c in EMB}
     for _ in range(ROUNDS):
         for c in EMB:
             tk, attrs = split(c)
-            saved = {k: getattr(net, k) for k in attrs}
+            saved = {k: getattr(owner(k), k) for k in attrs}
             for k, v in attrs.items():
-                setattr(net, k, bool(v) if isinstance(saved[k], bool) else v)
+                setattr(owner(k), k, bool(v) if isinstance(saved[k], bool) else v)
             with ops.tuning(0, **tk):
                 res[c].append(wall(lambda: net.forward_test_u8(imgs)))
             for k, v in saved.items():
-                setattr(net, k, v)
+                setattr(owner(k), k, v)
     for c in EMB:
         print(f"embed {c:40s} median {statistics.median(res[c]):8.3f} ms  all {['%.2f' % v for v in res[c]]}",
               flush=True)
