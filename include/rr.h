@@ -53,7 +53,9 @@ typedef struct rr_handle_s* rr_handle_t;
  * LayerNorm fold); 5 = rr_bottleneck_seam_h2 was added and the tuning keys
  * RR_TUNE_SWEEP_ORDER (6), RR_TUNE_SWEEP_PF (7) and RR_TUNE_LP_IL (12) and the
  * lp_cfg value 6 were retired (round 5: they lost their A/Bs; rr_set_tuning
- * now returns RR_EINVAL for them, and their numbers are not reused).
+ * now returns RR_EINVAL for them, and their numbers are not reused), and
+ * rr_linear_bf16_ln / rr_ln_partials_bf16 now centre the bf16 rows on their
+ * 256-column tile means with colsum per k tile (same arguments, new layout).
  * Bindings compare rr_abi_version() with the RR_ABI_VERSION they were
  * written against.                                                          */
 #define RR_ABI_VERSION 5
@@ -460,21 +462,24 @@ int rr_linear_bf16(rr_handle_t h, const void* x, int m, int k, const void* w,
  * / ln_2 of :188-190) folded into the GEMMs, so no LayerNorm pass reads the
  * fp32 residual stream.  Exactly one of stats_in / stats_out is set:
  *  - stats_out (the out-proj / c_proj GEMMs: bias, residual, fp32 y, act 0,
- *    n % 256 == 0, k % 64 == 0): besides y, writes xb_out [m][n] = bf16(y) (RNE) and per row
- *    and 256-column tile t the LayerNorm partials of y: stats_out [m][n/256][2]
- *    = (mean_t, M2_t = sum (y - mean_t)^2 over the tile's 256 columns).
- *  - stats_in (the in-proj / c_fc GEMMs: bias, bf16 y, k % 64 == 0): x holds
- *    such bf16 rows (xb) with their partials [m][ceil(k/256)][2]; w =
- *    bf16(W o gamma) (columns scaled by the LayerNorm weight), colsum[n] =
- *    sum_k float(w[n][k]), bias = b + W beta:
- *      y = act(rstd_m (x.w^T - mean_m colsum) + bias),
+ *    n % 256 == 0, k % 64 == 0): besides y, writes per row and 256-column tile
+ *    t the LayerNorm partials of y, stats_out [m][n/256][2] = (mean_t, M2_t =
+ *    sum (y - mean_t)^2 over the tile's 256 columns), and xb_out [m][n] =
+ *    bf16(y - mean_t) (RNE), each tile centred on its own mean.
+ *  - stats_in (the in-proj / c_fc GEMMs: bias, bf16 y, k % 64 == 0, k <= 768):
+ *    x holds such centred bf16 rows (xb) with their partials
+ *    [m][ceil(k/256)][2]; w = bf16(W o gamma) (columns scaled by the LayerNorm
+ *    weight), colsum [ceil(k/256)][n] = sum over k-tile t of float(w[n][k]),
+ *    bias = b + W beta:
+ *      y = act(rstd_m (x.w^T + sum_t (mean_t - mean_m) colsum[t]) + bias),
  *    mean_m / rstd_m = 1 / sqrt(var + eps) from the partials (biased
  *    variance, combined as Chan et al.).  Equal to LayerNorm -> bf16 ->
- *    rr_linear_bf16 up to where bf16 rounding falls: the operand is bf16(y),
- *    not bf16(LayerNorm(y)), so each element's rounding error is 2^-9 |y_k|
- *    instead of 2^-9 |y_k - mean| and the fold's error grows with the rows'
- *    |mean| / std (tests/test_gpu_vit.py measures a mean offset of 20 std:
- *    test_linear_bf16_ln_fold_large_mean).                                  */
+ *    rr_linear_bf16 up to where bf16 rounding falls: the operand is
+ *    bf16(y - mean_t) instead of bf16(LayerNorm(y)), an element rounding error
+ *    of 2^-9 |y_k - mean_t| against the LayerNorm path's 2^-9 rstd |y_k -
+ *    mean| -- the same scale, whatever the rows' |mean| / std (centring was
+ *    added in ABI 5: with bf16(y) the error grew with |mean| / std;
+ *    tests/test_gpu_vit.py::test_linear_bf16_ln_fold_large_mean).             */
 int rr_linear_bf16_ln(rr_handle_t h, const void* x, int m, int k, const void* w,
                       const float* bias, int n, const float* residual, int act,
                       int out_bf16, void* y, const float* stats_in,
@@ -482,8 +487,8 @@ int rr_linear_bf16_ln(rr_handle_t h, const void* x, int m, int k, const void* w,
                       void* xb_out, void* stream);
 
 /* The producer side of rr_linear_bf16_ln for rows that no GEMM wrote (the
- * first block's ln_1 input): xb [m][d] = bf16(x) and the partials
- * stats [m][d/256][2] of fp32 x [m][d]; d % 256 == 0.                      */
+ * first block's ln_1 input): the partials stats [m][d/256][2] = (mean_t,
+ * M2_t) of fp32 x [m][d] and xb [m][d] = bf16(x - mean_t); d % 256 == 0.   */
 int rr_ln_partials_bf16(rr_handle_t h, const float* x, int m, int d, void* xb,
                         float* stats, void* stream);
 

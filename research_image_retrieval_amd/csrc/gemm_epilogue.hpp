@@ -58,24 +58,31 @@ inline int ep_flags(const GemmArgs& g) {
          (g.stats_out != nullptr ? EP_STATS : 0) | (g.stats_in != nullptr ? EP_LNFOLD : 0);
 }
 
-// Row m's LayerNorm mean and 1/sqrt(var + eps) from the producer's per-tile
-// partials (mean_t, M2_t over n_t = min(256, d - 256 t) columns), combined as
-// Chan et al.: mean = sum n_t mean_t / d, M2 = sum M2_t + n_t (mean_t - mean)^2
-// (biased variance M2 / d, as nn.LayerNorm).  The consumer GEMM computes its
-// tile's rows once, before its k-loop, into LDS (ln_tile_stats).
-__device__ __forceinline__ void ln_row_stats(const float* st, long long m, int d, float eps, float& mean,
-                                             float& rstd) {
+// The LayerNorm fold's consumer handles rows of up to LN_TMAX 256-column
+// tiles (d <= 768: the ViT-B/16 in-proj / c_fc inputs); per row it stages
+// LN_ROW floats: rstd and the tile-mean offsets d_t = mean_t - mean.
+constexpr int LN_TMAX = 3, LN_ROW = 4;
+// Row m's LayerNorm rstd = 1/sqrt(var + eps) and tile-mean offsets from the
+// producer's per-tile partials (mean_t, M2_t over n_t = min(256, d - 256 t)
+// columns), combined as Chan et al.: mean = sum n_t mean_t / d, M2 = sum M2_t
+// + n_t (mean_t - mean)^2 (biased variance M2 / d, as nn.LayerNorm).  The
+// consumer GEMM computes its tile's rows once, before its k-loop, into LDS.
+__device__ __forceinline__ f32x4 ln_row_stats(const float* st, long long m, int d, float eps) {
   const int T = (d + 255) >> 8;
   const float* p = st + m * T * 2;
   float s = 0.f;
   for (int t = 0; t < T; ++t) s += (float)min(256, d - 256 * t) * p[2 * t];
-  mean = s / (float)d;
+  const float mean = s / (float)d;
   float m2 = 0.f;
   for (int t = 0; t < T; ++t) {
     const float dm = p[2 * t] - mean;
     m2 += p[2 * t + 1] + (float)min(256, d - 256 * t) * dm * dm;
   }
-  rstd = 1.0f / sqrtf(m2 / (float)d + eps);
+  f32x4 r = {1.0f / sqrtf(m2 / (float)d + eps), 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int t = 0; t < LN_TMAX; ++t)
+    if (t < T) r[1 + t] = p[2 * t] - mean;
+  return r;
 }
 
 // ---- f16x2 split scales (gemm_s3.hip, SP 2) ----
@@ -117,6 +124,12 @@ __device__ __forceinline__ int h2_exp(float amax) {
   return e > 126 ? 126 : e;
 }
 
+// a fresh, opaque copy of v (loads addressed by it are not hoisted)
+__device__ __forceinline__ int ep_opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+
 // Write one staged slab (rows mb.. of the tile, row-major in ct): the LDS
 // reads of a group of row chunks first (counted lgkmcnt waits instead of an
 // LDS round trip between consecutive stores; the whole slab at once when no
@@ -128,11 +141,11 @@ __device__ __forceinline__ int h2_exp(float amax) {
 template <int FL, int P, int ITERS, int NT, int C4, int CS, int BI>
 __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const float* ct, const f32x4 (&bias_v)[BI],
                                            const f32x4 (&res)[ITERS], int tid, int mb, int n0, const f32x4 (&sc_v)[BI],
-                                           float& am, const f32x4& cs_v, const float* ln_l = nullptr) {
+                                           float& am, const float* ln_l = nullptr, const float* ln_cs = nullptr) {
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   constexpr bool FIXED = FL >= 0;
   // (the LayerNorm fold's epilogue holds two more values per row: fewer LDS reads ahead)
-  constexpr int GR = ITERS < 4 ? ITERS : (FIXED && (FL & EP_LNFOLD) != 0) ? 2 : (P == 1 ? 8 : 4);
+  constexpr int GR = (FIXED && (FL & EP_LNFOLD) != 0) ? 1 : ITERS < 4 ? ITERS : (P == 1 ? 8 : 4);
   // EP_STATS: one row of the 256-column tile per wave and iteration
   static_assert(!(FIXED && (FL & (EP_STATS | EP_LNFOLD))) || (BI == 1 && C4 == 64), "LayerNorm fold: 256-column tiles");
   const bool has_bias = FIXED ? (FL & EP_BIAS) != 0 : g.bias != nullptr;
@@ -142,6 +155,7 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
   // BI == 1: every iteration of a thread is the same column, NT / C4 rows on
   const int c40 = tid % C4, r0 = tid / C4;
   constexpr int RSTEP = NT / C4;
+
   const int n_fix = n0 + c40 * 4;
   const long long o0 = (long long)(mb + r0) * g.ldc + n_fix;
   const long long ostep = (long long)RSTEP * g.ldc;
@@ -173,9 +187,17 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
     f32x4 v = cv[it];
     if constexpr (FIXED && (FL & EP_SCALE) != 0) v *= sc_v[BI == 1 ? 0 : it];
     if constexpr (FIXED && (FL & EP_LNFOLD) != 0) {
-      // the row's (mean, rstd), staged in LDS before the k-loop (slab-relative)
-      const float2 mr = *reinterpret_cast<const float2*>(ln_l + 2 * (m - mb));
-      v = (v - mr.x * cs_v) * mr.y;
+      // the row's rstd and tile-mean offsets d_t = mean_t - mean and the
+      // tile's column sums per k tile, staged in LDS before the k-loop
+      // (rows slab-relative): y = rstd (acc + sum_t d_t colsum_t).  The
+      // column sums are re-read per row (an opaque offset), not held in
+      // registers through the stores: 12 more there spilled the 256 x 256 tile.
+      const f32x4 rd = *reinterpret_cast<const f32x4*>(ln_l + LN_ROW * (m - mb));
+      const int co = ep_opaque(c40 * 4);
+      f32x4 u = v;
+#pragma unroll
+      for (int t = 0; t < LN_TMAX; ++t) u += rd[1 + t] * *reinterpret_cast<const f32x4*>(ln_cs + t * (4 * C4) + co);
+      v = u * rd[0];
     }
     if (has_bias) v += bias_v[BI == 1 ? 0 : it];
     if (has_res) v += res[it];
@@ -197,12 +219,14 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
       *reinterpret_cast<f32x4*>(Cb + o) = v;
     }
     if constexpr (FIXED && (FL & EP_STATS) != 0) {
-      // the row's bf16 copy and its tile's LayerNorm partials, two passes
-      // over the 256 values the wave holds (row m is wave-uniform; N % 256 == 0)
-      const bf16x4 ob = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
-      *reinterpret_cast<bf16x4*>(g.c2 + o) = ob;
+      // the row's tile LayerNorm partials, two passes over the 256 values the
+      // wave holds (row m is wave-uniform; N % 256 == 0), and its bf16 copy
+      // centred on the tile mean: bf16(v - mean_t) rounds 2^-9 |v - mean_t|,
+      // not 2^-9 |v|, so a row mean far from 0 costs the fold no precision
       const float mt = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / 256.0f);
       const f32x4 dv = v - mt;
+      const bf16x4 ob = {(__bf16)dv[0], (__bf16)dv[1], (__bf16)dv[2], (__bf16)dv[3]};
+      *reinterpret_cast<bf16x4*>(g.c2 + o) = ob;
       const float m2 = wave_sum((dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]));
       // (wave-uniform: lane 0 stores)
       if ((threadIdx.x & 63) == 0) {
@@ -223,6 +247,7 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
 template <int WM, int WN, int FM, int FN, int CAPF, bool MF16 = false, int FL = -1>
 __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, const f32x16 (&acc)[FM][FN], float* lds,
                                                int m0, int n0, float a_isc = 1.f, const float* ln_lds = nullptr) {
+  // (EP_LNFOLD: ln_lds = [BM][LN_ROW] row statistics, then [LN_TMAX][BN] column sums)
   constexpr int NT = 64 * WM * WN;
   constexpr int WTM = 32 * FM, WTN = 32 * FN;
   constexpr int BM = WTM * WM, BN = WTN * WN;
@@ -255,12 +280,8 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
   constexpr int BI = (NT % C4 == 0) ? 1 : ITERS;
   constexpr bool SCALED = FL >= 0 && (FL & EP_SCALE) != 0;
   static_assert(!(FL >= 0 && (FL & (EP_SCALE | EP_AMAX))) || BI == 1, "scaled epilogues: one column per thread");
-  f32x4 bias_v[BI], sc_v[BI], cs_v = {0.f, 0.f, 0.f, 0.f};
+  f32x4 bias_v[BI], sc_v[BI];
   float am = 0.f;
-  if constexpr (FL >= 0 && (FL & EP_LNFOLD) != 0) {
-    const int n = n0 + (tid % C4) * 4;
-    if (n < g.N) cs_v = *reinterpret_cast<const f32x4*>(g.colsum + n);
-  }
   if (vec_ok) {
 #pragma unroll
     for (int it = 0; it < BI; ++it) {
@@ -328,9 +349,9 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) asm volatile("" : "+v"(res[it]));
       }
-      if constexpr (FL >= 0 && (FL & EP_LNFOLD) != 0) asm volatile("" : "+v"(cs_v));
       store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, CS, BI>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0, sc_v, am,
-                                                                 cs_v, ln_lds ? ln_lds + 2 * rbase : nullptr);
+                                                                 ln_lds ? ln_lds + LN_ROW * rbase : nullptr,
+                                                                 ln_lds ? ln_lds + LN_ROW * BM : nullptr);
     } else {
       for (int idx = tid; idx < SLAB * C4; idx += NT) {
         const int row = idx / C4, c4 = idx - row * C4;

@@ -129,7 +129,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   constexpr int BUF = (BM + BN) * BK;  // floats per LDS buffer
   // EP_LNFOLD: the tile's rows' LayerNorm (mean, rstd) beside the stages
   constexpr bool LNF = EPI >= 0 && (EPI & EP_LNFOLD) != 0;
-  __shared__ __attribute__((aligned(16))) float lds[2 * BUF + (LNF ? 2 * BM : 0)];
+  __shared__ __attribute__((aligned(16))) float lds[2 * BUF + (LNF ? LN_ROW * BM + LN_TMAX * BN : 0)];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -357,9 +357,16 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_kernel(GemmArgs g, in
   // before the k-loop (the prologue's barrier publishes them to the epilogue)
   if constexpr (LNF) {
     if (tid < BM) {
-      float mean = 0.f, rstd = 0.f;
-      if (m0 + tid < g.M) ln_row_stats(g.stats_in, m0 + tid, g.stats_k, g.ln_eps, mean, rstd);
-      *reinterpret_cast<float2*>(lds + 2 * BUF + 2 * tid) = float2{mean, rstd};
+      const f32x4 r = m0 + tid < g.M ? ln_row_stats(g.stats_in, m0 + tid, g.stats_k, g.ln_eps) : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(lds + 2 * BUF + LN_ROW * tid) = r;
+    }
+    // the tile's column sums per k tile (colsum [T][N]), zero past N and T
+    const int T = (g.stats_k + 255) >> 8;
+    for (int i = tid; i < LN_TMAX * BN / 4; i += NT) {
+      const int t = i / (BN / 4), c = (i - t * (BN / 4)) * 4;
+      const f32x4 v = (t < T && n0 + c < g.N) ? *reinterpret_cast<const f32x4*>(g.colsum + (long long)t * g.N + n0 + c)
+                                              : f32x4{0.f, 0.f, 0.f, 0.f};
+      *reinterpret_cast<f32x4*>(lds + 2 * BUF + LN_ROW * BM + t * BN + c) = v;
     }
   }
 

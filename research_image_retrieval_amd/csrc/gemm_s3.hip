@@ -1094,7 +1094,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
 #pragma unroll
       for (int q = 0; q < 2; ++q)
         store_slab<EPI, 2, HITERS, NT, C4, CS, 1>(g, g.C, ct + q * 32 * CS, bias_v, res[sl][q], te,
-                                                  m0 + q * 64 + sl * 32, n0, sc_v, am, f32x4{0.f, 0.f, 0.f, 0.f});
+                                                  m0 + q * 64 + sl * 32, n0, sc_v, am);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();  // every LDS read of the slab done
       asm volatile("" ::: "memory");

@@ -76,6 +76,38 @@ __device__ __forceinline__ void seam_static_for(F&& f, std::integer_sequence<int
   (f(std::integral_constant<int, Is>{}), ...);
 }
 
+// Diagnostic build only (-DRR_SEAM_PHASES=1, tools/phase_build.sh): per-wave
+// s_memtime deltas of the seam kernel's phases, summed per wave role
+// (0 = residual waves, 1 = loader waves) into seam_phase_sum (read by
+// rr_debug_seam_phases).  Phases: 0 conv3 MFMAs, 1 DMA issue, 2 k-tile end
+// wait, 3 k-tile barrier, 4 residual wait + barrier, 5 chunk epilogue,
+// 6 conv1 MFMAs, 7 prologue + conv1 epilogue.
+#ifndef RR_SEAM_PHASES
+#define RR_SEAM_PHASES 0
+#endif
+#if RR_SEAM_PHASES
+__device__ unsigned long long seam_phase_sum[2][8];
+#define SP_DECL unsigned long long sp_t = __builtin_amdgcn_s_memtime(), sp_acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#define SP(i)                                                   \
+  do {                                                          \
+    const unsigned long long sp_n = __builtin_amdgcn_s_memtime(); \
+    sp_acc[i] += sp_n - sp_t;                                   \
+    sp_t = sp_n;                                                \
+  } while (0)
+#define SP_FLUSH(role)                                                              \
+  do {                                                                              \
+    if ((threadIdx.x & 63) == 0)                                                    \
+      for (int i = 0; i < 8; ++i) atomicAdd(&seam_phase_sum[role][i], sp_acc[i]);   \
+  } while (0)
+#else
+#define SP_DECL
+#define SP(i) ((void)0)
+#define SP_FLUSH(role) ((void)0)
+#endif
+
+// the fp32 chunk's granule swizzle (gemm_seam.hip dma_res)
+__device__ __forceinline__ int rsw(int row) { return ((row >> 2) & 3) << 2; }
+
 template <int P>
 __global__ __launch_bounds__(512, 1) void seam_h2_kernel(SeamArgs a) {
   static_assert(P == 64 || P == 128 || P == 256, "planes");
@@ -98,11 +130,15 @@ __global__ __launch_bounds__(512, 1) void seam_h2_kernel(SeamArgs a) {
   // K = 64, profiles/r03j_acc1_ab.txt)
   constexpr bool ACC2 = P < 256;
   // LDS (16-bit units): [0, 32768) the chunk region (fp32 residual -> y ->
-  // conv1's A planes [NK1][2][128][32]); two 32 KB stages (conv3's B planes
-  // [2][128][32] or conv1's [2][P][32]); 8 block-max words
-  constexpr int A1 = 0, STG = 32768, STG_SZ = 16384, AMX = STG + 2 * STG_SZ;
+  // conv1's A planes [NK1][2][128][32]); NS 32 KB stages (conv3's B planes
+  // [2][128][32] or conv1's [2][P][32]); the epilogue's 8 block-max words go
+  // in the stage its chunk's last conv3 k-tile has released
+  // NS stages: three (the weight DMA two k-tiles ahead) when a chunk's
+  // k-tiles divide by three, so every chunk starts on stage 0; else two
+  constexpr int NS = (NK3 + NK1) % 3 == 0 ? 3 : 2;
+  constexpr int A1 = 0, STG = 32768, STG_SZ = 16384;
   static_assert(2 * P * 32 <= STG_SZ, "conv1 B tile must fit a stage");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[AMX + 16];
+  __shared__ __attribute__((aligned(16))) uint16_t lds[STG + NS * STG_SZ];
   float* const lds_f = reinterpret_cast<float*>(lds);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -118,6 +154,7 @@ __global__ __launch_bounds__(512, 1) void seam_h2_kernel(SeamArgs a) {
   const int lr = lane & 31, lh = lane >> 5;      // 32x32x16 lane roles
   const int wm1 = wave % WM1, wn1 = wave / WM1;  // conv1 wave grid
   const int M = a.M, m0 = blockIdx.x * BM;
+  SP_DECL
 
   // ---- conv3's A: wave w's 16 rows x P, split once into 16x16x32 fragments
   // held in registers for every chunk (lane: row 16 w + l16, k 32 q + 8 lg ..
@@ -176,12 +213,17 @@ __global__ __launch_bounds__(512, 1) void seam_h2_kernel(SeamArgs a) {
   // chunk region, instruction i of wave lw = rows 2 (4 i + lw) + {0, 1} ----
   // (addresses from an opaque base, recomputed per chunk: hoisted out of
   // the chunk loop, the 16 per-lane pointers were spilled)
+  // Granule swizzle of the fp32 chunk: 16-B granule g of row r sits at
+  // g ^ rsw(r) (rows 4 apart in different 16-bank windows: the epilogue's
+  // accumulator-layout reads are conflict-free); the DMA moves it on the
+  // source side (its LDS destination is lane-linear).
   auto dma_res = [&](int c) __attribute__((always_inline)) {
     const int rb = s3_opaque(m0 + 2 * lw + lh);
-    const float* base = a.R + CW * c + lr * 4;
+    const float* base = a.R + CW * c;
 #pragma unroll
     for (int i = 0; i < NR; ++i) {
-      const float* src = base + (long long)min(rb + 8 * i, M - 1) * N3;
+      const int row = 2 * (4 * i + lw) + lh;  // local row
+      const float* src = base + (long long)min(rb + 8 * i, M - 1) * N3 + 4 * (lr ^ rsw(row));
       __builtin_amdgcn_global_load_lds((const void*)src,
                                        (__attribute__((address_space(3))) void*)(lds + A1 + 2 * (4 * i + lw) * 256), 16,
                                        0, 0);
@@ -262,6 +304,8 @@ __global__ __launch_bounds__(512, 1) void seam_h2_kernel(SeamArgs a) {
   // ---- chunk epilogue: y = ReLU(acc3 scale + b3 + residual), stored, split
   // into conv1's A planes.  Entered after the barrier that ends the chunk's
   // last conv3 k-tile, behind the residual waves' wait for their DMA ----
+  // the stage the chunk's last conv3 k-tile released: the block-max words
+  constexpr int AMX_F = (STG + ((NK3 - 1) % NS) * STG_SZ) / 2;
   auto epi3 = [&](int c) __attribute__((always_inline)) {
     float am = 0.f;
 #pragma unroll
@@ -273,20 +317,24 @@ __global__ __launch_bounds__(512, 1) void seam_h2_kernel(SeamArgs a) {
       if constexpr (ACC2) v += acc3lo[n];
       float rv[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) rv[r] = lds_f[(16 * wave + 4 * lg + r) * CW + col];
+      for (int r = 0; r < 4; ++r) {
+        const int row = 16 * wave + 4 * lg + r;
+        rv[r] = lds_f[row * CW + 4 * ((col >> 2) ^ rsw(row)) + (col & 3)];
+      }
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
+        const int row = 16 * wave + 4 * lg + r;
         float x = v[r] * sc;
         x += bb;
         x += rv[r];
         x = fmaxf(x, 0.f);
         am = amax_acc(am, x);
-        lds_f[(16 * wave + 4 * lg + r) * CW + col] = x;
+        lds_f[row * CW + 4 * ((col >> 2) ^ rsw(row)) + (col & 3)] = x;
       }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) am = __builtin_fmaxf(am, __shfl_xor(am, o));
-    if (lane == 0) lds_f[AMX / 2 + wave] = am;
+    if (lane == 0) lds_f[AMX_F + wave] = am;
     seam_barrier();
     // row-contiguous: thread = (row r0 + 16 it, columns 4 c4 .. + 3)
     // (s3_opaque: recomputed here, not hoisted and held through the k-loop)
@@ -294,16 +342,29 @@ __global__ __launch_bounds__(512, 1) void seam_h2_kernel(SeamArgs a) {
     const int c4 = te & 31, r0 = te >> 5;
     f32x4 yv[8];
 #pragma unroll
-    for (int it = 0; it < 8; ++it) yv[it] = *reinterpret_cast<const f32x4*>(lds_f + (r0 + 16 * it) * CW + c4 * 4);
-    float bm = lds_f[AMX / 2];
+    for (int it = 0; it < 8; ++it) {
+      const int row = r0 + 16 * it;
+      yv[it] = *reinterpret_cast<const f32x4*>(lds_f + row * CW + 4 * (c4 ^ rsw(row)));
+    }
+    float bm = lds_f[AMX_F];
 #pragma unroll
-    for (int w = 1; w < 8; ++w) bm = __builtin_fmaxf(bm, lds_f[AMX / 2 + w]);
+    for (int w = 1; w < 8; ++w) bm = __builtin_fmaxf(bm, lds_f[AMX_F + w]);
     y_am = __builtin_fmaxf(y_am, bm);
     run_max = __builtin_fmaxf(run_max, bm);
+    // y stored by the residual waves only (their counter holds nothing the
+    // k-loop waits on): rows r0 + 16 it of their own and r0 + 8 + 16 it
+    if (!ldw) {
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {
-      const int m = m0 + r0 + 16 * it;
-      if (m < M) *reinterpret_cast<f32x4*>(a.Y + (long long)m * N3 + CW * c + c4 * 4) = yv[it];
+      for (int it = 0; it < 8; ++it) {
+        const int m = m0 + r0 + 16 * it;
+        if (m < M) *reinterpret_cast<f32x4*>(a.Y + (long long)m * N3 + CW * c + c4 * 4) = yv[it];
+      }
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int row = r0 + 8 + 16 * it, m = m0 + row;
+        const f32x4 v2 = *reinterpret_cast<const f32x4*>(lds_f + row * CW + 4 * (c4 ^ rsw(row)));
+        if (m < M) *reinterpret_cast<f32x4*>(a.Y + (long long)m * N3 + CW * c + c4 * 4) = v2;
+      }
     }
     const int e = __builtin_amdgcn_readfirstlane(h2_exp(run_max));
     const float ysc = __int_as_float((127 + e) << 23);
@@ -383,7 +444,20 @@ __global__ __launch_bounds__(512, 1) void seam_h2_kernel(SeamArgs a) {
   // loader wave issues the next k-tile's weight DMA at the top of each
   // k-tile and waits for it (vmcnt 0: nothing else is in its counter) before
   // the k-tile's closing barrier ----
+  // position k of chunk c (0 .. NK3 + NK1 - 1; the next chunk's 0, 1 past
+  // the end): its weight DMA into stage (k % NS)
+  auto dma_pos = [&](int c, int k) __attribute__((always_inline)) {
+    if (k < NK3) dma_b3(c, k, k % NS);
+    else if (k < NK3 + NK1) dma_b1(c, k - NK3, k % NS);
+    else if (c + 1 < NC) dma_b3(c + 1, k - NK3 - NK1, k % NS);
+  };
+  // ---- the k-stream: per chunk NK3 conv3 k-tiles, the chunk epilogue, NK1
+  // conv1 k-tiles on a ring of NS stages (a chunk starts on stage 0).  A
+  // loader wave issues position k + NS - 1's weight DMA at the top of k-tile
+  // k and waits for k + 1's (counted vmcnt: only its own DMA are in its
+  // counter) before the k-tile's closing barrier ----
   auto chunk = [&](int c) __attribute__((always_inline)) {
+    const bool last = c + 1 == NC;
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
       acc3[n] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -391,48 +465,62 @@ __global__ __launch_bounds__(512, 1) void seam_h2_kernel(SeamArgs a) {
     }
     // the chunk region is free (the previous chunk's conv1 ended on a barrier)
     if (!ldw) dma_res(c);
-    seam_static_for(
-        [&](auto qc) __attribute__((always_inline)) {
-          constexpr int q = decltype(qc)::value;
-          constexpr int st = q & 1;
-          if (ldw) {
-            if constexpr (q + 1 < NK3) dma_b3(c, q + 1, st ^ 1);
-            else dma_b1(c, 0, st ^ 1);
-          }
-          mma3(q, st);
-          if (ldw) seam_vm_wait<0>();
-          seam_barrier();
-        },
-        std::make_integer_sequence<int, NK3>{});
-    if (!ldw) seam_vm_wait<0>();  // the residual rows (and this wave's older y stores)
-    seam_barrier();
-    epi3(c);
-    seam_static_for(
-        [&](auto tc) __attribute__((always_inline)) {
-          constexpr int t = decltype(tc)::value;
-          constexpr int st = (NK3 + t) & 1;
-          if (ldw) {
-            if constexpr (t + 1 < NK1) dma_b1(c, t + 1, st ^ 1);
-            else if (c + 1 < NC) dma_b3(c + 1, 0, st ^ 1);
-          }
-          mma1(t, st);
-          if (ldw) seam_vm_wait<0>();
-          seam_barrier();
-        },
-        std::make_integer_sequence<int, NK1>{});
+    SP(1);
+    auto kstep = [&](auto kc) __attribute__((always_inline)) {
+      constexpr int k = decltype(kc)::value;
+      constexpr int ahead = k + NS - 1;  // the position whose DMA goes out now
+      constexpr bool crosses = ahead >= NK3 + NK1;
+      if (ldw) dma_pos(c, ahead);
+      SP(1);
+      if constexpr (k < NK3) {
+        mma3(k, k % NS);
+        SP(0);
+      } else {
+        mma1(k - NK3, k % NS);
+        SP(6);
+      }
+      if (ldw) {
+        // every DMA but the one just issued has landed (position k + 1's)
+        if constexpr (NS == 3) {
+          if (crosses && last) seam_vm_wait<0>();
+          else seam_vm_wait<(ahead < NK3 ? NB3 : ahead < NK3 + NK1 ? NB1 : NB3)>();
+        } else {
+          seam_vm_wait<0>();
+        }
+      }
+      SP(2);
+      seam_barrier();
+      SP(3);
+      if constexpr (k == NK3 - 1) {
+        if (!ldw) seam_vm_wait<0>();  // the residual rows (and this wave's older y stores)
+        seam_barrier();
+        SP(4);
+        epi3(c);
+        SP(5);
+      }
+    };
+    seam_static_for(kstep, std::make_integer_sequence<int, NK3 + NK1>{});
   };
 
-  // ---- prologue: conv3 k-tile 0 of chunk 0 (the A fragments are loaded above) ----
+  // ---- prologue: the first NS - 1 positions' weight DMA (the A fragments are loaded above) ----
   if (ldw) {
-    dma_b3(0, 0, 0);
-    seam_vm_wait<0>();
+    dma_pos(0, 0);
+    if constexpr (NS == 3) {
+      dma_pos(0, 1);
+      seam_vm_wait<NB3>();
+    } else {
+      seam_vm_wait<0>();
+    }
   }
   seam_barrier();
+  SP(7);
 #pragma unroll 1
   for (int c = 0; c < NC; ++c) chunk(c);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   epi1();
   if (a.y_amax != nullptr) amax_publish(a.y_amax, y_am, blockIdx.x * 8 + wave);
+  SP(7);
+  SP_FLUSH(ldw ? 1 : 0);
 }
 
 static int launch_seam_h2(rr_handle_s* h, const SeamArgs& a, int planes, hipStream_t s, int timer_cls) {
@@ -460,10 +548,11 @@ extern "C" int rr_bottleneck_seam_h2(rr_handle_t h, const float* y2, const unsig
                                      const void* w1, const float* w1_iscale, const float* b1, float* out,
                                      unsigned* out_amax, float* h1, unsigned* h1_amax, void* stream) {
   RR_ENTRY(h);
-  if (!y2 || !y2_amax || !res || !w3 || !w3_iscale || !w1 || !w1_iscale || !out || !h1 || m < 0)
+  if (m < 0 || (planes != 64 && planes != 128 && planes != 256))
+    return set_error(h, RR_EINVAL, "rr_bottleneck_seam_h2: m >= 0 and planes 64, 128 or 256");
+  if (m == 0) return RR_OK;  // (empty tensors may carry NULL pointers)
+  if (!y2 || !y2_amax || !res || !w3 || !w3_iscale || !w1 || !w1_iscale || !out || !h1)
     return set_error(h, RR_EINVAL, "rr_bottleneck_seam_h2: bad argument");
-  if (planes != 64 && planes != 128 && planes != 256)
-    return set_error(h, RR_EINVAL, "rr_bottleneck_seam_h2: planes must be 64, 128 or 256");
   const void* ptrs[] = {y2, res, w3, w3_iscale, w1, w1_iscale, out, h1, b3, b1};
   for (const void* p : ptrs)
     if ((uintptr_t)p & 15) return set_error(h, RR_EINVAL, "rr_bottleneck_seam_h2: pointers must be 16-byte aligned");
@@ -486,3 +575,14 @@ extern "C" int rr_bottleneck_seam_h2(rr_handle_t h, const float* y2, const unsig
   a.M = m;
   return launch_seam_h2(h, a, planes, (hipStream_t)stream, kTimeGemm);
 }
+
+#if RR_SEAM_PHASES
+extern "C" int rr_debug_seam_phases(unsigned long long* out) {
+  // out[16] <- seam_phase_sum (residual waves 0-7, loader waves 8-15), then cleared
+  unsigned long long h[16] = {};
+  if (hipMemcpyFromSymbol(h, HIP_SYMBOL(rr::seam_phase_sum), sizeof(h)) != hipSuccess) return RR_EHIP;
+  for (int i = 0; i < 16; ++i) out[i] = h[i];
+  const unsigned long long z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(rr::seam_phase_sum), z, sizeof(z)) == hipSuccess ? RR_OK : RR_EHIP;
+}
+#endif

@@ -3,6 +3,7 @@
 #include <cstring>
 #include <initializer_list>
 
+#include "gemm_epilogue.hpp"
 #include "rr_internal.hpp"
 
 namespace rr {
@@ -372,10 +373,12 @@ int rr_linear_bf16_ln(rr_handle_t h, const void* x, int m, int k, const void* w,
       return set_error(h, RR_EINVAL,
                        "rr_linear_bf16_ln: stats_out needs bias, residual, fp32 output, n % 256 == 0, k % 64 == 0");
   } else {
-    // the consumer: bias, bf16 output, K in whole 64-deep k-tiles
-    if (!colsum || !bias || residual || !out_bf16 || (k % 64) || (n & 3) || ((uintptr_t)colsum & 15) ||
-        !(eps >= 0.f))
-      return set_error(h, RR_EINVAL, "rr_linear_bf16_ln: stats_in needs colsum, bias, bf16 output, k % 64 == 0");
+    // the consumer: bias, bf16 output, K in whole 64-deep k-tiles, at most
+    // three 256-column LayerNorm tiles (LN_TMAX)
+    if (!colsum || !bias || residual || !out_bf16 || (k % 64) || k > 256 * LN_TMAX || (n & 3) ||
+        ((uintptr_t)colsum & 15) || !(eps >= 0.f))
+      return set_error(h, RR_EINVAL,
+                       "rr_linear_bf16_ln: stats_in needs colsum, bias, bf16 output, k % 64 == 0, k <= 768");
   }
   if (m == 0) return RR_OK;
   GemmArgs g;

@@ -165,9 +165,10 @@ __global__ __launch_bounds__(256) void ln_partials_kernel(const float* __restric
   const int t = (int)(w - row * T);
   const long long o = row * D + 256 * t + 4 * lane;
   const f32x4 v = *reinterpret_cast<const f32x4*>(x + o);
-  *reinterpret_cast<bf16x4*>(xb + o) = bf16x4{(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
   const float mt = wave_sum((v[0] + v[1]) + (v[2] + v[3])) * (1.0f / 256.0f);
   const f32x4 dv = v - mt;
+  // the bf16 rows are centred on their tile's mean (see rr_linear_bf16_ln)
+  *reinterpret_cast<bf16x4*>(xb + o) = bf16x4{(__bf16)dv[0], (__bf16)dv[1], (__bf16)dv[2], (__bf16)dv[3]};
   const float m2 = wave_sum((dv[0] * dv[0] + dv[1] * dv[1]) + (dv[2] * dv[2] + dv[3] * dv[3]));
   if (lane == 0) *reinterpret_cast<float2*>(st + w * 2) = float2{mt, m2};
 }

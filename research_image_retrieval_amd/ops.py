@@ -758,8 +758,9 @@ def linear_bf16(x, w, bias=None, residual=None, act=0, out_bf16=False):
 def linear_bf16_ln_produce(x, w, bias, residual):
     """The residual GEMM of a ViT block with the next LayerNorm's inputs
     produced in its epilogue (rr_linear_bf16_ln, stats_out): returns (y fp32
-    [M,N] = x.w^T + bias + residual, bf16(y), per-row 256-column-tile
-    LayerNorm partials [M, N/256, 2])."""
+    [M,N] = x.w^T + bias + residual, bf16(y - mean_t) with mean_t the mean of
+    the row's 256-column tile, the per-row tile LayerNorm partials
+    [M, N/256, 2] = (mean_t, M2_t))."""
     if x.dtype != torch.bfloat16 or w.dtype != torch.bfloat16:
         raise TypeError("linear_bf16_ln_produce: x and w must be bfloat16")
     if x.dim() != 2 or w.dim() != 2 or not x.is_contiguous() or not w.is_contiguous() or x.shape[1] != w.shape[1]:
@@ -782,17 +783,18 @@ def linear_bf16_ln_produce(x, w, bias, residual):
 
 def linear_bf16_ln_fold(xb, stats, w_folded, colsum, bias_folded, act=0, eps=1e-5):
     """act(LayerNorm(x) . W^T + b) -> bf16 with the LayerNorm folded into the
-    GEMM (rr_linear_bf16_ln, stats_in): xb = bf16 rows of x and their
-    partials (linear_bf16_ln_produce / ln_partials_bf16), w_folded =
-    bf16(W o gamma), colsum = its fp32 row sums, bias_folded = b + W beta
-    (ln_fold_weights)."""
+    GEMM (rr_linear_bf16_ln, stats_in): xb = the tile-centred bf16 rows of x
+    and their partials (linear_bf16_ln_produce / ln_partials_bf16), w_folded =
+    bf16(W o gamma), colsum = its fp32 row sums per 256-deep k tile
+    [ceil(K/256), N], bias_folded = b + W beta (ln_fold_weights); K <= 768."""
     if xb.dtype != torch.bfloat16 or w_folded.dtype != torch.bfloat16:
         raise TypeError("linear_bf16_ln_fold: xb and w_folded must be bfloat16")
     dev = _dev(xb)
     m, k = xb.shape
     n = w_folded.shape[0]
-    if tuple(stats.shape) != (m, (k + 255) // 256, 2) or w_folded.shape[1] != k:
-        raise ValueError("linear_bf16_ln_fold: stats [M, ceil(K/256), 2], w_folded [N, K]")
+    t = (k + 255) // 256
+    if tuple(stats.shape) != (m, t, 2) or w_folded.shape[1] != k or tuple(colsum.shape) != (t, n):
+        raise ValueError("linear_bf16_ln_fold: stats [M, ceil(K/256), 2], w_folded [N, K], colsum [ceil(K/256), N]")
     y = torch.empty((m, n), dtype=torch.bfloat16, device=xb.device)
     hd = _lib.handle(dev)
     _lib.check(_lib.lib().rr_linear_bf16_ln(hd, _ptr(xb), m, k, _ptr(w_folded), _ptr(bias_folded), n, None, int(act),
@@ -802,7 +804,8 @@ def linear_bf16_ln_fold(xb, stats, w_folded, colsum, bias_folded, act=0, eps=1e-
 
 
 def ln_partials_bf16(x):
-    """(bf16(x), the LayerNorm partials [M, D/256, 2]) of fp32 rows x [M, D]
+    """(bf16(x - mean_t), the LayerNorm partials [M, D/256, 2]) of fp32 rows x
+    [M, D], each 256-column tile t centred on its own mean mean_t
     (rr_ln_partials_bf16): the first block's ln_1 input, which no GEMM wrote."""
     _f32(x, "ln_partials_bf16")
     dev = _dev(x)
@@ -818,9 +821,12 @@ def ln_partials_bf16(x):
 
 def ln_fold_weights(w, b, gamma, beta):
     """Fold a LayerNorm (gamma, beta) into the following linear (w [N,K] fp32,
-    b [N]): (bf16(w o gamma), fp32 row sums of that bf16 matrix, b + w beta)."""
+    b [N]): (bf16(w o gamma), the fp32 row sums of that bf16 matrix per
+    256-deep k tile [ceil(K/256), N], b + w beta)."""
     wf = (w.float() * gamma.float()[None, :]).to(torch.bfloat16).contiguous()
-    colsum = wf.float().sum(dim=1).contiguous()
+    n, k = wf.shape
+    t = (k + 255) // 256
+    colsum = torch.nn.functional.pad(wf.float(), (0, 256 * t - k)).view(n, t, 256).sum(dim=2).t().contiguous()
     bf = (b.double() + w.double() @ beta.double()).float().contiguous()
     return wf, colsum, bf
 

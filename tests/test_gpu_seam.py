@@ -78,18 +78,15 @@ def test_seam_vs_float64_and_two_launches(cuda, b, h, w, planes):
     # the records hold exactly max |out| and max |h1|
     assert ops.amax_value(rec[1]) == float(out_c.abs().max())
     assert ops.amax_value(rec[2]) == float(h1_c.abs().max())
-    # against the two launches: at P = 256 the block output bit for bit with
-    # conv3 on the same 256 x 256 one-accumulator tile (config 12); at P < 256
-    # (two accumulators for conv3's short K) and for h1 (conv1 on the library's
-    # pick) to within accumulation-order and split-scale rounding
+    # against the two launches (the library's picks): both outputs to within
+    # accumulation-order rounding (the seam's conv3 runs 16x16x32 MFMAs, the
+    # two-launch path 32x32x16 or 16x16x32 tiles; the same products)
     ru = ops.amax_records(2, cuda)
-    with ops.tuning(cuda.index, s3_cfg=12 if planes == 256 else 0):
-        out_u = ops.conv2d_h2(y2d, rec[0], c3, b3.to(cuda), 1, 0, resd, True, ru[0])
+    out_u = ops.conv2d_h2(y2d, rec[0], c3, b3.to(cuda), 1, 0, resd, True, ru[0])
     h1_u = ops.conv2d_h2(out_u, ru[0], c1, b1.to(cuda), 1, 0, None, True, ru[1])
-    if planes == 256:
-        assert torch.equal(out, out_u)
-    else:
-        assert float((out - out_u).abs().max()) <= 2.0 ** -20 * float(out_u.abs().max())
+    d3 = (out - out_u).abs()
+    print(f"  out vs two launches: {int((d3 > 0).sum())} of {d3.numel()} elements differ, max {float(d3.max()):.3g}")
+    assert float(d3.max()) <= 2.0 ** -20 * float(out_u.abs().max())
     d = (h1 - h1_u).abs()
     n_diff = int((d > 0).sum())
     print(f"  h1 vs two launches: {n_diff} of {d.numel()} elements differ, max {float(d.max()):.3g}")

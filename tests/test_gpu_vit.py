@@ -141,9 +141,10 @@ def test_vit_bf16_linear_bf16_qkv_matches_fp32_qkv(cuda):
 
 def test_ln_partials_and_produce_epilogue(cuda):
     """The LayerNorm fold's producer side: rr_ln_partials_bf16 and the residual
-    GEMM's EP_STATS epilogue give bf16(y) exactly and per-tile (mean, M2)
-    whose Chan combination matches float64 LayerNorm statistics; the GEMM's
-    fp32 output is bit-identical to rr_linear_bf16's."""
+    GEMM's EP_STATS epilogue give per-tile (mean_t, M2) whose Chan combination
+    matches float64 LayerNorm statistics and the tile-centred copy
+    bf16(y - mean_t) exactly; the GEMM's fp32 output is bit-identical to
+    rr_linear_bf16's."""
     g = torch.Generator().manual_seed(3)
     m, k, n = 3 * 197 + 11, 768, 768
     a = (torch.randn(m, k, generator=g)).bfloat16().to(cuda)
@@ -154,7 +155,8 @@ def test_ln_partials_and_produce_epilogue(cuda):
     with ops.tuning(cuda.index, lp_cfg=3):
         y_ref = ops.linear_bf16(a, w, bias, residual=r)
     assert torch.equal(y.view(torch.int32), y_ref.view(torch.int32))
-    assert torch.equal(yb.view(torch.int16), y.bfloat16().view(torch.int16))
+    centred = (y.view(m, n // 256, 256) - st[..., 0:1]).view(m, n)  # the same fp32 subtraction
+    assert torch.equal(yb.view(torch.int16), centred.bfloat16().view(torch.int16))
     xb, st2 = ops.ln_partials_bf16(y)
     assert torch.equal(xb.view(torch.int16), yb.view(torch.int16))
     yd = y.double().cpu().view(m, n // 256, 256)
@@ -197,6 +199,35 @@ def test_linear_bf16_ln_fold_vs_float64(cuda, act):
     print(f"act {act}: fold max {e_fold.max().item() / scale:.3e} mean {e_fold.mean().item() / scale:.3e} | "
           f"LayerNorm path max {e_ln.max().item() / scale:.3e} mean {e_ln.mean().item() / scale:.3e} (x mean |ref|)")
     # bf16 output rounding alone is 2^-9 relative; the operand roundings add a few times that
+    assert e_fold.mean() <= 2.0 * e_ln.mean() + 1e-6
+    assert e_fold.max() <= 2.0 * e_ln.max() + 1e-6
+
+
+@pytest.mark.parametrize("offset", [20.0, -300.0])
+def test_linear_bf16_ln_fold_large_mean(cuda, offset):
+    """Rows whose mean is far from 0 against their spread (mean 20 and -300
+    standard deviations): the tile-centred bf16 rows keep the fold's error at
+    the LayerNorm -> bf16 path's scale (uncentred, bf16(x) would round
+    2^-9 |x| ~ 2^-9 |mean|, 20-300x that)."""
+    g = torch.Generator().manual_seed(11)
+    m, k, n = 2 * 197 + 1, 768, 2304
+    x = torch.randn(m, k, generator=g) + offset
+    x[:, 7] += 5.0  # one heavier channel
+    w = torch.randn(n, k, generator=g) / k ** 0.5
+    b = torch.randn(n, generator=g) * 0.1
+    gam = 1.0 + 0.2 * torch.randn(k, generator=g)
+    bet = 0.1 * torch.randn(k, generator=g)
+    xd = x.to(cuda)
+    xb, st = ops.ln_partials_bf16(xd)
+    wf, cs, bf = ops.ln_fold_weights(w.to(cuda), b.to(cuda), gam.to(cuda), bet.to(cuda))
+    y_fold = ops.linear_bf16_ln_fold(xb, st, wf, cs, bf).float().cpu().double()
+    y_ln = ops.linear_bf16(ops.layernorm_bf16(xd, gam.to(cuda), bet.to(cuda)), w.bfloat16().to(cuda), b.to(cuda),
+                           out_bf16=True).float().cpu().double()
+    ref = torch.nn.functional.layer_norm(x.double(), (k,), gam.double(), bet.double(), 1e-5) @ w.double().t() + b.double()
+    e_fold, e_ln = (y_fold - ref).abs(), (y_ln - ref).abs()
+    scale = ref.abs().mean()
+    print(f"offset {offset}: fold max {e_fold.max().item() / scale:.3e} mean {e_fold.mean().item() / scale:.3e} | "
+          f"LayerNorm path max {e_ln.max().item() / scale:.3e} mean {e_ln.mean().item() / scale:.3e}")
     assert e_fold.mean() <= 2.0 * e_ln.mean() + 1e-6
     assert e_fold.max() <= 2.0 * e_ln.max() + 1e-6
 
@@ -252,8 +283,17 @@ def test_linear_bf16_ln_argument_checks_and_edges(cuda):
                                s) == _lib.RR_EINVAL
     assert L.rr_linear_bf16_ln(h, p(x), m, k, p(w), p(bias), 640, p(r), 0, 0, p(y), None, None, 0.0, p(st), p(yb),
                                s) == _lib.RR_EINVAL
-    # consumer with fp32 output
-    cs = w.float().sum(1)
+    # consumer with fp32 output; with k > 768 (more than three LayerNorm tiles)
+    cs = w.float().view(n, 3, 256).sum(-1).t().contiguous()
+    x4 = torch.randn(m, 1024, device=cuda).bfloat16()
+    w4 = torch.randn(n, 1024, device=cuda).bfloat16()
+    st4 = torch.zeros(m, 4, 2, device=cuda)
+    cs4 = torch.zeros(4, n, device=cuda)
+    assert L.rr_linear_bf16_ln(h, p(x4), m, 1024, p(w4), p(bias), n, None, 0, 1, p(yb), p(st4), p(cs4), 1e-5, None,
+                               None, s) == _lib.RR_EINVAL
+    # producer with k % 64 != 0
+    assert L.rr_linear_bf16_ln(h, p(x[:, :736].contiguous()), m, 736, p(w[:, :736].contiguous()), p(bias), n, p(r), 0,
+                               0, p(y), None, None, 0.0, p(st), p(yb), s) == _lib.RR_EINVAL
     assert L.rr_linear_bf16_ln(h, p(x), m, k, p(w), p(bias), n, None, 0, 0, p(y), p(st), p(cs), 1e-5, None, None,
                                s) == _lib.RR_EINVAL
     # m = 0: nothing to do
@@ -261,7 +301,7 @@ def test_linear_bf16_ln_argument_checks_and_edges(cuda):
                                s) == 0
     # one row, producer then consumer
     y1, yb1, st1 = ops.linear_bf16_ln_produce(x, w, bias, r)
-    assert torch.equal(yb1.view(torch.int16), y1.bfloat16().view(torch.int16))
+    assert torch.equal(yb1.view(torch.int16), (y1.view(m, 3, 256) - st1[..., 0:1]).view(m, n).bfloat16().view(torch.int16))
     gam, bet = torch.ones(n, device=cuda), torch.zeros(n, device=cuda)
     wf, csum, bf = ops.ln_fold_weights(w.float(), bias, gam, bet)
     out = ops.linear_bf16_ln_fold(yb1, st1, wf, csum, bf).float()

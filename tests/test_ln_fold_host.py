@@ -1,7 +1,8 @@
 """Host-side algebra of the ViT LayerNorm fold (rr_linear_bf16_ln; DESIGN.md
 ViT section): the per-256-column-tile partials combined as Chan et al. give
-the row's LayerNorm mean and biased variance, and
-    LayerNorm(x) W^T + b == rstd (x (W o gamma)^T - mean colsum(W o gamma)) + (b + W beta)
+the row's LayerNorm mean and biased variance, and with xc = x centred per
+256-column tile t on its mean mean_t,
+    LayerNorm(x) W^T + b == rstd (xc (W o gamma)^T + sum_t (mean_t - mean) colsum_t(W o gamma)) + (b + W beta)
 holds in float64 (networks/model.py:157-163, 188-190).  ops.ln_fold_weights
 is the weight preparation the GPU path uses (its bf16 rounding aside)."""
 import numpy as np
@@ -44,10 +45,13 @@ def test_fold_identity_float64():
     eps = 1e-5
     ref = torch.nn.functional.layer_norm(torch.from_numpy(x), (k,), torch.from_numpy(gam), torch.from_numpy(bet),
                                          eps).numpy() @ w.T + b
-    mean, var = _combine(*_partials(x), k)
+    mt, m2 = _partials(x)
+    mean, var = _combine(mt, m2, k)
     rstd = 1 / np.sqrt(var + eps)
     wf = w * gam[None, :]
-    got = rstd[:, None] * (x @ wf.T - mean[:, None] * wf.sum(1)[None, :]) + (b + w @ bet)
+    xc = (x.reshape(m, k // 256, 256) - mt[..., None]).reshape(m, k)
+    cst = wf.reshape(n, k // 256, 256).sum(-1)  # [n, T]
+    got = rstd[:, None] * (xc @ wf.T + (mt - mean[:, None]) @ cst.T) + (b + w @ bet)
     np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-10)
 
 
@@ -60,6 +64,13 @@ def test_ln_fold_weights_prep():
     wf, cs, bf = ops.ln_fold_weights(w, b, gam, bet)
     assert wf.dtype == torch.bfloat16 and cs.dtype == torch.float32 and bf.dtype == torch.float32
     assert torch.equal(wf, (w * gam[None, :]).to(torch.bfloat16))
-    # colsum of the bf16-rounded matrix the GEMM multiplies, not of the fp32 one
-    torch.testing.assert_close(cs.double(), wf.double().sum(1), rtol=1e-6, atol=1e-6)
+    # colsum per 256-deep k tile [T, N] of the bf16-rounded matrix the GEMM
+    # multiplies, not of the fp32 one
+    assert cs.shape == (1, 64)
+    torch.testing.assert_close(cs[0].double(), wf.double().sum(1), rtol=1e-6, atol=1e-6)
+    w2 = torch.randn(8, 640, generator=g)
+    _, cs2, _ = ops.ln_fold_weights(w2, torch.zeros(8), torch.ones(640), torch.zeros(640))
+    ref2 = torch.stack([w2.bfloat16().double()[:, 256 * t:256 * t + 256].sum(1) for t in range(3)])
+    assert cs2.shape == (3, 8)
+    torch.testing.assert_close(cs2.double(), ref2, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(bf.double(), b.double() + w.double() @ bet.double(), rtol=1e-6, atol=1e-6)

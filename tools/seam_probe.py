@@ -38,6 +38,24 @@ def unfused():
     return out, ops.conv2d_h2(out, rec[1], c1, b1, 1, 0, None, True, rec[2])
 
 
+if os.environ.get("SEAM_PHASES") == "1":
+    import ctypes
+    from research_image_retrieval_amd import _lib
+    dbg = _lib.lib().rr_debug_seam_phases
+    dbg.argtypes, dbg.restype = [ctypes.c_void_p], ctypes.c_int
+    buf = (ctypes.c_ulonglong * 16)()
+    fused()
+    torch.cuda.synchronize()
+    dbg(ctypes.cast(buf, ctypes.c_void_p))
+    for _ in range(REPS):
+        fused()
+    torch.cuda.synchronize()
+    dbg(ctypes.cast(buf, ctypes.c_void_p))
+    names = ["conv3 mfma", "dma issue", "end wait", "barrier", "res wait+bar", "epi3", "conv1 mfma", "pro+epi1"]
+    for role, nm in ((0, "residual waves"), (1, "loader waves")):
+        v = [buf[8 * role + i] for i in range(8)]
+        tot = sum(v)
+        print(nm, " ".join(f"{names[i]} {v[i] / tot:.3f}" for i in range(8)), flush=True)
 for name, fn in (("fused", fused), ("unfused", unfused)):
     if name == "unfused" and os.environ.get("SEAM_UNFUSED") != "1":
         continue
