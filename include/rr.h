@@ -90,10 +90,13 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     4 (256x320 for bf16 filter / score sweeps, 256x256 otherwise),
  *                     5 (bf16 sweeps with K % 128 == 0, fp8 sweeps with K % 256 == 0:
  *                     256x256 8-phase pipeline; otherwise as 3)
- *   RR_TUNE_S3_CFG:   split cores (bf16x3 and f16x2), 1..14 (gemm_s3.hip tile table;
- *                     9..14 f16x2 only; 13 = the halo-staged stride-1 3x3 tile on
+ *   RR_TUNE_S3_CFG:   split cores (bf16x3 and f16x2), 1..15 (gemm_s3.hip tile table;
+ *                     9..15 f16x2 only; 13 = the halo-staged stride-1 3x3 tile on
  *                     v_mfma_f32_32x32x16_f16, 14 = the same on v_mfma_f32_16x16x32_f16
  *                     (the default picks 14's form for cout % 256 == 0, 13's for cout 64);
+ *                     15 = the 256x256 tile (12) as a persistent k-stream (the default
+ *                     for dense A with cout % 256 == 0, K >= 256; forced, every other
+ *                     GEMM runs the library's pick; 12 forces the one-tile-per-block form);
  *                     7 also selects the implicit-GEMM fused stem over the halo stem)
  *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of
  *                     ~1 us for every other resident block (-1 = the library's pick)

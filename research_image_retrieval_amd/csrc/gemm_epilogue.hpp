@@ -94,11 +94,24 @@ __device__ __forceinline__ float amax_acc(float am, float x) {
   const float a = __builtin_fabsf(x);
   return a < __builtin_inff() ? __builtin_fmaxf(am, a) : am;
 }
+// (the wave max by DPP row shifts as wave_sum: out-of-row sources read 0,
+// below every value; no lane-address registers, which a __shfl_xor tree
+// holds from the kernel's start in the register-bound persistent kernels)
 __device__ __forceinline__ void amax_publish(uint32_t* slots, float am, int slot) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) am = __builtin_fmaxf(am, __shfl_xor(am, o));
-  if ((threadIdx.x & 63) == 0)
-    __hip_atomic_fetch_max(slots + (slot & (RR_AMAX_SLOTS - 1)), __float_as_uint(am), __ATOMIC_RELAXED,
+  auto shr = [](float v, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), decltype(ctrl)::value, 0xf, 0xf, true));
+  };
+  am = __builtin_fmaxf(am, shr(am, std::integral_constant<int, 0x111>{}));  // row_shr:1
+  am = __builtin_fmaxf(am, shr(am, std::integral_constant<int, 0x112>{}));  // row_shr:2
+  am = __builtin_fmaxf(am, shr(am, std::integral_constant<int, 0x114>{}));  // row_shr:4
+  am = __builtin_fmaxf(am, shr(am, std::integral_constant<int, 0x118>{}));  // row_shr:8
+  const int xi = __float_as_int(am);
+  const float w = __builtin_fmaxf(
+      __builtin_fmaxf(__int_as_float(__builtin_amdgcn_readlane(xi, 15)), __int_as_float(__builtin_amdgcn_readlane(xi, 31))),
+      __builtin_fmaxf(__int_as_float(__builtin_amdgcn_readlane(xi, 47)), __int_as_float(__builtin_amdgcn_readlane(xi, 63))));
+  // (lane 0 by mbcnt: nothing held from the kernel's start for it)
+  if (__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) == 0)
+    __hip_atomic_fetch_max(slots + (slot & (RR_AMAX_SLOTS - 1)), __float_as_uint(w), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
 }
 // the max over the slots (every lane of the wave gets it)

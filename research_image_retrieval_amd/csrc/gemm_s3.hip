@@ -1216,6 +1216,365 @@ static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
   return hipGetLastError();
 }
 
+// ---- Persistent 256x256 one-accumulator tile (config 15, f16x2) -----------
+// Config 12 (8 waves of 128x64 on v_mfma_f32_32x32x16_f16, one accumulator
+// set, BK 32, dense A) as one block per CU walking its tiles as ONE k-stream,
+// as config 8 does for config 4: the B DMA one k-tile and the A loads two
+// k-tiles ahead across tile boundaries, so a tile's epilogue runs with the
+// next tile's first k-tile in LDS and its second in flight, and a fresh tile
+// never pays the cold prologue of a new block.  The epilogue goes in four
+// 64-row slabs (slab s = MFMA row tile s of every wave: rows 32 s + [0, 32)
+// and 128 + 32 s + [0, 32), so all eight waves stage every slab) through the
+// stage buffer the tile's last k-tile released, and slab s + 1's residual rows
+// are in flight while slab s is staged and stored: one exposed residual round
+// trip per tile instead of config 12's two (its two 128-row slabs each load
+// their residual after staging, and only half the waves stage each slab).
+// Same per-accumulator k order (per 16-deep k-step: a0b0, a0b1, a1b0) and
+// epilogue arithmetic as config 12: bit-identical to it.
+// Counted waits: vector-memory operations retire in issue order (stores
+// included), so each wait names how many younger operations may remain; where
+// fewer were issued (rows past M store nothing) the wait is longer, never
+// shorter.
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_n, int ntiles) {
+  static_assert((EPI & EP_SCALE) != 0, "f16x2: scaled epilogue");
+  typedef f16x8 frag_t;
+  constexpr int NP = 2, WM = 2, FM = 4, FN = 2, BK = 32, NT = 512, NW = 8;
+  constexpr int WTM = 128, WTN = 64, BM = 256, BN = 256, SL = BK / 8;
+  constexpr int A_EL = NP * BM * BK, BUF = A_EL + NP * BN * BK;
+  // stage stride: a stage also holds one 64-row slab of C (rows padded by 8
+  // floats: the 32x32 accumulator writes hit distinct banks)
+  constexpr int CS = BN + 8;
+  constexpr int STG = BUF > 64 * CS * 2 ? BUF : 64 * CS * 2;
+  constexpr int B_INS = NP * BN / (64 / SL) / NW;  // LDS-DMA instructions per wave per k-tile (4)
+  constexpr int A_RPP = NT / SL, A_CH = BM / A_RPP;  // 128 rows per pass, 2 chunks per thread
+  constexpr int A_LD = 2 * A_CH;                     // A loads per thread per k-tile
+  static_assert(B_INS * NW * (64 / SL) == NP * BN && A_CH * A_RPP == BM, "staging must tile the block");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * STG];
+  const uint32_t a_amax_w = amax_load_slot(g.a_amax);
+  float a_sc = 1.f, a_isc = 1.f, am = 0.f;
+
+  // round stagger: every block is resident from the start, so half of them
+  // (every other XCD slot) start later and the halves stay out of phase
+  if (g.stagger_sleeps > 0 && ((blockIdx.x >> 3) & 1))
+    for (int i = 0; i < g.stagger_sleeps; ++i) __builtin_amdgcn_s_sleep(32);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  const int lr = lane & 31, lh = lane >> 5;
+  const int wave_u = __builtin_amdgcn_readfirstlane(wave);  // (scalar: the amax slot at the end)
+  const int G = gridDim.x, bid = blockIdx.x;
+  const int nk = g.K / BK;
+  const int my_tiles = (ntiles - bid + G - 1) / G;
+  const int J = my_tiles * nk;  // k-tiles in this block's stream
+  // local tile tl -> origin (as config 8: virtual block bid + tl G keeps the
+  // block's XCD, then the bijective XCD remap)
+  auto tile_origin = [&](int tl, int& m0, int& n0) __attribute__((always_inline)) {
+    const int v = bid + tl * G;
+    const int xcd = v & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
+    const int tn = wgid % tiles_n, tm = wgid / tiles_n;
+    m0 = tm * BM;
+    n0 = tn * BN;
+  };
+
+  // ---- A loader: two 8-k chunks per thread (rows t / 4 and 128 + t / 4),
+  // two k-tiles ahead of the MFMAs, advancing along the stream; past the
+  // stream's end it runs into a virtual tile whose rows clamp to M - 1 ----
+  // (32-bit byte offsets from the uniform base, saddr form: 64-bit row
+  // pointers spilled this kernel; the host keeps A and C below 4 GB)
+  uint32_t a_off[A_CH];
+  int a_kt = 0, a_tl = 0;
+  auto a_tile = [&](int tl) __attribute__((always_inline)) {
+    int m0, n0;
+    tile_origin(tl, m0, n0);
+    const int t = s3_opaque(tid);
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int m = min(m0 + t / SL + i * A_RPP, g.M - 1);
+      a_off[i] = ((uint32_t)m * (uint32_t)g.lda + (uint32_t)(t % SL) * 8u) * 4u;
+    }
+  };
+  a_tile(0);
+  f32x4 ra2[2][A_CH][2];
+  auto load_a = [&](int rb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i)
+      asm volatile("global_load_dwordx4 %0, %2, %3\n\tglobal_load_dwordx4 %1, %2, %3 offset:16"
+                   : "=&v"(ra2[rb][i][0]), "=&v"(ra2[rb][i][1])
+                   : "v"(a_off[i] + (uint32_t)(a_kt * BK * 4)), "s"(g.A)
+                   : "memory");
+    if (++a_kt == nk) {
+      a_kt = 0;
+      a_tile(++a_tl);
+    }
+  };
+  u32x4 pk[A_CH][NP];
+  auto split_a = [&](int rb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) split2h8(ra2[rb][i], a_sc, pk[i][0], pk[i][1]);
+  };
+  auto write_a = [&](int buf) __attribute__((always_inline)) {
+    uint16_t* la = lds + buf * STG;
+    const int a_slot = tid % SL, a_row = tid / SL;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      const int row = a_row + i * A_RPP;
+      const int off = row * BK + pswz<BK, 2>(row, a_slot) * 8;
+#pragma unroll
+      for (int p = 0; p < NP; ++p) *reinterpret_cast<u32x4*>(la + p * BM * BK + off) = pk[i][p];
+    }
+  };
+  auto launder_a = [&](int rb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      s3_launder(ra2[rb][i][0]);
+      s3_launder(ra2[rb][i][1]);
+    }
+  };
+
+  // ---- B loader (as config 8): instruction i of a wave DMAs plane i / 2,
+  // plane rows 128 (i & 1) + 16 wave + lane / 4 ----
+  const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
+  const int b_r = wave * (64 / SL) + lane / SL;
+  const int b_sw = pswz<BK, 2>(b_r, lane % SL) * 8;  // the same for every i
+  const uint16_t* b_src = Bp;
+  int b_kt = 0, b_tl = 0;
+  auto b_tile = [&](int tl) __attribute__((always_inline)) {
+    int m0, n0;
+    tile_origin(tl, m0, n0);
+    b_src = Bp + (long long)(n0 + b_r) * g.ldb + b_sw;
+  };
+  b_tile(0);
+  auto glds_b = [&](int buf) __attribute__((always_inline)) {
+    uint16_t* lb = lds + buf * STG + A_EL;
+#pragma unroll
+    for (int i = 0; i < B_INS; ++i)
+      __builtin_amdgcn_global_load_lds((const void*)(b_src + (i >> 1) * g.b_plane + (long long)(i & 1) * (BN / 2) * g.ldb +
+                                                     b_kt * BK),
+                                       (__attribute__((address_space(3))) void*)(lb + (i * NW + wave) * (64 / SL) * BK),
+                                       16, 0, 0);
+    if (++b_kt == nk) {
+      b_kt = 0;
+      b_tile(++b_tl);
+    }
+  };
+
+  // ---- MFMAs: config 12's 16-deep k-step (st = 0, 1 of the k-tile) ----
+  f32x16 acc[FM][FN];
+  auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  };
+  zero_acc();
+  auto compute_st = [&](int cur, int st) __attribute__((always_inline)) {
+    const uint16_t* la = lds + cur * STG;
+    const uint16_t* lb = la + A_EL;
+    frag_t a[NP][FM], b[NP][FN];
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int row = wm * WTM + i * 32 + lr;
+        a[p][i] = *reinterpret_cast<const frag_t*>(la + (p * BM + row) * BK + pswz<BK, 2>(row, 2 * st + lh) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int row = wn * WTN + j * 32 + lr;
+        b[p][j] = *reinterpret_cast<const frag_t*>(lb + (p * BN + row) * BK + pswz<BK, 2>(row, 2 * st + lh) * 8);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = s3_mf32<2>(a[0][i], b[0][j], acc[i][j]);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        acc[i][j] = s3_mf32<2>(a[0][i], b[1][j], acc[i][j]);
+        acc[i][j] = s3_mf32<2>(a[1][i], b[0][j], acc[i][j]);
+      }
+  };
+
+  // ---- epilogue of local tile tl through stage buffer `buf` (free) ----
+  // Eight 32-row bands, band b = rows 128 (b & 1) + 32 (b >> 1) + [0, 32);
+  // bands 2s and 2s + 1 form slab s (MFMA row tile s of every wave), staged
+  // together.  Band b's residual rows are loaded two bands ahead (issued
+  // before band b - 2 is stored): at most three bands (48 registers) in
+  // flight -- a whole slab ahead (64) spilled the k-loop.
+  constexpr int C4 = BN / 4, HITERS = 32 * C4 / NT;  // 4 row chunks per thread and band
+  constexpr int NB = 2 * FM, RD = 2;                   // bands, residual look-ahead (bands)
+  auto epilogue = [&](int tl, int buf) __attribute__((always_inline)) {
+    int m0, n0;
+    tile_origin(tl, m0, n0);
+    const int te = s3_opaque(tid);
+    const int c40 = te % C4;
+    f32x4 bias_v[1] = {f32x4{0.f, 0.f, 0.f, 0.f}}, sc_v[1];
+    f32x4 res[RD + 1][HITERS];  // ring of bands
+    auto band_row0 = [&](int bb) { return (bb & 1) * 128 + (bb >> 1) * 32; };
+    auto load_band = [&](int bb) __attribute__((always_inline)) {
+      if constexpr ((EPI & EP_RES) != 0) {
+        // (addresses from an opaque thread index per band: hoisted, every
+        // band's addresses would be live through the epilogue and spill)
+        const int tq = s3_opaque(tid);
+        const int cq = tq % C4, rq = tq / C4;
+#pragma unroll
+        for (int it = 0; it < HITERS; ++it) {
+          const int m = min(m0 + band_row0(bb) + rq + it * (NT / C4), g.M - 1);
+          const uint32_t o = ((uint32_t)m * (uint32_t)g.ldc + (uint32_t)(n0 + cq * 4)) * 4u;
+          asm volatile("global_load_dwordx4 %0, %1, %2" : "=&v"(res[bb % (RD + 1)][it]) : "v"(o), "s"(g.residual) : "memory");
+        }
+      }
+    };
+    float* ct = reinterpret_cast<float*>(lds + buf * STG);  // [2 bands x 32 rows][CS]
+    // (wave and lane from the opaque index too: the staging addresses are
+    // loop-invariant and would otherwise be held through the k-loop)
+    const int le = te & 63, we = te >> 6;
+    auto stage = [&](int sl) __attribute__((always_inline)) {
+      float* cw = ct + ((we % WM) * 32) * CS + (we / WM) * WTN;
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) cw[acc_row<false>(0, r, le) * CS + acc_col<false>(j, r, le)] = acc[sl][j][r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+    };
+    // the bias / column scales first, by inline asm as well (a plain load's
+    // use would make hipcc wait vmcnt(0), the look-ahead bands included):
+    // older than every band, so band 0's wait covers them
+    if ((EPI & EP_BIAS) && g.bias != nullptr)
+      asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(bias_v[0]) : "v"(g.bias + n0 + c40 * 4) : "memory");
+    asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(sc_v[0]) : "v"(g.col_scale + n0 + c40 * 4) : "memory");
+    load_band(0);
+    load_band(1);
+    // vector-memory operations younger than band bb's residual at its wait:
+    // bands bb + 1 .. bb + RD (HITERS loads each, those issued) and the
+    // stores of bands bb - RD .. bb - 1 (HITERS each; fewer on a ragged
+    // tile, which only lengthens the wait)
+#pragma unroll
+    for (int bb = 0; bb < NB; ++bb) {
+      if ((bb & 1) == 0) stage(bb >> 1);
+      if (bb + RD < NB) load_band(bb + RD);
+      if constexpr ((EPI & EP_RES) != 0) {
+        const int ahead = (NB - 1 - bb < RD ? NB - 1 - bb : RD);
+        const int behind = (bb < RD ? bb : RD);
+        const int younger = HITERS * (ahead + behind);
+        // (s_waitcnt needs an immediate: the few values this unrolled loop produces)
+        switch (younger) {
+#define RR_VMW(n) \
+  case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
+          RR_VMW(0) RR_VMW(2) RR_VMW(4) RR_VMW(6) RR_VMW(8) RR_VMW(10) RR_VMW(12) RR_VMW(14)
+#undef RR_VMW
+          default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
+        }
+#pragma unroll
+        for (int it = 0; it < HITERS; ++it) asm volatile("" : "+v"(res[bb % (RD + 1)][it]));
+      } else if (bb == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      if (bb == 0) {
+        asm volatile("" : "+v"(bias_v[0]));
+        asm volatile("" : "+v"(sc_v[0]));
+        sc_v[0] *= a_isc;
+      }
+      store_slab<EPI, 2, HITERS, NT, C4, CS, 1>(g, g.C, ct + (bb & 1) * 32 * CS, bias_v, res[bb % (RD + 1)], te,
+                                                m0 + band_row0(bb), n0, sc_v, am);
+      if (bb & 1) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();  // every LDS read of the slab done (the last also frees `buf`)
+        asm volatile("" ::: "memory");
+      }
+    }
+    zero_acc();
+  };
+
+  // ---- the stream: k-tile j of the block = k-tile j % nk of local tile j / nk ----
+  load_a(0);
+  glds_b(0);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(B_INS) : "memory");  // A(0) landed
+  launder_a(0);
+  {
+    // uniform: the exponent and both powers of two stay in scalar registers
+    const int e = __builtin_amdgcn_readfirstlane(h2_exp(amax_reduce(a_amax_w)));
+    a_sc = __int_as_float((127 + e) << 23);
+    a_isc = __int_as_float((127 - e) << 23);
+  }
+  split_a(0);
+  write_a(0);
+  load_a(1);
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B(0) landed
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+  int c_kt = 0, c_tl = 0;
+  // iteration j (stage cur = j & 1 holds k-tile j, register buffer cur ^ 1
+  // holds A(j+1)): B DMA of j+1, A loads of j+2, the first k-step, the split
+  // of A(j+1) under the second, then -- after a tile's last k-tile -- its
+  // epilogue through stage cur.  A(j+1) of a tile's first k-tile was issued
+  // before the previous epilogue, whose waits already covered it: that
+  // iteration skips the A wait (it would wait for the epilogue's stores).
+  auto iter = [&](int cur, int j) __attribute__((always_inline)) {
+    glds_b(cur ^ 1);
+    load_a(cur);
+    compute_st(cur, 0);
+    if (c_kt != 0 || c_tl == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
+    launder_a(cur ^ 1);
+    split_a(cur ^ 1);
+    compute_st(cur, 1);
+    write_a(cur ^ 1);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of j+1 landed
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (++c_kt == nk) {
+      c_kt = 0;
+      epilogue(c_tl++, cur);
+    }
+    // the stream's last k-tile: the clamped tail loads (into buffer cur) are
+    // still in flight; that buffer stays live until they have landed, so no
+    // later value is allocated to it (laundering both buffers after the loop
+    // instead kept 32 registers live through every epilogue and spilled)
+    if (j == J - 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      launder_a(cur);
+    }
+  };
+  for (int j = 0; j < J; j += 2) {
+    iter(0, j);
+    if (j + 1 < J) iter(1, j + 1);
+  }
+  if constexpr ((EPI & EP_AMAX) != 0) {
+    if (g.c_amax != nullptr) amax_publish(g.c_amax, am, bid * NW + wave_u);
+  }
+}
+
+// config 15 addresses A and the residual by 32-bit byte offsets
+static bool s3q_fits(const GemmArgs& g) {
+  const long long lim = 1LL << 32;
+  return (long long)g.M * g.lda * 4 < lim && (long long)g.M * g.ldc * 4 < lim;
+}
+
+template <int EPI>
+static hipError_t launch_s3q_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
+  const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / 256;
+  const long long ntiles = tiles_m * tiles_n;
+  if (ntiles <= 0) return hipSuccess;
+  if (ntiles * (g.K / 32) > 0x7fffffffLL) return hipErrorInvalidValue;
+  // 32-bit byte offsets (checked by the caller, s3q_fits)
+  const int slots = std::max(8, n_cu & ~7);
+  const int grid = ntiles <= slots ? (int)ntiles : slots;
+  g.stagger_blocks = grid;
+  g.stagger_sleeps = ntiles > 2LL * grid ? stagger : 0;
+  hipLaunchKernelGGL((gemm_s3q_kernel<EPI>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
+  return hipGetLastError();
+}
+
 // f16x2 epilogue flag sets: the scale, the max-|C| record (skipped at run
 // time when c_amax is NULL) and the bias (zeros when NULL) always compiled
 // in; residual and ReLU select the instance
@@ -1701,6 +2060,10 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //      only; 254 VGPRs — two accumulator sets do not fit this tile): half the
 //      operand bytes per FLOP of config 4, the picked tile for N % 256 == 0
 //      except the K < 256 residual expansions
+//  15: config 12 as a persistent k-stream (gemm_s3q_kernel, f16x2, dense A,
+//      config 12's shapes; the pick there): the next tile's first k-tiles load under
+//      the epilogue, which runs in four slabs with the residual two 32-row
+//      bands ahead; bit-identical to config 12
 // (all others on v_mfma_f32_32x32x16_{bf16,f16}).  The f16x2 split is built
 // for configs 3, 4, 7, 8, 9, 10 and 11 (a forced 1, 2, 5 or 6 runs the pick).
 // Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the fastest
@@ -1797,6 +2160,26 @@ static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int
 
 template <int AM>
 static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
+  // config 15 (config 12 as a persistent k-stream): the pick for dense A
+  // with config 12's shape condition (forced 15: the same, every other GEMM
+  // on the library's pick; forced 12 runs config 12).  Measured at 1280
+  // images (profiles/r05f_cfg15_sweep.txt, interleaved): 256->1024 + residual
+  // x22 0.704 -> 0.569 ms, 512->2048 0.513 -> 0.432, 1024->256 0.409 ->
+  // 0.384, 2048->512 0.357 -> 0.351; the bench's embed 70.49 -> 69.05 ms
+  // (r05f_cfg15_e2e.txt; residual layers only: 69.17)
+  if (forced == 15 || forced == 0) {
+    if constexpr (AM == A_DENSE) {
+      if ((g.N % 256) == 0 && g.K >= 256 && s3q_fits(g)) {
+        switch (ep_flags(g) & (EP_RES | EP_RELU)) {
+          case EP_RELU: return launch_s3q_t<H2_EP | EP_RELU>(g, s, n_cu, st);
+          case EP_RES | EP_RELU: return launch_s3q_t<H2_EP | EP_RES | EP_RELU>(g, s, n_cu, st);
+          case EP_RES: return launch_s3q_t<H2_EP | EP_RES>(g, s, n_cu, st);
+          default: return launch_s3q_t<H2_EP>(g, s, n_cu, st);
+        }
+      }
+    }
+    if (forced == 15) forced = 0;
+  }
   // the halo-A tile (configs 13 / 14) is the pick for N % 256 == 0 and N == 64: the 3x3
   // 256@14 and 512@7 layers 2.7 % / 1.6 % faster than config 12 at 1280
   // images (profiles/r03t_h2_cfg_sweep.txt)
@@ -1817,6 +2200,7 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
   }
   if (forced == 13 || forced == 14) forced = 0;
   int cfg = pick_h2(g, forced);
+  // (dense A: config 15 above, config 12 as a persistent k-stream)
   // N % 256 == 0: the 256x256 one-accumulator tile (config 12) everywhere but
   // the short-K residual expansions (K < 256: their epilogue dominates and the
   // persistent k-stream, config 8, hides part of it).  Measured per R101 layer

@@ -144,7 +144,7 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.lp_cfg = value;
       return RR_OK;
     case RR_TUNE_S3_CFG:
-      if (value < 0 || value > 14) break;
+      if (value < 0 || value > 15) break;
       h->tune.s3_cfg = value;
       return RR_OK;
     case RR_TUNE_S3_STAGGER:
@@ -168,7 +168,7 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.halo_mf = value;
       return RR_OK;
     case RR_TUNE_S3_CFG_RES:
-      if (value < 0 || value > 14) break;
+      if (value < 0 || value > 15) break;
       h->tune.s3_cfg_res = value;
       return RR_OK;
     default:

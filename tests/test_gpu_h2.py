@@ -256,6 +256,32 @@ def test_h2_persistent_tile_bit_identical(cuda):
     assert torch.equal(y9[4], y9[9])
 
 
+@pytest.mark.parametrize("b,h,w,cin,cout,res,relu", [
+    (10, 56, 56, 256, 1024, True, True),   # the residual expansion shape: 490 tiles, ~2 per block, ragged M
+    (4, 67, 67, 256, 1024, True, False),   # residual without ReLU, ragged
+    (5, 80, 80, 1024, 512, False, True),   # K = 1024 reduction, 250 x 2 tiles
+    (2, 9, 11, 288, 256, True, True),      # K = 288: nine k-tiles, one tile (an odd stream length)
+    (1, 3, 5, 512, 256, False, False),     # one partial tile, no epilogue options
+])
+def test_h2_persistent_256_tile_bit_identical(cuda, b, h, w, cin, cout, res, relu):
+    """Config 15 (config 12 as a persistent k-stream, four-slab epilogue with
+    the residual two bands ahead) keeps config 12's per-accumulator k order and
+    epilogue arithmetic: identical bits and the same max-|y| record, with
+    several tiles per block (the stream across tile boundaries) and ragged M."""
+    x, wt, bias, r, _, _ = _conv_case(cuda, b, h, w, cin, cout, 1, 1, 0, res, seed=17)
+    xd, rd = x.to(cuda), (r.to(cuda) if res else None)
+    cw = ops.H2Conv(wt.to(cuda))
+    outs, amax = {}, {}
+    for cfg in (12, 15):
+        rec = ops.amax_records(2, cuda)
+        ops.amax_f32(xd, rec[0])
+        with ops.tuning(0, s3_cfg=cfg):
+            y = ops.conv2d_h2(xd, rec[0], cw, bias.to(cuda), 1, 0, rd, relu, rec[1])
+        outs[cfg], amax[cfg] = y.cpu(), ops.amax_value(rec[1])
+    assert torch.equal(outs[12], outs[15])
+    assert amax[12] == amax[15] == float(outs[15].abs().max())
+
+
 @pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res,cfg", [
     (3, 29, 31, 256, 1024, 1, 1, 0, True, 12),   # 1x1 + residual (dense A), ragged last tile
     (2, 14, 14, 1024, 256, 1, 1, 0, False, 12),  # 1x1, K = 1024
