@@ -50,8 +50,11 @@ __device__ __forceinline__ float quick_gelu(float x) {
 // EP_STATS / EP_LNFOLD (the bf16 ViT linears, 256-column tiles): the
 // LayerNorm partials + bf16 copy of C, and the LayerNorm folded into a
 // consumer's epilogue (GemmArgs stats_out / stats_in).
+// EP_SC1: fp32 C stored with sc1 (the line leaves the XCD's L2 instead of
+// staying in it, MI355X_MICROARCH.md: a streamed output then does not evict
+// the operand tiles other blocks of the XCD still re-read)
 enum { EP_BIAS = 1, EP_RES = 2, EP_RELU = 4, EP_GELU = 8, EP_BF16 = 16, EP_SCALE = 32, EP_AMAX = 64, EP_STATS = 128,
-       EP_LNFOLD = 256 };
+       EP_LNFOLD = 256, EP_SC1 = 512 };
 inline int ep_flags(const GemmArgs& g) {
   return (g.bias != nullptr ? EP_BIAS : 0) | (g.residual != nullptr ? EP_RES : 0) |
          (g.relu == 1 ? EP_RELU : g.relu == 2 ? EP_GELU : 0) | (g.out_bf16 ? EP_BF16 : 0) |
@@ -228,6 +231,12 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
     if (obf) {
       const bf16x4 ob = {(__bf16)v[0], (__bf16)v[1], (__bf16)v[2], (__bf16)v[3]};
       *reinterpret_cast<bf16x4*>(reinterpret_cast<uint16_t*>(Cb) + o) = ob;
+    } else if constexpr (FIXED && (FL & EP_SC1) != 0) {
+      // (the s_nop: a VALU write to the data registers of a store wider than
+      // 8 B needs a wait state after it, which hipcc inserts for its own
+      // stores but not after an inline-asm one; without it the registers
+      // were overwritten before the store read them: wrong outputs)
+      asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(Cb + o), "v"(v) : "memory");
     } else {
       *reinterpret_cast<f32x4*>(Cb + o) = v;
     }

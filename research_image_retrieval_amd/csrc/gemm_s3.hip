@@ -56,13 +56,17 @@ __device__ __forceinline__ const f32x4* s3_zero_page() { return s3_zero_src; }
 // s_memtime deltas of the k-loop phases of the f16x2 kernels, summed over
 // every wave into s3_phase_sum[kernel][phase] (rr_debug_phases reads them).
 // Phases: 0 issue loads, 1 first MFMA part, 2 mid wait, 3 split + second
-// MFMA part, 4 end wait, 5 barrier, 6 epilogue, 7 prologue.  The timers cost
-// a few % and are compiled out of the product library.
+// MFMA part, 4 end wait, 5 barrier, 6 epilogue, 7 prologue (kernel 0: the
+// one-tile kernels, 1: config 8).  Kernel 2 (config 15): 0 issue + first
+// k-step, 1 mid wait, 2 split + second k-step, 3 end wait + barrier, 4
+// epilogue staging (+ its barrier), 5 epilogue residual waits, 6 epilogue
+// stores (+ barriers), 7 prologue.  The timers cost a few % and are compiled
+// out of the product library.
 #ifndef RR_S3_PHASES
 #define RR_S3_PHASES 0
 #endif
 #if RR_S3_PHASES
-__device__ unsigned long long s3_phase_sum[2][8];
+__device__ unsigned long long s3_phase_sum[3][8];
 struct S3Phases {
   unsigned long long t, acc[8];
   __device__ __forceinline__ S3Phases() {
@@ -1409,6 +1413,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
   // flight -- a whole slab ahead (64) spilled the k-loop.
   constexpr int C4 = BN / 4, HITERS = 32 * C4 / NT;  // 4 row chunks per thread and band
   constexpr int NB = 2 * FM, RD = 2;                   // bands, residual look-ahead (bands)
+  RR_PH_DECL
   auto epilogue = [&](int tl, int buf) __attribute__((always_inline)) {
     int m0, n0;
     tile_origin(tl, m0, n0);
@@ -1427,7 +1432,10 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
         for (int it = 0; it < HITERS; ++it) {
           const int m = min(m0 + band_row0(bb) + rq + it * (NT / C4), g.M - 1);
           const uint32_t o = ((uint32_t)m * (uint32_t)g.ldc + (uint32_t)(n0 + cq * 4)) * 4u;
-          asm volatile("global_load_dwordx4 %0, %1, %2" : "=&v"(res[bb % (RD + 1)][it]) : "v"(o), "s"(g.residual) : "memory");
+          if constexpr ((EPI & EP_SC1) != 0)  // streamed: nt
+            asm volatile("global_load_dwordx4 %0, %1, %2 nt" : "=&v"(res[bb % (RD + 1)][it]) : "v"(o), "s"(g.residual) : "memory");
+          else
+            asm volatile("global_load_dwordx4 %0, %1, %2" : "=&v"(res[bb % (RD + 1)][it]) : "v"(o), "s"(g.residual) : "memory");
         }
       }
     };
@@ -1444,6 +1452,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
+      RR_PH(4);
     };
     // the bias / column scales first, by inline asm as well (a plain load's
     // use would make hipcc wait vmcnt(0), the look-ahead bands included):
@@ -1453,18 +1462,19 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
     asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(sc_v[0]) : "v"(g.col_scale + n0 + c40 * 4) : "memory");
     load_band(0);
     load_band(1);
-    // vector-memory operations younger than band bb's residual at its wait:
-    // bands bb + 1 .. bb + RD (HITERS loads each, those issued) and the
-    // stores of bands bb - RD .. bb - 1 (HITERS each; fewer on a ragged
-    // tile, which only lengthens the wait)
+    // band bb's wait: vmcnt(the loads issued after it: bands bb + 1 ..
+    // bb + RD, HITERS each).  The stores issued after it (bands bb - RD ..
+    // bb - 1) are not counted: loads return in order among themselves, but
+    // nothing is assumed about stores against loads, so the wait also covers
+    // those stores (measured free: 0.584 vs 0.590 ms counting them,
+    // profiles/r05j_probe.txt)
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
       if ((bb & 1) == 0) stage(bb >> 1);
       if (bb + RD < NB) load_band(bb + RD);
       if constexpr ((EPI & EP_RES) != 0) {
         const int ahead = (NB - 1 - bb < RD ? NB - 1 - bb : RD);
-        const int behind = (bb < RD ? bb : RD);
-        const int younger = HITERS * (ahead + behind);
+        const int younger = HITERS * ahead;
         // (s_waitcnt needs an immediate: the few values this unrolled loop produces)
         switch (younger) {
 #define RR_VMW(n) \
@@ -1478,6 +1488,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
       } else if (bb == 0) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
+      RR_PH(5);
       if (bb == 0) {
         asm volatile("" : "+v"(bias_v[0]));
         asm volatile("" : "+v"(sc_v[0]));
@@ -1490,6 +1501,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
         __builtin_amdgcn_s_barrier();  // every LDS read of the slab done (the last also frees `buf`)
         asm volatile("" ::: "memory");
       }
+      RR_PH(6);
     }
     zero_acc();
   };
@@ -1523,15 +1535,19 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
     glds_b(cur ^ 1);
     load_a(cur);
     compute_st(cur, 0);
+    RR_PH(0);
     if (c_kt != 0 || c_tl == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
     launder_a(cur ^ 1);
+    RR_PH(1);
     split_a(cur ^ 1);
     compute_st(cur, 1);
     write_a(cur ^ 1);
+    RR_PH(2);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD) : "memory");  // B DMA of j+1 landed
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    RR_PH(3);
     if (++c_kt == nk) {
       c_kt = 0;
       epilogue(c_tl++, cur);
@@ -1545,10 +1561,12 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
       launder_a(cur);
     }
   };
+  RR_PH(7);
   for (int j = 0; j < J; j += 2) {
     iter(0, j);
     if (j + 1 < J) iter(1, j + 1);
   }
+  RR_PH_FLUSH(2);
   if constexpr ((EPI & EP_AMAX) != 0) {
     if (g.c_amax != nullptr) amax_publish(g.c_amax, am, bid * NW + wave_u);
   }
@@ -2170,10 +2188,17 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
   if (forced == 15 || forced == 0) {
     if constexpr (AM == A_DENSE) {
       if ((g.N % 256) == 0 && g.K >= 256 && s3q_fits(g)) {
+        // residual epilogues streamed (EP_SC1): output stores sc1, residual
+        // loads nt -- neither keeps XCD L2 lines the row tile's other column
+        // tiles still re-read (256->1024 + residual 0.604 -> 0.579 ms, 512->2048
+        // 0.470 -> 0.466; the embed 69.82 -> 69.47 ms with every config-15
+        // layer streamed).  Without a residual the plain policy stays: streamed
+        // stores there ran 1024->256 0.395 -> 0.406 ms (profiles/r05i_sweep.txt,
+        // r05j_probe2.txt)
         switch (ep_flags(g) & (EP_RES | EP_RELU)) {
           case EP_RELU: return launch_s3q_t<H2_EP | EP_RELU>(g, s, n_cu, st);
-          case EP_RES | EP_RELU: return launch_s3q_t<H2_EP | EP_RES | EP_RELU>(g, s, n_cu, st);
-          case EP_RES: return launch_s3q_t<H2_EP | EP_RES>(g, s, n_cu, st);
+          case EP_RES | EP_RELU: return launch_s3q_t<H2_EP | EP_RES | EP_RELU | EP_SC1>(g, s, n_cu, st);
+          case EP_RES: return launch_s3q_t<H2_EP | EP_RES | EP_SC1>(g, s, n_cu, st);
           default: return launch_s3q_t<H2_EP>(g, s, n_cu, st);
         }
       }
@@ -2603,10 +2628,10 @@ int launch_amax(rr_handle_s* h, const float* x, long long n, uint32_t* slots, hi
 }
 
 #if RR_S3_PHASES
-// diagnostic build: read and clear the phase sums ([2][8] cycles)
+// diagnostic build: read and clear the phase sums ([3][8] cycles)
 int debug_phases(unsigned long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(s3_phase_sum), sizeof(s3_phase_sum)) != hipSuccess) return RR_EHIP;
-  unsigned long long z[2][8] = {};
+  unsigned long long z[3][8] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(s3_phase_sum), z, sizeof(z)) == hipSuccess ? RR_OK : RR_EHIP;
 }
 #endif

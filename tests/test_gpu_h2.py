@@ -272,7 +272,7 @@ def test_h2_persistent_256_tile_bit_identical(cuda, b, h, w, cin, cout, res, rel
     xd, rd = x.to(cuda), (r.to(cuda) if res else None)
     cw = ops.H2Conv(wt.to(cuda))
     outs, amax = {}, {}
-    for cfg in (12, 15):
+    for cfg in (12, 15):  # 15 with a residual: sc1 output stores, nt residual loads
         rec = ops.amax_records(2, cuda)
         ops.amax_f32(xd, rec[0])
         with ops.tuning(0, s3_cfg=cfg):

@@ -118,7 +118,7 @@ def test_handle_device_and_tuning_validation(cuda):
     assert L.rr_get_device(h, ctypes.byref(d)) == 0 and d.value == cuda.index
     assert L.rr_set_tuning(h, 99, 1) == _lib.RR_EINVAL and b"unknown key" in L.rr_last_error(h)
     assert L.rr_set_tuning(h, _lib.TUNE_GEMM_CFG, 23) == _lib.RR_EINVAL
-    assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG, 15) == _lib.RR_EINVAL
+    assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG, 16) == _lib.RR_EINVAL
     for retired in (6, 7, 12):  # sweep_order, sweep_pf, lp_il (ABI 5)
         assert L.rr_set_tuning(h, retired, 0) == _lib.RR_EINVAL and b"unknown key" in L.rr_last_error(h)
     assert L.rr_set_tuning(h, _lib.TUNE_LP_CFG, 6) == _lib.RR_EINVAL
@@ -126,7 +126,7 @@ def test_handle_device_and_tuning_validation(cuda):
     assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_IL, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_CONV_IL, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_HALO_MF, 2) == _lib.RR_EINVAL
-    assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG_RES, 15) == _lib.RR_EINVAL
+    assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG_RES, 16) == _lib.RR_EINVAL
     for key in (_lib.TUNE_GEMM_CFG, _lib.TUNE_GEMM_BK, _lib.TUNE_LP_CFG, _lib.TUNE_S3_CFG, _lib.TUNE_SWEEP_MF16,
                 _lib.TUNE_SWEEP_IL, _lib.TUNE_CONV_IL, _lib.TUNE_HALO_MF, _lib.TUNE_S3_CFG_RES):
         assert L.rr_set_tuning(h, key, 0) == 0

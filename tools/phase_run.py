@@ -19,9 +19,12 @@ fn = L.rr_debug_phases
 fn.argtypes = [ctypes.c_void_p]
 fn.restype = ctypes.c_int
 NAMES = ["issue", "mfma1", "wait_mid", "split+mfma2", "wait_end", "barrier", "epilogue", "prologue"]
-SHAPES = [(14, 256, 1024, 1, 1, 1), (14, 1024, 256, 1, 1, 0), (14, 256, 256, 3, 1, 0), (28, 128, 512, 1, 1, 1),
-          (56, 64, 256, 1, 1, 1), (7, 512, 512, 3, 1, 0)]
-buf = (ctypes.c_ulonglong * 16)()
+# config 15 (gemm_s3q_kernel, kernel 2): its own phase map
+NAMES_Q = ["issue+step0", "wait_mid", "split+step1", "wait_end+barrier", "epi_stage", "epi_res_wait", "epi_store",
+           "prologue"]
+SHAPES = [(14, 256, 1024, 1, 1, 1), (14, 1024, 256, 1, 1, 0), (7, 512, 2048, 1, 1, 1), (14, 256, 256, 3, 1, 0),
+          (28, 128, 512, 1, 1, 1), (56, 64, 256, 1, 1, 1), (7, 512, 512, 3, 1, 0)]
+buf = (ctypes.c_ulonglong * 24)()
 for h, cin, cout, k, s, res in SHAPES:
     p = k // 2
     x = torch.relu(torch.randn(B, h, h, cin, device=dev))
@@ -43,11 +46,11 @@ for h, cin, cout, k, s, res in SHAPES:
     en.record()
     torch.cuda.synchronize()
     fn(ctypes.cast(buf, ctypes.c_void_p))
-    for kern in (0, 1):
+    for kern in (0, 1, 2):
         v = [buf[kern * 8 + i] for i in range(8)]
         tot = sum(v)
         if tot == 0:
             continue
-        share = " ".join(f"{n} {x / tot:.3f}" for n, x in zip(NAMES, v))
+        share = " ".join(f"{n} {x / tot:.3f}" for n, x in zip(NAMES_Q if kern == 2 else NAMES, v))
         print(f"h{h} {cin}->{cout} k{k} r{res}: {st.elapsed_time(en) / 3:.3f} ms  "
-              f"{'s3p' if kern else 'tile'}: {share}", flush=True)
+              f"{('tile', 's3p', 's3q')[kern]}: {share}", flush=True)

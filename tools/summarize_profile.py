@@ -22,9 +22,10 @@ def cls_of(name):
     """Kernel class as bench.py's timer classes: gemm_kernel<WM, WN, FM, FN,
     AMODE, EMODE, ...> by its epilogue (EMODE 2 = cosine filter sweep, 1 =
     seed scores, 0 = stored C: convs / linears); gemm_s3_kernel and the
-    persistent gemm_s3p_kernel and the halo-staged gemm_h2_halo_kernel / stem_pool_halo_kernel = convs."""
-    if ("gemm_s3_kernel" in name or "gemm_s3p_kernel" in name or "gemm_h2_halo_kernel" in name
-            or "stem_pool_halo_kernel" in name):
+    persistent gemm_s3p_kernel / gemm_s3q_kernel, the halo-staged gemm_h2_halo_kernel /
+    stem_pool_halo_kernel and the block seam seam_h2_kernel = convs."""
+    if ("gemm_s3_kernel" in name or "gemm_s3p_kernel" in name or "gemm_s3q_kernel" in name
+            or "gemm_h2_halo_kernel" in name or "stem_pool_halo_kernel" in name or "seam_h2_kernel" in name):
         return "conv_gemm"
     m = re.search(r"gemm_8p_kernel<(\d)>", name)
     if m:  # the 8-phase bf16 sweep (filter / seed scores only)
