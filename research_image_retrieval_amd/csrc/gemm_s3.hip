@@ -1072,7 +1072,10 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
           for (int it = 0; it < HITERS; ++it) {
             const int m = min(m0 + q * 64 + sl * 32 + r0 + it * (NT / C4), g.M - 1);
             const float* p = g.residual + (long long)m * g.ldc + n0 + c40 * 4;
-            asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(res[sl][q][it]) : "v"(p) : "memory");
+            if constexpr ((EPI & EP_SC1) != 0)  // streamed (EP_SC1): nt
+              asm volatile("global_load_dwordx4 %0, %1, off nt" : "=&v"(res[sl][q][it]) : "v"(p) : "memory");
+            else
+              asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(res[sl][q][it]) : "v"(p) : "memory");
           }
       }
     };
@@ -2022,10 +2025,13 @@ static bool s3_persist_ok(const GemmArgs& g, int amode) {
 template <int SP>
 static hipError_t launch_s3p(const GemmArgs& g, hipStream_t s, int n_cu, int st) {
   if constexpr (SP == 2) {
+    // residual epilogues streamed (EP_SC1, as config 15's): 128->512 + residual
+    // x3 0.908 -> 0.877 ms, 64->256 x2 1.701 -> 1.707; the embed 69.09 -> 69.06
+    // ms (profiles/r05k_sweep.txt, r05k_e2e.txt)
     switch (ep_flags(g) & (EP_RES | EP_RELU)) {
       case EP_RELU: return launch_s3p_t<H2_EP | EP_RELU, 2>(g, s, n_cu, st);
-      case EP_RES | EP_RELU: return launch_s3p_t<H2_EP | EP_RES | EP_RELU, 2>(g, s, n_cu, st);
-      case EP_RES: return launch_s3p_t<H2_EP | EP_RES, 2>(g, s, n_cu, st);
+      case EP_RES | EP_RELU: return launch_s3p_t<H2_EP | EP_RES | EP_RELU | EP_SC1, 2>(g, s, n_cu, st);
+      case EP_RES: return launch_s3p_t<H2_EP | EP_RES | EP_SC1, 2>(g, s, n_cu, st);
       default: return launch_s3p_t<H2_EP, 2>(g, s, n_cu, st);
     }
   } else {
