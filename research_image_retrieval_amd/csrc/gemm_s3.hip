@@ -60,13 +60,15 @@ __device__ __forceinline__ const f32x4* s3_zero_page() { return s3_zero_src; }
 // one-tile kernels, 1: config 8).  Kernel 2 (config 15): 0 issue + first
 // k-step, 1 mid wait, 2 split + second k-step, 3 end wait + barrier, 4
 // epilogue staging (+ its barrier), 5 epilogue residual waits, 6 epilogue
-// stores (+ barriers), 7 prologue.  The timers cost a few % and are compiled
-// out of the product library.
+// stores (+ barriers), 7 prologue.  Kernel 3 (the halo tile): 0 B DMA + halo
+// pass issue / split, 1 MFMAs (+ fragment reads), 2 end wait, 3 barrier, 6
+// epilogue, 7 prologue.  The timers cost a few % and are compiled out of the
+// product library.
 #ifndef RR_S3_PHASES
 #define RR_S3_PHASES 0
 #endif
 #if RR_S3_PHASES
-__device__ unsigned long long s3_phase_sum[3][8];
+__device__ unsigned long long s3_phase_sum[4][8];
 struct S3Phases {
   unsigned long long t, acc[8];
   __device__ __forceinline__ S3Phases() {
@@ -1684,13 +1686,14 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   const int a_slot = tid % SL, a_row = tid / SL;
   constexpr int RA_N = TPK == 1 ? 1 : A_PASS;
   f32x4 ra[RA_N][2];
-  auto load_pass = [&](int c, int p) {
+  auto load_pass_to = [&](int c, int p, f32x4(&r)[2]) {
     const int hr = a_row + p * (NT / SL);
     const long long q = (long long)m0 - hoff + hr;
     const bool ok = hr < HALO_HR && q >= 0 && q < g.M;
     const f32x4* src = ok ? reinterpret_cast<const f32x4*>(g.A + q * g.Cin + c * BK + a_slot * 8) : s3_zero_page();
-    s3_load2<1>(src, ra[TPK == 1 ? 0 : p]);
+    s3_load2<1>(src, r);
   };
+  auto load_pass = [&](int c, int p) { load_pass_to(c, p, ra[TPK == 1 ? 0 : p]); };
   auto launder_pass = [&]() {
 #pragma unroll
     for (int p = 0; p < RA_N; ++p) {
@@ -1698,10 +1701,10 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
       s3_launder(ra[p][1]);
     }
   };
-  auto store_pass = [&](int buf, int p) {
+  auto store_pass_from = [&](int buf, int p, const f32x4(&r)[2]) {
     const int hr = a_row + p * (NT / SL);
     u32x4 p0, p1;
-    split2h8(ra[TPK == 1 ? 0 : p], a_sc, p0, p1);
+    split2h8(r, a_sc, p0, p1);
     if (hr < HALO_HR) {
       uint16_t* la = lds + buf * A_EL;
       const int off = hr * BK + hswz(hr, a_slot) * 8;
@@ -1709,6 +1712,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
       *reinterpret_cast<u32x4*>(la + HRA * BK + off) = p1;
     }
   };
+  auto store_pass = [&](int buf, int p) { store_pass_from(buf, p, ra[TPK == 1 ? 0 : p]); };
 
   // ---- B planes: LDS-DMA, instruction i of a wave fills plane rows
   // prow = (i NW + wave) B_RPI + lane / 4 of the [2][BN] stage (N % BN == 0:
@@ -1887,18 +1891,27 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   };
 
   // ---- prologue: the zero rows, slice 0's halo (pass by pass), k-tile 0's B ----
+  RR_PH_DECL
   if (tid < 16) {
     // row HALO_HR of both planes of both buffers: 4 x 64 B, 16 B per thread
     const int buf = tid >> 3, p = (tid >> 2) & 1, sl = tid & 3;
     *reinterpret_cast<u32x4*>(lds + buf * A_EL + (p * HRA + HALO_HR) * BK + sl * 8) = u32x4{0u, 0u, 0u, 0u};
   }
   glds_b(0, 0);
+  {
+    // slice 0's halo: every pass's loads first, one wait (three waits in
+    // turn cost a tile three HBM round trips before its first MFMA); the
+    // accumulators are still constant zeros here, so the registers are free
+    f32x4 rp[A_PASS][2];
 #pragma unroll
-  for (int p = 0; p < A_PASS; ++p) {
-    load_pass(0, p);
+    for (int p = 0; p < A_PASS; ++p) load_pass_to(0, p, rp[p]);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    launder_pass();
-    if (p == 0) {
+#pragma unroll
+    for (int p = 0; p < A_PASS; ++p) {
+      s3_launder(rp[p][0]);
+      s3_launder(rp[p][1]);
+    }
+    {
       // the record's wave max, with shuffle addresses from an opaque lane id:
       // amax_reduce's would be shared with the epilogue's amax_publish and held
       // (spilled) through the whole k-loop
@@ -1913,7 +1926,8 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
       a_sc = __int_as_float((127 + e) << 23);
       a_isc = __int_as_float((127 - e) << 23);
     }
-    store_pass(0, p);
+#pragma unroll
+    for (int p = 0; p < A_PASS; ++p) store_pass_from(0, p, rp[p]);
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
@@ -1925,6 +1939,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   // start of tap p + 1's (that buffer's last reader was slice c - 1) ----
   static_assert(A_PASS < 9, "the halo passes must fit in one slice's taps");
   int c = 0, tg = 0;
+  RR_PH(7);
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = c + 1 < nch;
     if constexpr (!IL) glds_b(min(kt + 1, nk - 1), (kt + 1) & 1);
@@ -1942,13 +1957,17 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
         for (int p = 0; p < A_PASS; ++p) load_pass(c + 1, p);
       }
     }
+    RR_PH(0);
 #pragma unroll
     for (int u = 0; u < TPK; ++u) compute(c & 1, kt & 1, tg * TPK + u, u, min(kt + 1, nk - 1));
+    RR_PH(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next B (and a halo pass)
     launder_pass();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    RR_PH(2);
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
+    RR_PH(3);
     if (++tg == ngrp) {
       tg = 0;
       ++c;
@@ -1967,6 +1986,8 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   }
   epilogue_store<WM, WN, FM, FN, LDS_U16 / 2, (bool)MF, EPI>(g, g.C, acc, reinterpret_cast<float*>(lds), m0, n0,
                                                              a_isc);
+  RR_PH(6);
+  RR_PH_FLUSH(3);
 }
 
 // config 13 serves: f16x2, conv A, 3x3 stride 1 pad 1 (output = input size),
@@ -2634,10 +2655,10 @@ int launch_amax(rr_handle_s* h, const float* x, long long n, uint32_t* slots, hi
 }
 
 #if RR_S3_PHASES
-// diagnostic build: read and clear the phase sums ([3][8] cycles)
+// diagnostic build: read and clear the phase sums ([4][8] cycles)
 int debug_phases(unsigned long long* out) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(s3_phase_sum), sizeof(s3_phase_sum)) != hipSuccess) return RR_EHIP;
-  unsigned long long z[3][8] = {};
+  unsigned long long z[4][8] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(s3_phase_sum), z, sizeof(z)) == hipSuccess ? RR_OK : RR_EHIP;
 }
 #endif

@@ -315,4 +315,8 @@ int launch_prefilter_rescore(rr_handle_s* h, unsigned long long* cand, long long
 int launch_merge(rr_handle_s* h, const float* ps, const long long* pi, int nparts, int nq, int kin,
                  int kout, float* os, long long* oi, hipStream_t s);
 
+// gemm_lpp.hip: the bf16 stored-C GEMM as a persistent 256x256 k-stream
+bool lpp_eligible(const GemmArgs& g);
+hipError_t launch_lpp(const GemmArgs& g, hipStream_t s, int n_cu);
+
 }  // namespace rr

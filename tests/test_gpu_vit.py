@@ -307,3 +307,44 @@ def test_linear_bf16_ln_argument_checks_and_edges(cuda):
     out = ops.linear_bf16_ln_fold(yb1, st1, wf, csum, bf).float()
     ref = ops.linear_bf16(ops.layernorm_bf16(y1, gam, bet), w, bias).float()
     assert (out - ref).abs().max().item() <= 0.05 * ref.abs().mean().item()
+
+
+@pytest.mark.parametrize("kind", ["bf16_out", "residual", "gelu", "produce", "fold", "fold_gelu"])
+def test_linear_bf16_persistent_tile_bit_identical(cuda, kind):
+    """The default for the ViT linears with K <= 1024 (gemm_lpp.hip: the
+    256x256 bf16 tile as a persistent k-stream, slab epilogue, residual two
+    bands ahead) keeps the one-tile kernel's (lp_cfg 3) fragments,
+    per-accumulator MFMA order and epilogue arithmetic: identical bits for
+    every ViT linear epilogue, with several tiles per block and a ragged last
+    row tile."""
+    g = torch.Generator().manual_seed(23)
+    n = 2304 if kind in ("bf16_out", "gelu", "fold", "fold_gelu") else 768
+    m = 8000 + 37 if n == 2304 else 30001  # > 256 tiles either way
+    k = 768
+    x = (torch.randn(m, k, generator=g) + 0.3).to(cuda)
+    w = (torch.randn(n, k, generator=g) * k ** -0.5).to(cuda)
+    bias = (torch.randn(n, generator=g) * 0.1).to(cuda)
+    r = torch.randn(m, n, generator=g).to(cuda)
+    gam, bet = (1 + 0.1 * torch.randn(k, generator=g)).to(cuda), (0.1 * torch.randn(k, generator=g)).to(cuda)
+    xb16, wb16 = x.bfloat16().contiguous(), w.bfloat16().contiguous()
+
+    def run():
+        if kind == "bf16_out":
+            return (ops.linear_bf16(xb16, wb16, bias, out_bf16=True),)
+        if kind == "residual":
+            return (ops.linear_bf16(xb16, wb16, bias, residual=r),)
+        if kind == "gelu":
+            return (ops.linear_bf16(xb16, wb16, bias, act=2, out_bf16=True),)
+        if kind == "produce":
+            return ops.linear_bf16_ln_produce(xb16, wb16, bias, r)
+        xb, st = ops.ln_partials_bf16(x)
+        wf, cs, bf = ops.ln_fold_weights(w, bias, gam, bet)
+        return (ops.linear_bf16_ln_fold(xb, st, wf, cs, bf, act=2 if kind == "fold_gelu" else 0),)
+
+    with ops.tuning(0, lp_cfg=3):
+        ref = run()
+    out = run()
+    for a, b in zip(ref, out):
+        assert a.shape == b.shape and a.dtype == b.dtype
+        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
+                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32)), kind

@@ -22,9 +22,11 @@ NAMES = ["issue", "mfma1", "wait_mid", "split+mfma2", "wait_end", "barrier", "ep
 # config 15 (gemm_s3q_kernel, kernel 2): its own phase map
 NAMES_Q = ["issue+step0", "wait_mid", "split+step1", "wait_end+barrier", "epi_stage", "epi_res_wait", "epi_store",
            "prologue"]
-SHAPES = [(14, 256, 1024, 1, 1, 1), (14, 1024, 256, 1, 1, 0), (7, 512, 2048, 1, 1, 1), (14, 256, 256, 3, 1, 0),
-          (28, 128, 512, 1, 1, 1), (56, 64, 256, 1, 1, 1), (7, 512, 512, 3, 1, 0)]
-buf = (ctypes.c_ulonglong * 24)()
+# the halo tile (kernel 3)
+NAMES_H = ["issue", "mfma", "wait_end", "barrier", "-", "-", "epilogue", "prologue"]
+SHAPES = [(14, 256, 256, 3, 1, 0), (7, 512, 512, 3, 1, 0), (56, 64, 64, 3, 1, 0), (14, 256, 1024, 1, 1, 1),
+          (14, 1024, 256, 1, 1, 0), (28, 128, 512, 1, 1, 1)]
+buf = (ctypes.c_ulonglong * 32)()
 for h, cin, cout, k, s, res in SHAPES:
     p = k // 2
     x = torch.relu(torch.randn(B, h, h, cin, device=dev))
@@ -46,11 +48,11 @@ for h, cin, cout, k, s, res in SHAPES:
     en.record()
     torch.cuda.synchronize()
     fn(ctypes.cast(buf, ctypes.c_void_p))
-    for kern in (0, 1, 2):
+    for kern in (0, 1, 2, 3):
         v = [buf[kern * 8 + i] for i in range(8)]
         tot = sum(v)
         if tot == 0:
             continue
-        share = " ".join(f"{n} {x / tot:.3f}" for n, x in zip(NAMES_Q if kern == 2 else NAMES, v))
+        share = " ".join(f"{n} {x / tot:.3f}" for n, x in zip((NAMES, NAMES, NAMES_Q, NAMES_H)[kern], v))
         print(f"h{h} {cin}->{cout} k{k} r{res}: {st.elapsed_time(en) / 3:.3f} ms  "
-              f"{('tile', 's3p', 's3q')[kern]}: {share}", flush=True)
+              f"{('tile', 's3p', 's3q', 'halo')[kern]}: {share}", flush=True)
