@@ -17,11 +17,13 @@
 // and per-accumulator MFMA sequence (v_mfma_f32_16x16x32_bf16, one per
 // sub-tile per 32-deep k-step, k-steps in order) and the same epilogue
 // arithmetic (store_slab) as the one-tile kernel: bit-identical results.
-// Measured (tools/vit_lin_ab.py, 1280 images; profiles/r05o_vitlin.txt):
-// in-proj 1.091 -> 1.062 ms, out-proj 0.603 -> 0.586, c_fc 1.571 -> 1.548,
-// but c_proj (K = 3072) 1.265 -> 1.402; so it serves K <= 1024.  A ring of
-// four 32-deep stages with the DMA three k-tiles ahead was slower on all
-// four (c_fc 1.744, c_proj 1.498 ms, r05p_vitlin.txt): twice the barriers.
+// Measured against the one-tile kernel (tools/vit_lin_ab.py, 1280 images,
+// profiles/r05s_vitlin.txt): in-proj 1.101 -> 1.039 ms, out-proj 0.602 ->
+// 0.577, c_fc 1.570 -> 1.509 (step 1's fragments read among step 0's MFMAs;
+// without that, 1.072 / 0.589 / 1.570).  c_proj (K = 3072) ran 1.291 -> 1.343
+// (r05t_vitlin_k4096.txt), so the kernel serves K <= 1024.  A ring of four
+// 32-deep stages with the DMA three k-tiles ahead was slower on all four
+// (c_fc 1.744, c_proj 1.498 ms, r05p_vitlin.txt): twice the barriers.
 //
 // Operands: A [M][K] bf16 (lda), B [N][K] bf16 (ldb), K % 64 == 0, K <= 1024,
 // N % 256 == 0 (lpp_eligible).  Rows past M read row M - 1 (never stored).
@@ -116,37 +118,52 @@ __global__ __launch_bounds__(512, 1) void gemm_lpp_kernel(GemmArgs g, int tiles_
         for (int t = 0; t < 4; ++t) acc4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
   zero_acc();
+  // the k-tile's two 32-deep k-steps (lane group lg: k 8 lg .. +7 of slot
+  // 4 st + lg); step 1's fragments are read among step 0's MFMAs (the
+  // one-tile kernel's order), step 0's before them (the SIMD's other wave
+  // covers that latency)
   auto compute = [&](int cur) __attribute__((always_inline)) {
     const float* la = lds + cur * STG;
     const float* lb = la + BM * BK;
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int st = 0; st < BK / 16; ++st) {
-      // one fragment set per 32-deep k-step (lane group lg: k 8 lg .. +7 of
-      // slot 4 st + lg), read whole before its MFMAs; the SIMD's other wave
-      // covers the read latency
-      bf16x8 af[FM][2], bf[FN][2];
+    bf16x8 af[2][FM][2], bf[2][FN][2];
+    auto rd = [&](int st) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int row = wm * WTM + i * 32 + h * 16 + l16;
-          af[i][h] = *reinterpret_cast<const bf16x8*>(la + row * BK + lswz(row, 4 * st + lg) * 4);
+          af[st][i][h] = *reinterpret_cast<const bf16x8*>(la + row * BK + lswz(row, 4 * st + lg) * 4);
         }
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int row = wn * WTN + j * 32 + h * 16 + l16;
-          bf[j][h] = *reinterpret_cast<const bf16x8*>(lb + row * BK + lswz(row, 4 * st + lg) * 4);
+          bf[st][j][h] = *reinterpret_cast<const bf16x8*>(lb + row * BK + lswz(row, 4 * st + lg) * 4);
         }
+    };
+    rd(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int st = 0; st < BK / 16; ++st) {
+      if (st + 1 < BK / 16) rd(st + 1);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int t = 0; t < 4; ++t)
-            acc4[i][j][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][t >> 1], bf[j][t & 1], acc4[i][j][t], 0, 0, 0);
+            acc4[i][j][t] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[st][i][t >> 1], bf[st][j][t & 1], acc4[i][j][t], 0, 0, 0);
+      if (st + 1 < BK / 16) {
+        // MFMA, read, MFMA, read, ... then the remaining MFMAs
+#pragma unroll
+        for (int x = 0; x < 2 * (FM + FN); ++x) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        }
+        __builtin_amdgcn_sched_group_barrier(0x008, 4 * FM * FN - 2 * (FM + FN), 0);
+      }
     }
     __builtin_amdgcn_s_setprio(0);
   };
