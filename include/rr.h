@@ -89,7 +89,8 @@ int rr_get_device(rr_handle_t h, int* device);
  *   RR_TUNE_LP_CFG:   bf16/fp8 core (0, the default: for the bf16 stored-C GEMMs with
  *                     the ViT epilogues, N % 256 == 0 and K <= 1024, the persistent
  *                     256x256 k-stream; its one-tile form is 3), 1 (128x128), 2 (256x64),
- *                     3 (256x256),
+ *                     3 (256x256), 6 (the persistent form with three A stages for the
+ *                     epilogues without the LayerNorm fold, at any K; tests),
  *                     4 (256x320 for bf16 filter / score sweeps, 256x256 otherwise),
  *                     5 (bf16 sweeps with K % 128 == 0, fp8 sweeps with K % 256 == 0:
  *                     256x256 8-phase pipeline; otherwise as 3)

@@ -154,7 +154,10 @@ __device__ __forceinline__ int ep_opaque(int v) {
 // fixed at compile time and (BI == 1) one column per thread, so the loop is
 // the arithmetic, a row bound and an address step; FL = -1: the flags read
 // from g per element.
-template <int FL, int P, int ITERS, int NT, int C4, int CS, int BI>
+// CSW: the staged rows are unpadded with their 16-B chunks XOR-swizzled,
+// chunk c of row r at c ^ (((r >> 2) & 1) << 2) (csw_chunk; gemm_lpp.hip)
+__device__ __forceinline__ int csw_chunk(int row, int c4) { return c4 ^ (((row >> 2) & 1) << 2); }
+template <int FL, int P, int ITERS, int NT, int C4, int CS, int BI, int CSW = 0>
 __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const float* ct, const f32x4 (&bias_v)[BI],
                                            const f32x4 (&res)[ITERS], int tid, int mb, int n0, const f32x4 (&sc_v)[BI],
                                            float& am, const float* ln_l = nullptr, const float* ln_cs = nullptr) {
@@ -183,7 +186,7 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
       for (int u = it; u < it + GR && u < ITERS; ++u) {
         const int idx = tid + u * NT;
         const int row = idx / C4, c4 = idx - row * C4;
-        cv[u] = *reinterpret_cast<const f32x4*>(ct + row * CS + c4 * 4);
+        cv[u] = *reinterpret_cast<const f32x4*>(ct + row * CS + (CSW ? csw_chunk(row, c4) : c4) * 4);
       }
     }
     int m, n;

@@ -1029,9 +1029,15 @@ int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& g, hipStre
       TimedLaunch tl(h, timer_cls, s);
       if (dt == DT_BF16) {
         // the ViT linears' epilogue flag sets with K <= 1024: the persistent
-        // 256x256 k-stream (gemm_lpp.hip; lp_cfg 3 forces the one-tile
-        // kernel).  The C4 embed 62.29 -> 61.54 ms (profiles/r05q_e2e_c4.txt)
-        if (emode == E_STORE && h->tune.lp_cfg == 0 && lpp_eligible(g)) e = launch_lpp(g, s, device_cu_count(h));
+        // 256x256 k-stream (gemm_lpp.hip), with three A stages where the
+        // fold's LDS is not needed (lp_cfg 3 forces the one-tile kernel; 6
+        // the three-A-stage form for the no-fold flag sets at any K).  Per
+        // block of linears 4.51 -> 4.35 ms (profiles/r05u_vitlin.txt); the C4
+        // embed 62.29 -> 61.54 ms with the first form (r05q_e2e_c4.txt)
+        if (emode == E_STORE && lpp3_eligible(g) && (h->tune.lp_cfg == 6 || (h->tune.lp_cfg == 0 && g.K <= 1024)))
+          e = launch_lpp3(g, s, device_cu_count(h));
+        else if (emode == E_STORE && (h->tune.lp_cfg == 0 || h->tune.lp_cfg == 6) && lpp_eligible(g))
+          e = launch_lpp(g, s, device_cu_count(h));
         else if (emode == E_STORE) e = launch_lp<E_STORE, DT_BF16>(g, s, h->tune);
         else if (emode == E_SCORES_T) e = launch_lp<E_SCORES_T, DT_BF16>(g, s, h->tune);
         else e = launch_lp<E_FILTER, DT_BF16>(g, s, h->tune);

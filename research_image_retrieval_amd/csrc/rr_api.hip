@@ -140,7 +140,7 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.gemm_bk = value;
       return RR_OK;
     case RR_TUNE_LP_CFG:
-      if (value < 0 || value > 5) break;
+      if (value < 0 || value > 6) break;
       h->tune.lp_cfg = value;
       return RR_OK;
     case RR_TUNE_S3_CFG:

@@ -318,5 +318,7 @@ int launch_merge(rr_handle_s* h, const float* ps, const long long* pi, int npart
 // gemm_lpp.hip: the bf16 stored-C GEMM as a persistent 256x256 k-stream
 bool lpp_eligible(const GemmArgs& g);
 hipError_t launch_lpp(const GemmArgs& g, hipStream_t s, int n_cu);
+bool lpp3_eligible(const GemmArgs& g);
+hipError_t launch_lpp3(const GemmArgs& g, hipStream_t s, int n_cu);
 
 }  // namespace rr

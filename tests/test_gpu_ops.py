@@ -121,7 +121,7 @@ def test_handle_device_and_tuning_validation(cuda):
     assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG, 16) == _lib.RR_EINVAL
     for retired in (6, 7, 12):  # sweep_order, sweep_pf, lp_il (ABI 5)
         assert L.rr_set_tuning(h, retired, 0) == _lib.RR_EINVAL and b"unknown key" in L.rr_last_error(h)
-    assert L.rr_set_tuning(h, _lib.TUNE_LP_CFG, 6) == _lib.RR_EINVAL
+    assert L.rr_set_tuning(h, _lib.TUNE_LP_CFG, 7) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_MF16, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_IL, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_CONV_IL, 2) == _lib.RR_EINVAL

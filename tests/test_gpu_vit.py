@@ -309,7 +309,7 @@ def test_linear_bf16_ln_argument_checks_and_edges(cuda):
     assert (out - ref).abs().max().item() <= 0.05 * ref.abs().mean().item()
 
 
-@pytest.mark.parametrize("kind", ["bf16_out", "residual", "gelu", "produce", "fold", "fold_gelu"])
+@pytest.mark.parametrize("kind", ["bf16_out", "residual", "gelu", "produce", "produce_k3072", "fold", "fold_gelu"])
 def test_linear_bf16_persistent_tile_bit_identical(cuda, kind):
     """The default for the ViT linears with K <= 1024 (gemm_lpp.hip: the
     256x256 bf16 tile as a persistent k-stream, slab epilogue, residual two
@@ -320,7 +320,7 @@ def test_linear_bf16_persistent_tile_bit_identical(cuda, kind):
     g = torch.Generator().manual_seed(23)
     n = 2304 if kind in ("bf16_out", "gelu", "fold", "fold_gelu") else 768
     m = 8000 + 37 if n == 2304 else 30001  # > 256 tiles either way
-    k = 768
+    k = 3072 if kind == "produce_k3072" else 768  # (c_proj's K: the one-tile kernel by default, lp_cfg 6 streams it)
     x = (torch.randn(m, k, generator=g) + 0.3).to(cuda)
     w = (torch.randn(n, k, generator=g) * k ** -0.5).to(cuda)
     bias = (torch.randn(n, generator=g) * 0.1).to(cuda)
@@ -335,7 +335,7 @@ def test_linear_bf16_persistent_tile_bit_identical(cuda, kind):
             return (ops.linear_bf16(xb16, wb16, bias, residual=r),)
         if kind == "gelu":
             return (ops.linear_bf16(xb16, wb16, bias, act=2, out_bf16=True),)
-        if kind == "produce":
+        if kind in ("produce", "produce_k3072"):
             return ops.linear_bf16_ln_produce(xb16, wb16, bias, r)
         xb, st = ops.ln_partials_bf16(x)
         wf, cs, bf = ops.ln_fold_weights(w, bias, gam, bet)
@@ -343,8 +343,11 @@ def test_linear_bf16_persistent_tile_bit_identical(cuda, kind):
 
     with ops.tuning(0, lp_cfg=3):
         ref = run()
-    out = run()
-    for a, b in zip(ref, out):
-        assert a.shape == b.shape and a.dtype == b.dtype
-        assert torch.equal(a.view(torch.int16) if a.dtype == torch.bfloat16 else a.view(torch.int32),
-                           b.view(torch.int16) if b.dtype == torch.bfloat16 else b.view(torch.int32)), kind
+    outs = [run()]
+    with ops.tuning(0, lp_cfg=6):  # the three-A-stage form (no-fold flag sets)
+        outs.append(run())
+    as_int = lambda t: t.view(torch.int16) if t.dtype == torch.bfloat16 else t.view(torch.int32)  # noqa: E731
+    for out in outs:
+        for a, b in zip(ref, out):
+            assert a.shape == b.shape and a.dtype == b.dtype
+            assert torch.equal(as_int(a), as_int(b)), kind
