@@ -1647,7 +1647,7 @@ __device__ __forceinline__ int hswz(int row, int slot) { return slot ^ ((row >> 
 // IL (16x16x32, one tap per barrier): the next k-tile's B DMA goes out one
 // instruction at a time among the k-tile's first MFMAs instead of as one
 // burst before them (the halo pass load stays at the top: it comes from HBM).
-template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1, int MF = 0, int IL = 0>
+template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1, int MF = 0, int IL = 0, int PERS = 0>
 __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int tiles_n) {
   constexpr int NP = 2, BK = 32, NT = 512, NW = 8;
   constexpr int WTM = 32 * FM, WTN = 32 * FN, BM = WTM * WM, BN = WTN * WN, SL = BK / 8;
@@ -1670,11 +1670,24 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   const int wm = wave % WM, wn = wave / WM;
   const int lr = lane & 31, lh = lane >> 5;
 
+  static_assert(!PERS || (TPK > 1 && !IL), "persistent halo tile: the all-passes-at-once instance");
   const int nwg = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tn = wgid % tiles_n, tm = wgid / tiles_n;
-  const int m0 = tm * BM, n0 = tn * BN;
+  // PERS: one block per CU walks the row tiles bid + t nwg (tiles_n == 1, so
+  // the weights never change), remapped per virtual block as config 8 / 15
+  const int ntiles = PERS ? (g.M + BM - 1) / BM * tiles_n : nwg;
+  auto tile_m0 = [&](int tl) __attribute__((always_inline)) {
+    const int v = bid + tl * nwg;
+    const int xcd = v & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (v >> 3);
+    return (wgid / tiles_n) * BM;
+  };
+  int m0, n0;
+  {
+    const int xcd = bid & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+    const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+    m0 = (wgid / tiles_n) * BM;
+    n0 = (wgid % tiles_n) * BN;
+  }
   const int W = g.W, H = g.H, KW = g.KW, ntap = g.KH * g.KW;
   const int nch = g.Cin / BK, ngrp = ntap / TPK, nk = nch * ngrp;  // k-step kt = (slice, group of TPK taps)
   const int hoff = g.pad * W + g.pad;  // halo row 0 = input raster index m0 - hoff
@@ -1686,14 +1699,14 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   const int a_slot = tid % SL, a_row = tid / SL;
   constexpr int RA_N = TPK == 1 ? 1 : A_PASS;
   f32x4 ra[RA_N][2];
-  auto load_pass_to = [&](int c, int p, f32x4(&r)[2]) {
+  auto load_pass_to = [&](int c, int p, f32x4(&r)[2], int mb) {
     const int hr = a_row + p * (NT / SL);
-    const long long q = (long long)m0 - hoff + hr;
+    const long long q = (long long)mb - hoff + hr;
     const bool ok = hr < HALO_HR && q >= 0 && q < g.M;
     const f32x4* src = ok ? reinterpret_cast<const f32x4*>(g.A + q * g.Cin + c * BK + a_slot * 8) : s3_zero_page();
     s3_load2<1>(src, r);
   };
-  auto load_pass = [&](int c, int p) { load_pass_to(c, p, ra[TPK == 1 ? 0 : p]); };
+  auto load_pass = [&](int c, int p) { load_pass_to(c, p, ra[TPK == 1 ? 0 : p], m0); };
   auto launder_pass = [&]() {
 #pragma unroll
     for (int p = 0; p < RA_N; ++p) {
@@ -1778,19 +1791,22 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   constexpr int RPT = MF ? 2 : 1;
   const int l16 = lane & 15, lg = lane >> 4;
   int tmask[FM][RPT];
+  auto masks = [&](int mb) __attribute__((always_inline)) {
 #pragma unroll
-  for (int i = 0; i < FM; ++i)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-    for (int a = 0; a < RPT; ++a) {
-      const int m = m0 + wm * WTM + i * 32 + (MF ? 16 * a + l16 : lr);
-      const int rem = m % (H * W), oh = rem / W, ow = rem - oh * W;
-      int mk = 0;
-      for (int kh = 0; kh < g.KH; ++kh)
-        for (int kw = 0; kw < KW; ++kw)
-          if ((unsigned)(oh + kh - g.pad) < (unsigned)H && (unsigned)(ow + kw - g.pad) < (unsigned)W)
-            mk |= 1 << (kh * KW + kw);
-      tmask[i][a] = m < g.M ? mk : 0;
-    }
+      for (int a = 0; a < RPT; ++a) {
+        const int m = mb + wm * WTM + i * 32 + (MF ? 16 * a + l16 : lr);
+        const int rem = m % (H * W), oh = rem / W, ow = rem - oh * W;
+        int mk = 0;
+        for (int kh = 0; kh < g.KH; ++kh)
+          for (int kw = 0; kw < KW; ++kw)
+            if ((unsigned)(oh + kh - g.pad) < (unsigned)H && (unsigned)(ow + kw - g.pad) < (unsigned)W)
+              mk |= 1 << (kh * KW + kw);
+        tmask[i][a] = m < g.M ? mk : 0;
+      }
+  };
+  masks(m0);
 
   f32x16 acc[FM][FN];
   f32x4 acc4[MF ? FM : 1][MF ? FN : 1][4];
@@ -1904,7 +1920,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     // accumulators are still constant zeros here, so the registers are free
     f32x4 rp[A_PASS][2];
 #pragma unroll
-    for (int p = 0; p < A_PASS; ++p) load_pass_to(0, p, rp[p]);
+    for (int p = 0; p < A_PASS; ++p) load_pass_to(0, p, rp[p], m0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 #pragma unroll
     for (int p = 0; p < A_PASS; ++p) {
@@ -1938,6 +1954,83 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   // landed by the end-of-tile wait) and split into the other buffer at the
   // start of tap p + 1's (that buffer's last reader was slice c - 1) ----
   static_assert(A_PASS < 9, "the halo passes must fit in one slice's taps");
+  if constexpr (PERS) {
+    // ---- the persistent stream: k-step q of the block = k-step q % nk of
+    // local tile q / nk, B stage q & 1, halo buffer sg & 1 (sg: the block's
+    // slice counter).  The next slice -- the tile's next, or after the
+    // tile's last the next tile's slice 0 -- loads in a slice's first group
+    // and splits into the other buffer in its second (with that buffer's
+    // zero rows: an epilogue may have staged C over them); the next k-step's
+    // B DMA may belong to the next tile (the same weights).  After a tile's
+    // last k-step its epilogue stages C through the halo buffer that slice
+    // released, in 128-row slabs ----
+    const int my_tiles = (ntiles - bid + nwg - 1) / nwg;
+    const int Q = my_tiles * nk;
+    int tl = 0, c = 0, tg = 0, kt = 0, sg = 0;
+    int m_next = my_tiles > 1 ? tile_m0(1) : m0;
+    for (int q = 0; q < Q; ++q) {
+      const bool last_slice = c + 1 == nch;
+      const bool more = !last_slice || tl + 1 < my_tiles;
+      if (q + 1 < Q) glds_b(kt + 1 == nk ? 0 : kt + 1, (q + 1) & 1);
+      if (more && tg == 1) {
+        const int nb = (sg + 1) & 1;
+#pragma unroll
+        for (int p = 0; p < A_PASS; ++p) store_pass(nb, p);
+        if (tid < 8) {
+          const int pl = tid >> 2, sl = tid & 3;
+          *reinterpret_cast<u32x4*>(lds + nb * A_EL + (pl * HRA + HALO_HR) * BK + sl * 8) = u32x4{0u, 0u, 0u, 0u};
+        }
+      }
+      if (more && tg == 0) {
+#pragma unroll
+        for (int p = 0; p < A_PASS; ++p) load_pass_to(last_slice ? 0 : c + 1, p, ra[p], last_slice ? m_next : m0);
+      }
+#pragma unroll
+      for (int u = 0; u < TPK; ++u) compute(sg & 1, q & 1, tg * TPK + u, u);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next B (and the next slice's passes)
+      launder_pass();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (++tg == ngrp) {
+        tg = 0;
+        ++c;
+        ++sg;
+      }
+      if (++kt == nk) {
+        if constexpr (MF) {
+#pragma unroll
+          for (int i = 0; i < FM; ++i)
+#pragma unroll
+            for (int j = 0; j < FN; ++j)
+#pragma unroll
+              for (int t = 0; t < 4; ++t)
+#pragma unroll
+                for (int e = 0; e < 4; ++e) acc[i][j][4 * t + e] = acc4[i][j][t][e];
+        }
+        epilogue_store<WM, WN, FM, FN, A_EL / 2, (bool)MF, EPI>(
+            g, g.C, acc, reinterpret_cast<float*>(lds + ((sg - 1) & 1) * A_EL), m0, n0, a_isc);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+            if constexpr (MF) {
+#pragma unroll
+              for (int t = 0; t < 4; ++t) acc4[i][j][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+            }
+          }
+        kt = 0;
+        c = 0;
+        ++tl;
+        m0 = m_next;
+        m_next = tl + 1 < my_tiles ? tile_m0(tl + 1) : m0;
+        masks(m0);
+      }
+    }
+    return;
+  }
   int c = 0, tg = 0;
   RR_PH(7);
   for (int kt = 0; kt < nk; ++kt) {
@@ -2004,28 +2097,34 @@ static int h2_halo_rows(const GemmArgs& g) {
   if ((g.N % 64) == 0) return need <= 384 ? 384 : 0;
   return 0;
 }
-template <int EPI, int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int IL = 0>
-static hipError_t launch_h2_halo_t(const GemmArgs& g, hipStream_t s) {
+template <int EPI, int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int IL = 0, int PERS = 0>
+static hipError_t launch_h2_halo_t(const GemmArgs& g, hipStream_t s, int n_cu = 256) {
   constexpr int BN = 32 * FN * WN;
   const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((gemm_h2_halo_kernel<EPI, WM, WN, FM, FN, HR, TPK, MF, IL>), dim3((unsigned)nblk), dim3(512), 0, s,
-                     g, (int)tiles_n);
+  // PERS: one block per CU walking the row tiles (tiles_n == 1; a block that
+  // owns several stays on its XCD: grid a multiple of 8)
+  const int slots = std::max(8, n_cu & ~7);
+  const long long grid = PERS ? (nblk <= slots ? nblk : slots) : nblk;
+  hipLaunchKernelGGL((gemm_h2_halo_kernel<EPI, WM, WN, FM, FN, HR, TPK, MF, IL, PERS>), dim3((unsigned)grid), dim3(512), 0,
+                     s, g, (int)tiles_n);
   return hipGetLastError();
 }
-template <int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int IL = 0>
-static hipError_t launch_h2_halo_ep(const GemmArgs& g, hipStream_t s) {
+template <int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int IL = 0, int PERS = 0>
+static hipError_t launch_h2_halo_ep(const GemmArgs& g, hipStream_t s, int n_cu = 256) {
   switch (ep_flags(g) & (EP_RES | EP_RELU)) {
-    case EP_RELU: return launch_h2_halo_t<H2_EP | EP_RELU, WM, WN, FM, FN, HR, TPK, MF, IL>(g, s);
-    case EP_RES | EP_RELU: return launch_h2_halo_t<H2_EP | EP_RES | EP_RELU, WM, WN, FM, FN, HR, TPK, MF, IL>(g, s);
-    case EP_RES: return launch_h2_halo_t<H2_EP | EP_RES, WM, WN, FM, FN, HR, TPK, MF, IL>(g, s);
-    default: return launch_h2_halo_t<H2_EP, WM, WN, FM, FN, HR, TPK, MF, IL>(g, s);
+    case EP_RELU: return launch_h2_halo_t<H2_EP | EP_RELU, WM, WN, FM, FN, HR, TPK, MF, IL, PERS>(g, s, n_cu);
+    case EP_RES | EP_RELU: return launch_h2_halo_t<H2_EP | EP_RES | EP_RELU, WM, WN, FM, FN, HR, TPK, MF, IL, PERS>(g, s, n_cu);
+    case EP_RES: return launch_h2_halo_t<H2_EP | EP_RES, WM, WN, FM, FN, HR, TPK, MF, IL, PERS>(g, s, n_cu);
+    default: return launch_h2_halo_t<H2_EP, WM, WN, FM, FN, HR, TPK, MF, IL, PERS>(g, s, n_cu);
   }
 }
-// mf: 1 = the 16x16x32 form (s3_cfg 14 forces it)
-static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s, int hr, int mf) {
+// mf: 1 = the 16x16x32 form (s3_cfg 14 forces it); pers: the N = 64 instance
+// as a persistent stream (one column tile)
+static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s, int hr, int mf, bool pers = false, int n_cu = 256) {
+  if (hr == 384 && !mf && pers && g.N == 64) return launch_h2_halo_ep<4, 2, 2, 1, 384, 3, 0, 0, 1>(g, s, n_cu);
   // (the 16x16x32 256x256 form with its B DMA spread among the MFMAs: conv_il)
   if (hr == 288 && mf && g.issue_spread) return launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 1, 1>(g, s);
   if (hr == 288) return mf ? launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 1>(g, s) : launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 0>(g, s);
@@ -2205,6 +2304,10 @@ static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int
 
 template <int AM>
 static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
+  // the N = 64 halo tile as a persistent stream: the default (s3_cfg 13
+  // forces the one-tile form); 64@56 3x3 1.212 -> 1.161 ms, bit-identical
+  // (profiles/r05w_sweep.txt; the embed 68.26 / 68.22 ms, r05w_e2e.txt)
+  const bool hpers = forced == 0;
   // config 15 (config 12 as a persistent k-stream): the pick for dense A
   // with config 12's shape condition (forced 15: the same, every other GEMM
   // on the library's pick; forced 12 runs config 12).  Measured at 1280
@@ -2247,7 +2350,8 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
     if (forced == 13 || forced == 14 || (forced == 0 && ((g.N % 256) == 0 || g.N == 64))) {
       if (const int hr = h2_halo_rows(g))
         return launch_h2_halo(g, s, hr,
-                              forced == 14 ? 1 : forced == 13 ? 0 : g.halo_mf >= 0 ? g.halo_mf : (hr == 288 ? 1 : 0));
+                              forced == 14 ? 1 : forced == 13 ? 0 : g.halo_mf >= 0 ? g.halo_mf : (hr == 288 ? 1 : 0),
+                              hpers, n_cu);
     }
   }
   if (forced == 13 || forced == 14) forced = 0;

@@ -505,3 +505,25 @@ def test_h2_batch_coupling_bounded(cuda, ratio_log2):
     ea, eb = (alone - ref).abs().max().item(), (batch[:1] - ref).abs().max().item()
     print(f"batch coupling 2^{ratio_log2}: alone vs in batch {d:.3g}; vs float64 alone {ea:.3g} in batch {eb:.3g}")
     assert d <= DESC_TOL and ea <= DESC_TOL and eb <= DESC_TOL
+
+
+@pytest.mark.parametrize("b,h,w,cin,res", [
+    (24, 56, 56, 64, False),   # the R101 64@56 shape, 294 tiles (several per block)
+    (40, 31, 63, 32, True),    # the widest map, one slice per tile: every next slice is the next tile's
+    (30, 28, 28, 128, False),  # four slices per tile
+    (1, 56, 56, 64, False),    # fewer tiles than blocks
+])
+def test_h2_halo_persistent_bit_identical(cuda, b, h, w, cin, res):
+    """The N = 64 halo tile as a persistent stream (the default: the next
+    tile's first halo slice and B stage load under the current tile's last
+    slice; C staged through the released halo buffer) computes the same
+    products in the same order as the one-tile kernel (s3_cfg 13): identical
+    bits and max-|y| record."""
+    x, wt, bias, r, _, _ = _conv_case(cuda, b, h, w, cin, 64, 3, 1, 1, res, seed=29)
+    outs, amax = {}, {}
+    for cfg in (13, 0):
+        with ops.tuning(0, s3_cfg=cfg):
+            y, rec = _run_h2(cuda, x, wt, bias, r, 1, 1)
+        outs[cfg], amax[cfg] = y.cpu(), ops.amax_value(rec[1])
+    assert torch.equal(outs[13], outs[0])
+    assert amax[13] == amax[0] == float(outs[0].abs().max())
