@@ -1,5 +1,5 @@
 #!/bin/bash
-# usage: bash tools/r05_check.sh <tag> [pytest paths...]: the given GPU tests, then the C3 bench line.
+# usage: bash tools/gpu_check.sh <tag> [pytest paths...]: the given GPU tests, then the C3 bench line.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-chk}; shift
