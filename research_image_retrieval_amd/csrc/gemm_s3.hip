@@ -1154,10 +1154,15 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
     RR_PH(0);
     rd_mf(cur, 0);
     rd_mf(cur, 1);
+    // (a tile's first k-tile skips the A wait: its A(j+1) was issued before
+    // the previous epilogue, whose waits -- the residual's vmcnt(0), or the
+    // bias / scale loads' -- covered it; waiting here would wait for that
+    // epilogue's stores as well)
+    const bool wait_a = c_kt != 0 || c_tl == 0;
     if constexpr (SP == 3) {
       mf_hi();
       mf_lo1();
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
+      if (wait_a) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
       launder_a(cur ^ 1);
       split_a(cur ^ 1);
       rd_mf(cur, NP - 1);
@@ -1167,7 +1172,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
       // VALU per MFMA gap (same per-accumulator order as config 4)
       mf_lo1();
       RR_PH(1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
+      if (wait_a) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(A_LD + B_INS) : "memory");  // A(j+1) landed
       launder_a(cur ^ 1);
       RR_PH(2);
       split_a(cur ^ 1);
