@@ -1244,23 +1244,27 @@ static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
 // trip per tile instead of config 12's two (its two 128-row slabs each load
 // their residual after staging, and only half the waves stage each slab).
 // Same per-accumulator k order (per 16-deep k-step: a0b0, a0b1, a1b0) and
-// epilogue arithmetic as config 12: bit-identical to it.
+// epilogue arithmetic as config 12: bit-identical to it.  FN = 1: the 256x128
+// form (waves of 128x32, two B DMA instructions per wave, 96 KB of LDS) for
+// N = 128, whose every column is config 12's column bit for bit.
 // Counted waits: vector-memory operations retire in issue order (stores
 // included), so each wait names how many younger operations may remain; where
 // fewer were issued (rows past M store nothing) the wait is longer, never
 // shorter.
-template <int EPI>
+template <int EPI, int FN = 2>
 __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_n, int ntiles) {
   static_assert((EPI & EP_SCALE) != 0, "f16x2: scaled epilogue");
+  static_assert(FN == 1 || FN == 2, "256x128 or 256x256");
   typedef f16x8 frag_t;
-  constexpr int NP = 2, WM = 2, FM = 4, FN = 2, BK = 32, NT = 512, NW = 8;
-  constexpr int WTM = 128, WTN = 64, BM = 256, BN = 256, SL = BK / 8;
+  constexpr int NP = 2, WM = 2, FM = 4, BK = 32, NT = 512, NW = 8;
+  constexpr int WTM = 128, WTN = 32 * FN, BM = 256, BN = 4 * WTN, SL = BK / 8;
   constexpr int A_EL = NP * BM * BK, BUF = A_EL + NP * BN * BK;
   // stage stride: a stage also holds one 64-row slab of C (rows padded by 8
   // floats: the 32x32 accumulator writes hit distinct banks)
   constexpr int CS = BN + 8;
   constexpr int STG = BUF > 64 * CS * 2 ? BUF : 64 * CS * 2;
-  constexpr int B_INS = NP * BN / (64 / SL) / NW;  // LDS-DMA instructions per wave per k-tile (4)
+  constexpr int B_INS = NP * BN / (64 / SL) / NW;  // LDS-DMA instructions per wave per k-tile (4 / 2)
+  constexpr int IPP = BN / 128;                     // of them per plane
   constexpr int A_RPP = NT / SL, A_CH = BM / A_RPP;  // 128 rows per pass, 2 chunks per thread
   constexpr int A_LD = 2 * A_CH;                     // A loads per thread per k-tile
   static_assert(B_INS * NW * (64 / SL) == NP * BN && A_CH * A_RPP == BM, "staging must tile the block");
@@ -1347,8 +1351,8 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
     }
   };
 
-  // ---- B loader (as config 8): instruction i of a wave DMAs plane i / 2,
-  // plane rows 128 (i & 1) + 16 wave + lane / 4 ----
+  // ---- B loader (as config 8): instruction i of a wave DMAs plane i / IPP,
+  // plane rows 128 (i % IPP) + 16 wave + lane / 4 ----
   const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
   const int b_r = wave * (64 / SL) + lane / SL;
   const int b_sw = pswz<BK, 2>(b_r, lane % SL) * 8;  // the same for every i
@@ -1364,7 +1368,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
     uint16_t* lb = lds + buf * STG + A_EL;
 #pragma unroll
     for (int i = 0; i < B_INS; ++i)
-      __builtin_amdgcn_global_load_lds((const void*)(b_src + (i >> 1) * g.b_plane + (long long)(i & 1) * (BN / 2) * g.ldb +
+      __builtin_amdgcn_global_load_lds((const void*)(b_src + (i / IPP) * g.b_plane + (long long)(i % IPP) * 128 * g.ldb +
                                                      b_kt * BK),
                                        (__attribute__((address_space(3))) void*)(lb + (i * NW + wave) * (64 / SL) * BK),
                                        16, 0, 0);
@@ -1588,9 +1592,9 @@ static bool s3q_fits(const GemmArgs& g) {
   return (long long)g.M * g.lda * 4 < lim && (long long)g.M * g.ldc * 4 < lim;
 }
 
-template <int EPI>
+template <int EPI, int FN = 2>
 static hipError_t launch_s3q_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
-  const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / 256;
+  const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / (128 * FN);
   const long long ntiles = tiles_m * tiles_n;
   if (ntiles <= 0) return hipSuccess;
   if (ntiles * (g.K / 32) > 0x7fffffffLL) return hipErrorInvalidValue;
@@ -1599,7 +1603,7 @@ static hipError_t launch_s3q_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
   const int grid = ntiles <= slots ? (int)ntiles : slots;
   g.stagger_blocks = grid;
   g.stagger_sleeps = ntiles > 2LL * grid ? stagger : 0;
-  hipLaunchKernelGGL((gemm_s3q_kernel<EPI>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
+  hipLaunchKernelGGL((gemm_s3q_kernel<EPI, FN>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
   return hipGetLastError();
 }
 
@@ -2212,7 +2216,8 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //  15: config 12 as a persistent k-stream (gemm_s3q_kernel, f16x2, dense A,
 //      config 12's shapes; the pick there): the next tile's first k-tiles load under
 //      the epilogue, which runs in four slabs with the residual two 32-row
-//      bands ahead; bit-identical to config 12
+//      bands ahead; bit-identical to config 12.  Its 256x128 form serves
+//      dense N == 128, K >= 256
 // (all others on v_mfma_f32_32x32x16_{bf16,f16}).  The f16x2 split is built
 // for configs 3, 4, 7, 8, 9, 10 and 11 (a forced 1, 2, 5 or 6 runs the pick).
 // Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the fastest
@@ -2335,6 +2340,14 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
           case EP_RES | EP_RELU: return launch_s3q_t<H2_EP | EP_RES | EP_RELU | EP_SC1>(g, s, n_cu, st);
           case EP_RES: return launch_s3q_t<H2_EP | EP_RES | EP_SC1>(g, s, n_cu, st);
           default: return launch_s3q_t<H2_EP>(g, s, n_cu, st);
+        }
+      }
+      if (g.N == 128 && g.K >= 256 && s3q_fits(g)) {
+        switch (ep_flags(g) & (EP_RES | EP_RELU)) {
+          case EP_RELU: return launch_s3q_t<H2_EP | EP_RELU, 1>(g, s, n_cu, st);
+          case EP_RES | EP_RELU: return launch_s3q_t<H2_EP | EP_RES | EP_RELU | EP_SC1, 1>(g, s, n_cu, st);
+          case EP_RES: return launch_s3q_t<H2_EP | EP_RES | EP_SC1, 1>(g, s, n_cu, st);
+          default: return launch_s3q_t<H2_EP, 1>(g, s, n_cu, st);
         }
       }
     }

@@ -282,6 +282,32 @@ def test_h2_persistent_256_tile_bit_identical(cuda, b, h, w, cin, cout, res, rel
     assert amax[12] == amax[15] == float(outs[15].abs().max())
 
 
+@pytest.mark.parametrize("b,h,w,cin,res,relu", [
+    (6, 28, 28, 512, False, True),    # the R101 512->128 reduction shape: 19 tiles, ragged M
+    (5, 80, 80, 256, True, True),     # 125 tiles, several per block, residual (sc1 / nt)
+    (2, 9, 11, 288, True, False),     # K = 288: nine k-tiles, one partial tile
+    (1, 3, 5, 1024, False, False),    # one partial tile, no epilogue options
+])
+def test_h2_persistent_256x128_tile_bit_identical(cuda, b, h, w, cin, res, relu):
+    """The 256x128 form of config 15 (the pick for dense N = 128, K >= 256)
+    computes each output column with config 12's products in config 12's
+    order: a 128-channel layer equals the first 128 channels of the same layer
+    at 256 channels on config 12 (per-channel weight scales: the sliced planes
+    are the same), bit for bit, and its max-|y| record is exact."""
+    x, wt, bias, r, _, _ = _conv_case(cuda, b, h, w, cin, 256, 1, 1, 0, res, seed=19)
+    xd = x.to(cuda)
+    rec = ops.amax_records(3, cuda)
+    ops.amax_f32(xd, rec[0])
+    with ops.tuning(0, s3_cfg=12):
+        y256 = ops.conv2d_h2(xd, rec[0], ops.H2Conv(wt.to(cuda)), bias.to(cuda), 1, 0,
+                             r.to(cuda) if res else None, relu, rec[1]).cpu()
+    r128 = r[..., :128].contiguous().to(cuda) if res else None
+    y128 = ops.conv2d_h2(xd, rec[0], ops.H2Conv(wt[:128].contiguous().to(cuda)), bias[:128].contiguous().to(cuda),
+                         1, 0, r128, relu, rec[2]).cpu()
+    assert torch.equal(y128, y256[..., :128])
+    assert ops.amax_value(rec[2]) == float(y128.abs().max())
+
+
 @pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res,cfg", [
     (3, 29, 31, 256, 1024, 1, 1, 0, True, 12),   # 1x1 + residual (dense A), ragged last tile
     (2, 14, 14, 1024, 256, 1, 1, 0, False, 12),  # 1x1, K = 1024
