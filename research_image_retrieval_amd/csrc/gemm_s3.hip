@@ -2208,7 +2208,8 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //      products accumulate with a0b0; error vs float64 still at the exact-fp32
 //      core's, profiles/r03j_acc1_ab.txt; 196 instead of 254 VGPRs)
 //  11: 128x128, 4 waves of 64x64, BK 32, 2/CU (64 KB), 16x16x32, ACC1 (f16x2
-//      only): the picked tile for N == 128
+//      only): the picked tile for N == 128 (dense K >= 256: config 15's
+//      256x128 form)
 //  12: 256x256, 8 waves of 128x64, BK 32, 1/CU (128 KB), 32x32x16, ACC1 (f16x2
 //      only; 254 VGPRs — two accumulator sets do not fit this tile): half the
 //      operand bytes per FLOP of config 4, the picked tile for N % 256 == 0
@@ -2251,7 +2252,9 @@ static int pick_h2(const GemmArgs& g, int forced) {
   if (forced == 11) return (g.N % 128) == 0 ? 11 : pick_h2(g, 0);
   if (forced == 12) return (g.N % 256) == 0 ? 12 : pick_h2(g, 0);
   // N == 128: two 128x128 blocks per CU (config 11) run the R101 N = 128
-  // layers 4-7 % faster than the 256x128 tile (profiles/r03l_h2_cfg_sweep.txt)
+  // layers 4-7 % faster than the 256x128 tile (profiles/r03l_h2_cfg_sweep.txt);
+  // the dense K >= 256 ones take config 15's persistent 256x128 form before
+  // this pick (profiles/r05ae_s3q128_ab/)
   if (forced == 0 && g.N == 128) return 11;
   int cfg = pick_s3(g, forced);
   if (cfg == 3 || cfg == 4 || cfg == 7 || cfg == 8) return cfg;
