@@ -19,8 +19,8 @@ struct rr_handle_s {
   struct Tuning {
     int gemm_cfg = 0;  // fp32 core: 22, 41 or 88
     int gemm_bk = 0;   // fp32 core k-tile depth: 16 or 32
-    int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 / fp8 sweeps)
-    int s3_cfg = 0;    // split cores: 1..15 (gemm_s3.hip tile table; 9-15 f16x2 only)
+    int lp_cfg = 0;    // bf16 / fp8 core: 1 = 128x128, 2 = 256x64, 3 = 256x256, 4 = 256x320 (filter sweeps), 5 = 8-phase 256x256 (bf16 / fp8 sweeps), 6 = the persistent bf16 tile with three A stages (tests); 0: the pick (the persistent 256x256 bf16 tile for the ViT epilogues, K <= 1024)
+    int s3_cfg = 0;    // split cores: 1..15 (gemm_s3.hip tile table; 9-15 f16x2 only); 0: the pick
     int s3_stagger = -1;  // split-bf16 core round stagger in ~1 us sleeps (-1: the library's pick)
     int sweep_mf16 = -1;   // bf16 256x320 filter sweep on v_mfma_f32_16x16x32_bf16 (1) or 32x32x16 (0); -1: the pick (0)
     int sweep_il = -1;     // bf16 256x320 filter sweep: next k-tile's DMA spread among the MFMAs (1) or one burst (0); -1: the pick (1)
