@@ -99,8 +99,9 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     v_mfma_f32_32x32x16_f16, 14 = the same on v_mfma_f32_16x16x32_f16
  *                     (the default picks 14's form for cout % 256 == 0, 13's for cout 64);
  *                     15 = the 256x256 tile (12) as a persistent k-stream (the default
- *                     for dense A with cout % 256 == 0, K >= 256, and its 256x128 form
- *                     for dense cout 128, K >= 256; forced, every other
+ *                     for dense A with cout % 256 == 0, K >= 256, its 256x128 form
+ *                     for dense cout 128, K >= 256, its 256x64 form for dense cout 64,
+ *                     K >= 64; forced, every other
  *                     GEMM runs the library's pick; 12 forces the one-tile-per-block form);
  *                     7 also selects the implicit-GEMM fused stem over the halo stem)
  *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of

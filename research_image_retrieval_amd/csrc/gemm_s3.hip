@@ -1246,25 +1246,27 @@ static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
 // Same per-accumulator k order (per 16-deep k-step: a0b0, a0b1, a1b0) and
 // epilogue arithmetic as config 12: bit-identical to it.  FN = 1: the 256x128
 // form (waves of 128x32, two B DMA instructions per wave, 96 KB of LDS) for
-// N = 128, whose every column is config 12's column bit for bit.
+// N = 128; FN = 1, WM = 4: the 256x64 form (waves 4 x 2 of 64x32, one B DMA
+// instruction per wave spanning both planes, slabs of four 32-row bands, 80
+// KB) for N = 64.  Every column of either is config 12's column bit for bit.
 // Counted waits: vector-memory operations retire in issue order (stores
 // included), so each wait names how many younger operations may remain; where
 // fewer were issued (rows past M store nothing) the wait is longer, never
 // shorter.
-template <int EPI, int FN = 2>
+template <int EPI, int FN = 2, int WM = 2>
 __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_n, int ntiles) {
   static_assert((EPI & EP_SCALE) != 0, "f16x2: scaled epilogue");
-  static_assert(FN == 1 || FN == 2, "256x128 or 256x256");
+  static_assert((WM == 2 && (FN == 1 || FN == 2)) || (WM == 4 && FN == 1), "256x256, 256x128 or 256x64");
   typedef f16x8 frag_t;
-  constexpr int NP = 2, WM = 2, FM = 4, BK = 32, NT = 512, NW = 8;
-  constexpr int WTM = 128, WTN = 32 * FN, BM = 256, BN = 4 * WTN, SL = BK / 8;
+  constexpr int NP = 2, FM = 8 / WM, BK = 32, NT = 512, NW = 8, WN = NW / WM;
+  constexpr int WTM = 32 * FM, WTN = 32 * FN, BM = 256, BN = WN * WTN, SL = BK / 8;
   constexpr int A_EL = NP * BM * BK, BUF = A_EL + NP * BN * BK;
   // stage stride: a stage also holds one 64-row slab of C (rows padded by 8
   // floats: the 32x32 accumulator writes hit distinct banks)
   constexpr int CS = BN + 8;
-  constexpr int STG = BUF > 64 * CS * 2 ? BUF : 64 * CS * 2;
+  constexpr int STG = BUF > WM * 32 * CS * 2 ? BUF : WM * 32 * CS * 2;
   constexpr int B_INS = NP * BN / (64 / SL) / NW;  // LDS-DMA instructions per wave per k-tile (4 / 2)
-  constexpr int IPP = BN / 128;                     // of them per plane
+  constexpr int IPP = BN >= 128 ? BN / 128 : 1;     // of them per plane (64 columns: one spans both)
   constexpr int A_RPP = NT / SL, A_CH = BM / A_RPP;  // 128 rows per pass, 2 chunks per thread
   constexpr int A_LD = 2 * A_CH;                     // A loads per thread per k-tile
   static_assert(B_INS * NW * (64 / SL) == NP * BN && A_CH * A_RPP == BM, "staging must tile the block");
@@ -1361,7 +1363,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
   auto b_tile = [&](int tl) __attribute__((always_inline)) {
     int m0, n0;
     tile_origin(tl, m0, n0);
-    b_src = Bp + (long long)(n0 + b_r) * g.ldb + b_sw;
+    b_src = Bp + (long long)(b_r / BN) * g.b_plane + (long long)(n0 + b_r % BN) * g.ldb + b_sw;
   };
   b_tile(0);
   auto glds_b = [&](int buf) __attribute__((always_inline)) {
@@ -1425,8 +1427,9 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
   // together.  Band b's residual rows are loaded two bands ahead (issued
   // before band b - 2 is stored): at most three bands (48 registers) in
   // flight -- a whole slab ahead (64) spilled the k-loop.
-  constexpr int C4 = BN / 4, HITERS = 32 * C4 / NT;  // 4 row chunks per thread and band
-  constexpr int NB = 2 * FM, RD = 2;                   // bands, residual look-ahead (bands)
+  constexpr int C4 = BN / 4, HITERS = 32 * C4 / NT;  // 4 / 2 / 1 row chunks per thread and band
+  static_assert(HITERS * 2 <= 16 && (HITERS == 1 || HITERS % 2 == 0), "the counted waits' immediates");
+  constexpr int NB = WM * FM, RD = 2;                  // bands, residual look-ahead (bands)
   RR_PH_DECL
   auto epilogue = [&](int tl, int buf) __attribute__((always_inline)) {
     int m0, n0;
@@ -1435,7 +1438,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
     const int c40 = te % C4;
     f32x4 bias_v[1] = {f32x4{0.f, 0.f, 0.f, 0.f}}, sc_v[1];
     f32x4 res[RD + 1][HITERS];  // ring of bands
-    auto band_row0 = [&](int bb) { return (bb & 1) * 128 + (bb >> 1) * 32; };
+    auto band_row0 = [&](int bb) { return (bb % WM) * WTM + (bb / WM) * 32; };
     auto load_band = [&](int bb) __attribute__((always_inline)) {
       if constexpr ((EPI & EP_RES) != 0) {
         // (addresses from an opaque thread index per band: hoisted, every
@@ -1484,7 +1487,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
     // profiles/r05j_probe.txt)
 #pragma unroll
     for (int bb = 0; bb < NB; ++bb) {
-      if ((bb & 1) == 0) stage(bb >> 1);
+      if (bb % WM == 0) stage(bb / WM);
       if (bb + RD < NB) load_band(bb + RD);
       if constexpr ((EPI & EP_RES) != 0) {
         const int ahead = (NB - 1 - bb < RD ? NB - 1 - bb : RD);
@@ -1493,7 +1496,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
         switch (younger) {
 #define RR_VMW(n) \
   case n: asm volatile("s_waitcnt vmcnt(" #n ")" ::: "memory"); break;
-          RR_VMW(0) RR_VMW(2) RR_VMW(4) RR_VMW(6) RR_VMW(8) RR_VMW(10) RR_VMW(12) RR_VMW(14)
+          RR_VMW(0) RR_VMW(1) RR_VMW(2) RR_VMW(3) RR_VMW(4) RR_VMW(6) RR_VMW(8) RR_VMW(10) RR_VMW(12) RR_VMW(14)
 #undef RR_VMW
           default: asm volatile("s_waitcnt vmcnt(16)" ::: "memory"); break;
         }
@@ -1508,9 +1511,9 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
         asm volatile("" : "+v"(sc_v[0]));
         sc_v[0] *= a_isc;
       }
-      store_slab<EPI, 2, HITERS, NT, C4, CS, 1>(g, g.C, ct + (bb & 1) * 32 * CS, bias_v, res[bb % (RD + 1)], te,
+      store_slab<EPI, 2, HITERS, NT, C4, CS, 1>(g, g.C, ct + (bb % WM) * 32 * CS, bias_v, res[bb % (RD + 1)], te,
                                                 m0 + band_row0(bb), n0, sc_v, am);
-      if (bb & 1) {
+      if (bb % WM == WM - 1) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         __builtin_amdgcn_s_barrier();  // every LDS read of the slab done (the last also frees `buf`)
         asm volatile("" ::: "memory");
@@ -1592,9 +1595,9 @@ static bool s3q_fits(const GemmArgs& g) {
   return (long long)g.M * g.lda * 4 < lim && (long long)g.M * g.ldc * 4 < lim;
 }
 
-template <int EPI, int FN = 2>
+template <int EPI, int FN = 2, int WM = 2>
 static hipError_t launch_s3q_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
-  const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / (128 * FN);
+  const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / (32 * FN * (8 / WM));
   const long long ntiles = tiles_m * tiles_n;
   if (ntiles <= 0) return hipSuccess;
   if (ntiles * (g.K / 32) > 0x7fffffffLL) return hipErrorInvalidValue;
@@ -1603,7 +1606,7 @@ static hipError_t launch_s3q_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
   const int grid = ntiles <= slots ? (int)ntiles : slots;
   g.stagger_blocks = grid;
   g.stagger_sleeps = ntiles > 2LL * grid ? stagger : 0;
-  hipLaunchKernelGGL((gemm_s3q_kernel<EPI, FN>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
+  hipLaunchKernelGGL((gemm_s3q_kernel<EPI, FN, WM>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
   return hipGetLastError();
 }
 
@@ -2199,7 +2202,8 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //   6: 256x64,  4 waves of 64x64, BK 16, 2/CU (60 KB)
 //   7: 256x64,  8 waves of 32x64, BK 16, 2/CU (60 KB), 4 waves per SIMD
 //      (<= 128 registers): the picked 256x64 tile (the N = 64 layers and the
-//      stem 2-7 % faster than 6, profiles/r02f_s3_cfg7.txt)
+//      stem 2-7 % faster than 6, profiles/r02f_s3_cfg7.txt; f16x2 dense N = 64
+//      now takes config 15's 256x64 form, profiles/r05ah_s3q64_ab/)
 //   8: config 4 as a persistent k-stream (gemm_s3p_kernel): dense A, N % 256
 //      == 0 — the picked tile for the 1x1 layers it serves
 //   9: config 4 with three LDS stages (f16x2 only, 144 KB): the B DMA two
@@ -2218,7 +2222,7 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //      config 12's shapes; the pick there): the next tile's first k-tiles load under
 //      the epilogue, which runs in four slabs with the residual two 32-row
 //      bands ahead; bit-identical to config 12.  Its 256x128 form serves
-//      dense N == 128, K >= 256
+//      dense N == 128, K >= 256, its 256x64 form dense N == 64, K >= 64
 // (all others on v_mfma_f32_32x32x16_{bf16,f16}).  The f16x2 split is built
 // for configs 3, 4, 7, 8, 9, 10 and 11 (a forced 1, 2, 5 or 6 runs the pick).
 // Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the fastest
@@ -2351,6 +2355,14 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
           case EP_RES | EP_RELU: return launch_s3q_t<H2_EP | EP_RES | EP_RELU | EP_SC1, 1>(g, s, n_cu, st);
           case EP_RES: return launch_s3q_t<H2_EP | EP_RES | EP_SC1, 1>(g, s, n_cu, st);
           default: return launch_s3q_t<H2_EP, 1>(g, s, n_cu, st);
+        }
+      }
+      if (g.N == 64 && g.K >= 64 && s3q_fits(g)) {
+        switch (ep_flags(g) & (EP_RES | EP_RELU)) {
+          case EP_RELU: return launch_s3q_t<H2_EP | EP_RELU, 1, 4>(g, s, n_cu, st);
+          case EP_RES | EP_RELU: return launch_s3q_t<H2_EP | EP_RES | EP_RELU | EP_SC1, 1, 4>(g, s, n_cu, st);
+          case EP_RES: return launch_s3q_t<H2_EP | EP_RES | EP_SC1, 1, 4>(g, s, n_cu, st);
+          default: return launch_s3q_t<H2_EP, 1, 4>(g, s, n_cu, st);
         }
       }
     }

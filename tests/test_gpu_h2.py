@@ -282,18 +282,23 @@ def test_h2_persistent_256_tile_bit_identical(cuda, b, h, w, cin, cout, res, rel
     assert amax[12] == amax[15] == float(outs[15].abs().max())
 
 
-@pytest.mark.parametrize("b,h,w,cin,res,relu", [
-    (6, 28, 28, 512, False, True),    # the R101 512->128 reduction shape: 19 tiles, ragged M
-    (5, 80, 80, 256, True, True),     # 125 tiles, several per block, residual (sc1 / nt)
-    (2, 9, 11, 288, True, False),     # K = 288: nine k-tiles, one partial tile
-    (1, 3, 5, 1024, False, False),    # one partial tile, no epilogue options
+@pytest.mark.parametrize("b,h,w,cin,res,relu,nout", [
+    (6, 28, 28, 512, False, True, 128),   # the R101 512->128 reduction shape: 19 tiles, ragged M
+    (5, 80, 80, 256, True, True, 128),    # 125 tiles, several per block, residual (sc1 / nt)
+    (2, 9, 11, 288, True, False, 128),    # K = 288: nine k-tiles, one partial tile
+    (1, 3, 5, 1024, False, False, 128),   # one partial tile, no epilogue options
+    (6, 56, 56, 64, False, True, 64),     # the R101 64->64 stage-1 shape: K = 64, 74 tiles, ragged
+    (4, 56, 56, 256, False, True, 64),    # 256->64
+    (9, 64, 64, 96, True, True, 64),      # K = 96: three k-tiles, residual, 144 tiles
+    (1, 3, 5, 64, True, False, 64),       # one partial tile
 ])
-def test_h2_persistent_256x128_tile_bit_identical(cuda, b, h, w, cin, res, relu):
-    """The 256x128 form of config 15 (the pick for dense N = 128, K >= 256)
-    computes each output column with config 12's products in config 12's
-    order: a 128-channel layer equals the first 128 channels of the same layer
-    at 256 channels on config 12 (per-channel weight scales: the sliced planes
-    are the same), bit for bit, and its max-|y| record is exact."""
+def test_h2_persistent_narrow_tile_bit_identical(cuda, b, h, w, cin, res, relu, nout):
+    """The 256x128 and 256x64 forms of config 15 (the picks for dense N = 128,
+    K >= 256 and N = 64, K >= 64) compute each output column with config 12's
+    products in config 12's order: an N-channel layer equals the first N
+    channels of the same layer at 256 channels on config 12 (per-channel weight
+    scales: the sliced planes are the same), bit for bit, and its max-|y|
+    record is exact."""
     x, wt, bias, r, _, _ = _conv_case(cuda, b, h, w, cin, 256, 1, 1, 0, res, seed=19)
     xd = x.to(cuda)
     rec = ops.amax_records(3, cuda)
@@ -301,11 +306,11 @@ def test_h2_persistent_256x128_tile_bit_identical(cuda, b, h, w, cin, res, relu)
     with ops.tuning(0, s3_cfg=12):
         y256 = ops.conv2d_h2(xd, rec[0], ops.H2Conv(wt.to(cuda)), bias.to(cuda), 1, 0,
                              r.to(cuda) if res else None, relu, rec[1]).cpu()
-    r128 = r[..., :128].contiguous().to(cuda) if res else None
-    y128 = ops.conv2d_h2(xd, rec[0], ops.H2Conv(wt[:128].contiguous().to(cuda)), bias[:128].contiguous().to(cuda),
-                         1, 0, r128, relu, rec[2]).cpu()
-    assert torch.equal(y128, y256[..., :128])
-    assert ops.amax_value(rec[2]) == float(y128.abs().max())
+    rn = r[..., :nout].contiguous().to(cuda) if res else None
+    yn = ops.conv2d_h2(xd, rec[0], ops.H2Conv(wt[:nout].contiguous().to(cuda)), bias[:nout].contiguous().to(cuda),
+                       1, 0, rn, relu, rec[2]).cpu()
+    assert torch.equal(yn, y256[..., :nout])
+    assert ops.amax_value(rec[2]) == float(yn.abs().max())
 
 
 @pytest.mark.parametrize("b,h,w,cin,cout,k,s,p,res,cfg", [
