@@ -1248,12 +1248,15 @@ static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
 // form (waves of 128x32, two B DMA instructions per wave, 96 KB of LDS) for
 // N = 128; FN = 1, WM = 4: the 256x64 form (waves 4 x 2 of 64x32, one B DMA
 // instruction per wave spanning both planes, slabs of four 32-row bands, 80
-// KB) for N = 64.  Every column of either is config 12's column bit for bit.
+// KB) for N = 64, with config 7's two accumulator sets (ACC2: its arithmetic
+// at K = 64, where one accumulator's error passes the exact-fp32 core's).
+// Every column of the 256x128 form is config 12's column bit for bit, the
+// 256x64 form's output config 7's.
 // Counted waits: vector-memory operations retire in issue order (stores
 // included), so each wait names how many younger operations may remain; where
 // fewer were issued (rows past M store nothing) the wait is longer, never
 // shorter.
-template <int EPI, int FN = 2, int WM = 2>
+template <int EPI, int FN = 2, int WM = 2, int ACC2 = 0>
 __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_n, int ntiles) {
   static_assert((EPI & EP_SCALE) != 0, "f16x2: scaled epilogue");
   static_assert((WM == 2 && (FN == 1 || FN == 2)) || (WM == 4 && FN == 1), "256x256, 256x128 or 256x64");
@@ -1381,14 +1384,19 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
   };
 
   // ---- MFMAs: config 12's 16-deep k-step (st = 0, 1 of the k-tile) ----
-  f32x16 acc[FM][FN];
+  // ACC2: config 7's two accumulator sets (a0b0 in acc, a0b1 + a1b0 in lo,
+  // summed before the epilogue)
+  f32x16 acc[FM][FN], lo[ACC2 ? FM : 1][ACC2 ? FN : 1];
   auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+        for (int r = 0; r < 16; ++r) {
+          acc[i][j][r] = 0.f;
+          if constexpr (ACC2) lo[i][j][r] = 0.f;
+        }
   };
   zero_acc();
   auto compute_st = [&](int cur, int st) __attribute__((always_inline)) {
@@ -1416,8 +1424,9 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
-        acc[i][j] = s3_mf32<2>(a[0][i], b[1][j], acc[i][j]);
-        acc[i][j] = s3_mf32<2>(a[1][i], b[0][j], acc[i][j]);
+        f32x16& L = ACC2 ? lo[ACC2 ? i : 0][ACC2 ? j : 0] : acc[i][j];
+        L = s3_mf32<2>(a[0][i], b[1][j], L);
+        L = s3_mf32<2>(a[1][i], b[0][j], L);
       }
   };
 
@@ -1465,7 +1474,9 @@ __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_
 #pragma unroll
       for (int j = 0; j < FN; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) cw[acc_row<false>(0, r, le) * CS + acc_col<false>(j, r, le)] = acc[sl][j][r];
+        for (int r = 0; r < 16; ++r)
+          cw[acc_row<false>(0, r, le) * CS + acc_col<false>(j, r, le)] =
+              ACC2 ? acc[sl][j][r] + lo[ACC2 ? sl : 0][ACC2 ? j : 0][r] : acc[sl][j][r];
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
@@ -1595,7 +1606,7 @@ static bool s3q_fits(const GemmArgs& g) {
   return (long long)g.M * g.lda * 4 < lim && (long long)g.M * g.ldc * 4 < lim;
 }
 
-template <int EPI, int FN = 2, int WM = 2>
+template <int EPI, int FN = 2, int WM = 2, int ACC2 = 0>
 static hipError_t launch_s3q_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / (32 * FN * (8 / WM));
   const long long ntiles = tiles_m * tiles_n;
@@ -1606,7 +1617,7 @@ static hipError_t launch_s3q_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
   const int grid = ntiles <= slots ? (int)ntiles : slots;
   g.stagger_blocks = grid;
   g.stagger_sleeps = ntiles > 2LL * grid ? stagger : 0;
-  hipLaunchKernelGGL((gemm_s3q_kernel<EPI, FN, WM>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
+  hipLaunchKernelGGL((gemm_s3q_kernel<EPI, FN, WM, ACC2>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles_n, (int)ntiles);
   return hipGetLastError();
 }
 
@@ -2359,10 +2370,10 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
       }
       if (g.N == 64 && g.K >= 64 && s3q_fits(g)) {
         switch (ep_flags(g) & (EP_RES | EP_RELU)) {
-          case EP_RELU: return launch_s3q_t<H2_EP | EP_RELU, 1, 4>(g, s, n_cu, st);
-          case EP_RES | EP_RELU: return launch_s3q_t<H2_EP | EP_RES | EP_RELU | EP_SC1, 1, 4>(g, s, n_cu, st);
-          case EP_RES: return launch_s3q_t<H2_EP | EP_RES | EP_SC1, 1, 4>(g, s, n_cu, st);
-          default: return launch_s3q_t<H2_EP, 1, 4>(g, s, n_cu, st);
+          case EP_RELU: return launch_s3q_t<H2_EP | EP_RELU, 1, 4, 1>(g, s, n_cu, st);
+          case EP_RES | EP_RELU: return launch_s3q_t<H2_EP | EP_RES | EP_RELU | EP_SC1, 1, 4, 1>(g, s, n_cu, st);
+          case EP_RES: return launch_s3q_t<H2_EP | EP_RES | EP_SC1, 1, 4, 1>(g, s, n_cu, st);
+          default: return launch_s3q_t<H2_EP, 1, 4, 1>(g, s, n_cu, st);
         }
       }
     }

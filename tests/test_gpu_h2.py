@@ -80,6 +80,9 @@ CONV_SHAPES = [  # b, h, w, cin, cout, k, stride, pad, residual
     (4, 7, 7, 512, 2048, 1, 1, 0, True),
     (2, 14, 14, 256, 256, 3, 1, 1, True),
     (3, 21, 19, 128, 512, 1, 1, 0, True),
+    (4, 28, 28, 64, 64, 1, 1, 0, False),    # dense N = 64, K = 64 (config 15's 256x64 form)
+    (3, 28, 30, 256, 64, 1, 1, 0, False),   # dense N = 64, K = 256
+    (2, 28, 28, 512, 128, 1, 1, 0, False),  # dense N = 128 (its 256x128 form)
 ]
 
 
@@ -293,23 +296,28 @@ def test_h2_persistent_256_tile_bit_identical(cuda, b, h, w, cin, cout, res, rel
     (1, 3, 5, 64, True, False, 64),       # one partial tile
 ])
 def test_h2_persistent_narrow_tile_bit_identical(cuda, b, h, w, cin, res, relu, nout):
-    """The 256x128 and 256x64 forms of config 15 (the picks for dense N = 128,
-    K >= 256 and N = 64, K >= 64) compute each output column with config 12's
-    products in config 12's order: an N-channel layer equals the first N
-    channels of the same layer at 256 channels on config 12 (per-channel weight
-    scales: the sliced planes are the same), bit for bit, and its max-|y|
-    record is exact."""
+    """The 256x128 form of config 15 (the pick for dense N = 128, K >= 256)
+    computes each output column with config 12's products in config 12's
+    order: a 128-channel layer equals the first 128 channels of the same layer
+    at 256 channels on config 12 (per-channel weight scales: the sliced planes
+    are the same), bit for bit.  The 256x64 form (dense N = 64, K >= 64) keeps
+    config 7's two accumulator sets and k order: the same layer on config 7,
+    bit for bit.  Both max-|y| records exact."""
     x, wt, bias, r, _, _ = _conv_case(cuda, b, h, w, cin, 256, 1, 1, 0, res, seed=19)
     xd = x.to(cuda)
     rec = ops.amax_records(3, cuda)
     ops.amax_f32(xd, rec[0])
-    with ops.tuning(0, s3_cfg=12):
-        y256 = ops.conv2d_h2(xd, rec[0], ops.H2Conv(wt.to(cuda)), bias.to(cuda), 1, 0,
-                             r.to(cuda) if res else None, relu, rec[1]).cpu()
     rn = r[..., :nout].contiguous().to(cuda) if res else None
-    yn = ops.conv2d_h2(xd, rec[0], ops.H2Conv(wt[:nout].contiguous().to(cuda)), bias[:nout].contiguous().to(cuda),
-                       1, 0, rn, relu, rec[2]).cpu()
-    assert torch.equal(yn, y256[..., :nout])
+    wn, bn = ops.H2Conv(wt[:nout].contiguous().to(cuda)), bias[:nout].contiguous().to(cuda)
+    if nout == 64:
+        with ops.tuning(0, s3_cfg=7):
+            ref = ops.conv2d_h2(xd, rec[0], wn, bn, 1, 0, rn, relu, rec[1]).cpu()
+    else:
+        with ops.tuning(0, s3_cfg=12):
+            ref = ops.conv2d_h2(xd, rec[0], ops.H2Conv(wt.to(cuda)), bias.to(cuda), 1, 0,
+                                r.to(cuda) if res else None, relu, rec[1]).cpu()[..., :nout]
+    yn = ops.conv2d_h2(xd, rec[0], wn, bn, 1, 0, rn, relu, rec[2]).cpu()
+    assert torch.equal(yn, ref)
     assert ops.amax_value(rec[2]) == float(yn.abs().max())
 
 
