@@ -37,19 +37,18 @@ from research_image_retrieval_amd.extract import _rescale  # noqa: E402
 
 METRIC = "images embedded+ranked/sec on 1.6M×2048 gallery; mAP on ROxf/RPar"
 # MI355X_MICROARCH.md: dense MFMA peaks (TFLOP/s) per input dtype, HBM3E peak.
-# "s3": fp32 products as six bf16 MFMA products (gemm_s3.hip, SP 3), so its
-# ceiling in algorithmic fp32 FLOP/s is the bf16 peak / 6; "h2": three fp16
-# MFMA products (the f16x2 split, SP 2), the fp16 dense peak (= bf16's) / 3.
+# "h2": three fp16 MFMA products per fp32 product (the f16x2 split), so its
+# ceiling in algorithmic fp32 FLOP/s is the fp16 dense peak (= bf16's) / 3;
+# "s3": the ceiling of round 2's retired six-product bf16 split (the bf16
+# peak / 6), kept only as the frac_of_bf16x3_ceiling comparison.
 PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0, "fp8": 5000.0, "s3": 2500.0 / 6, "h2": 2500.0 / 3}
 SPLIT_MATH = {
-    "s3": (6, "fp32 via exact 3-way bf16 split: 6 bf16 MFMA products per fp32 product, fp32 accumulation; "
-              "peak = bf16 dense peak / 6"),
     "h2": (3, "fp32-accurate f16x2 split at power-of-two scales: 3 fp16 MFMA products per fp32 product "
               "(a0b0 + a0b1 + a1b0), fp32 accumulation; tested bar vs float64 (tests/test_gpu_h2.py): per conv "
               "mean error <= 1.05x the exact-fp32 core's and max <= 1.25x (1.5x for the fused stage-entry "
               "bottleneck), descriptors <= 2x the exact-fp32 trunk's and <= 1e-6; peak = fp16 dense peak / 3"),
 }
-WEIGHT_BYTES = {"s3": 6, "h2": 4, "f32": 4}
+WEIGHT_BYTES = {"h2": 4, "f32": 4}
 PEAK_HBM_GBS = 8000.0
 
 
@@ -500,12 +499,10 @@ def main():
     ap.add_argument("--ranker", choices=("exhaustive", "prefilter"), default="prefilter",
                     help="fp32 exact ranking: exhaustive fp32 MFMA sweep, or the bf16-bound prefilter + exact "
                          "fp32 rescoring (bit-identical results)")
-    ap.add_argument("--conv-math", choices=("h2", "s3", "f32"), default="h2",
+    ap.add_argument("--conv-math", choices=("h2", "f32"), default="h2",
                     help="ResNet trunk convs: h2 = fp32-accurate f16x2 split on the fp16 matrix cores, 3 MFMA "
                          "products per fp32 product (tested bar vs float64, tests/test_gpu_h2.py: per conv mean "
-                         "error <= 1.05x and max <= 1.25x the exact-fp32 core's); s3 = 3-way bf16 split, 6 "
-                         "products (tests/test_gpu_s3.py); "
-                         "f32 = exact fp32 MFMA")
+                         "error <= 1.05x and max <= 1.25x the exact-fp32 core's); f32 = exact fp32 MFMA")
     ap.add_argument("--ws-budget-gb", type=float, default=4.0,
                     help="ranker workspace budget per rank (bounded candidate buffers, overflowed queries re-run; "
                          "0 = the worst-case size, ~Q*N*8 bytes)")

@@ -51,14 +51,22 @@ typedef struct rr_handle_s* rr_handle_t;
  * rr_split2_f16 / rr_amax_f32 were added (no existing entry changed); 4 =
  * rr_linear_bf16_ln / rr_ln_partials_bf16 were added (round 4; the ViT
  * LayerNorm fold); 5 = rr_bottleneck_seam_h2 was added and the tuning keys
- * RR_TUNE_SWEEP_ORDER (6), RR_TUNE_SWEEP_PF (7) and RR_TUNE_LP_IL (12) and the
- * lp_cfg value 6 were retired (round 5: they lost their A/Bs; rr_set_tuning
- * now returns RR_EINVAL for them, and their numbers are not reused), and
- * rr_linear_bf16_ln / rr_ln_partials_bf16 now centre the bf16 rows on their
- * 256-column tile means with colsum per k tile (same arguments, new layout).
+ * RR_TUNE_SWEEP_ORDER (6), RR_TUNE_SWEEP_PF (7) and RR_TUNE_LP_IL (12)
+ * were retired (round 5: they lost their A/Bs; rr_set_tuning returns
+ * RR_EINVAL for them, and their numbers are not reused); RR_TUNE_LP_CFG value
+ * 6 (the gallery-in-VGPR sweep) was retired then too, and the number was
+ * REDEFINED in the same revision as the tests' hook for the three-A-stage
+ * persistent bf16 tile (a caller of the old value 6 now gets that tile on
+ * stored-C GEMMs and the cost-based pick on sweeps); and rr_linear_bf16_ln /
+ * rr_ln_partials_bf16 now centre the bf16 rows on their 256-column tile
+ * means with colsum per k tile (same arguments, new layout); 6 = entries
+ * REMOVED: rr_bottleneck_seam_h2 (round 5's block seam, measured slower
+ * than the two launches it fused) and the split-bf16 core's rr_conv2d_s3 /
+ * rr_linear_s3 / rr_split3_bf16 (superseded by the f16x2 core in round 3);
+ * the tuning key RR_TUNE_SWEEP_FORM (14) was added (round 6).
  * Bindings compare rr_abi_version() with the RR_ABI_VERSION they were
  * written against.                                                          */
-#define RR_ABI_VERSION 5
+#define RR_ABI_VERSION 6
 int rr_abi_version(void);
 
 /* ---- handle ------------------------------------------------------------ */
@@ -90,12 +98,12 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     the ViT epilogues, N % 256 == 0 and K <= 1024, the persistent
  *                     256x256 k-stream; its one-tile form is 3), 1 (128x128), 2 (256x64),
  *                     3 (256x256), 6 (the persistent form with three A stages for the
- *                     epilogues without the LayerNorm fold, at any K; tests),
+ *                     epilogues without the LayerNorm fold, at any K; tests; this
+ *                     value's meaning changed in ABI 5, see above),
  *                     4 (256x320 for bf16 filter / score sweeps, 256x256 otherwise),
  *                     5 (bf16 sweeps with K % 128 == 0, fp8 sweeps with K % 256 == 0:
  *                     256x256 8-phase pipeline; otherwise as 3)
- *   RR_TUNE_S3_CFG:   split cores (bf16x3 and f16x2), 1..15 (gemm_s3.hip tile table;
- *                     9..15 f16x2 only; 13 = the halo-staged stride-1 3x3 tile on
+ *   RR_TUNE_S3_CFG:   f16x2 split core, 1..15 (gemm_s3.hip tile table; 13 = the halo-staged stride-1 3x3 tile on
  *                     v_mfma_f32_32x32x16_f16, 14 = the same on v_mfma_f32_16x16x32_f16
  *                     (the default picks 14's form for cout % 256 == 0, 13's for cout 64);
  *                     15 = the 256x256 tile (12) as a persistent k-stream (the default
@@ -104,7 +112,7 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     K >= 64; forced, every other
  *                     GEMM runs the library's pick; 12 forces the one-tile-per-block form);
  *                     7 also selects the implicit-GEMM fused stem over the halo stem)
- *   RR_TUNE_S3_STAGGER: split-bf16 core first-round stagger, 0..200 sleeps of
+ *   RR_TUNE_S3_STAGGER: split core first-round stagger, 0..200 sleeps of
  *                     ~1 us for every other resident block (-1 = the library's pick)
  *   RR_TUNE_SWEEP_MF16: the 256x320 bf16 filter sweep on v_mfma_f32_16x16x32_bf16 (1)
  *                     or v_mfma_f32_32x32x16_bf16 (0); -1 = the library's pick (0)
@@ -122,6 +130,11 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     13 / 14 override it)
  *   RR_TUNE_S3_CFG_RES: as RR_TUNE_S3_CFG, for the split-core GEMMs with a residual
  *                     epilogue only (0 = RR_TUNE_S3_CFG's choice)
+ *   RR_TUNE_SWEEP_FORM: the bf16 filter sweeps (the prefilter's pass 2, bf16
+ *                     rr_cosine_topk_lp): 0 = the gemm core's tiles (RR_TUNE_LP_CFG
+ *                     applies), 1 = the hand-scheduled 16x16x32 sweep (csrc/sweep16.hip)
+ *                     on 128-B LDS rows (K % 64 == 0; else as 2), 2 = the same on
+ *                     64-B rows; -1 = the library's pick
  * Any other key or value: RR_EINVAL. */
 #define RR_TUNE_GEMM_CFG 1
 #define RR_TUNE_GEMM_BK 2
@@ -135,6 +148,7 @@ int rr_get_device(rr_handle_t h, int* device);
 #define RR_TUNE_HALO_MF 11
 /* 12: retired (ABI 5) */
 #define RR_TUNE_S3_CFG_RES 13
+#define RR_TUNE_SWEEP_FORM 14
 int rr_set_tuning(rr_handle_t h, int key, int value);
 
 /* ---- search (ranker) ----------------------------------------------------
@@ -313,35 +327,9 @@ int rr_resize_bilinear(rr_handle_t h, const float* x, int b, int hgt, int wid,
                        int c, int out_h, int out_w, float inv_scale_h,
                        float inv_scale_w, float* y, void* stream);
 
-/* fp32-accurate convolution on the bf16 matrix cores (gemm_s3.hip): the
- * same operation, layouts and epilogue as rr_conv2d, with the weights given
- * as three bf16 planes w3 [3][cout][kh][kw][cin] from rr_split3_bf16 and the
- * activations split in-kernel (x = x0 + x1 + x2 exactly; six bf16 MFMA
- * products per fp32 product, error vs float64 at or below the exact-fp32
- * MFMA's).  Needs cin % 32 == 0, or cin == 4 for the NHWC4 stem (RGB + a
- * zero channel): then w3 is [3][cout][Kp], the flattened [kh][kw][4] filter
- * zero-padded to Kp = kh*kw*4 rounded up to 32.  Replaces the same reference
- * ops as rr_conv2d (networks/backbone.py:103-109, models/gem_pooling.py:44,61). */
-int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid,
-                 int cin, const void* w3, const float* bias, int cout, int kh,
-                 int kw, int stride, int pad, const float* residual, int relu,
-                 float* y, void* stream);
-
-/* y = x . w^T + bias (+ residual, act as rr_linear_ex) on the split-bf16
- * core; w3 = three bf16 planes [3][n][k] (rr_split3_bf16); k % 32 == 0.    */
-int rr_linear_s3(rr_handle_t h, const float* x, int m, int k, const void* w3,
-                 const float* bias, int n, const float* residual, int act,
-                 float* y, void* stream);
-
-/* Exact 3-way bf16 split of fp32 x[n]: planes [3][n] (bf16 bit patterns),
- * x = p0 + p1 + p2 exactly (p0 = x truncated to bf16, p1 = the same of the
- * remainder, p2 = the rest).  Done once per weight tensor.                 */
-int rr_split3_bf16(rr_handle_t h, const float* x, long long n, void* planes,
-                   void* stream);
-
 /* fp32-accurate convolution on the fp16 matrix cores (gemm_s3.hip, f16x2
- * split): the same operation, layouts and epilogue as rr_conv2d_s3 at half
- * its MFMA count.  Every fp32 operand is scaled by a power of two and split
+ * split): the same operation, layouts and epilogue as rr_conv2d on the
+ * 16-bit MFMA at three fp16 products per fp32 product.  Every fp32 operand is scaled by a power of two and split
  * into two fp16 pieces, x 2^e = x0 + x1 + r with |r| <= 2^-22 |x 2^e|; a.b
  * keeps a0b0 + (a0b1 + a1b0) (dropped terms <= 3 2^-22 |a||b|), three fp16
  * MFMAs with exact products and fp32 accumulation (a0b0 in its own
@@ -381,30 +369,6 @@ int rr_bottleneck_out_h2(rr_handle_t h, const float* y, const unsigned* y_amax,
                          int stride, const void* w2, const float* w_iscale,
                          const float* bias, int cout, float* out,
                          unsigned* out_amax, void* stream);
-
-/* The seam between two bottleneck blocks of a stage on the f16x2 core, as
- * ONE launch: block i's conv3 with its residual and block i+1's conv1,
- *   out = ReLU(y2 . W3^T + b3 + res)        [m][4 planes]  (block i's output)
- *   h1  = ReLU(out . W1^T + b1)             [m][planes]    (block i+1's conv1)
- * (torchvision Bottleneck / the reference's ResBlock + BottleneckTransform,
- * networks/backbone.py:305-346), so block i's output is written once and
- * never read back for the next conv1.  y2: block i's conv2 output [m][planes]
- * with its max-|x| record y2_amax; res: block i's input [m][4 planes];
- * w3 / w3_iscale: rr_split2_f16 of conv3's [4 planes][planes] weights; w1 /
- * w1_iscale: rr_split2_f16 of the next conv1's [planes][4 planes]; b3 / b1
- * may be NULL.  out_amax / h1_amax (optional, zeroed by the caller): the
- * max-|x| records of out and h1.  planes = 64, 128 or 256; every pointer
- * 16-byte aligned.  `out` equals rr_conv2d_h2's conv3 (+ residual, ReLU) bit
- * for bit where that call runs its 256 x 256 one-accumulator tile (K >= 256);
- * h1's A operand is split at the running max of each 128-row group's
- * outputs instead of one scale per tensor, which rounds no differently except
- * where it keeps more low bits (tests/test_gpu_seam.py).                     */
-int rr_bottleneck_seam_h2(rr_handle_t h, const float* y2, const unsigned* y2_amax,
-                          int m, int planes, const float* res, const void* w3,
-                          const float* w3_iscale, const float* b3, const void* w1,
-                          const float* w1_iscale, const float* b1, float* out,
-                          unsigned* out_amax, float* h1, unsigned* h1_amax,
-                          void* stream);
 
 /* The ResNet stem on the f16x2 core with its max-pool fused: NHWC4 conv
  * (cin == 4, as rr_conv2d_h2) + bias + ReLU, then the 3x3 stride-2 padding-1

@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("RR_LIB_PATH") or os.path.join(_HERE, "librr.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 RR_OK, RR_EINVAL, RR_EHIP, RR_EWORKSPACE, RR_EOVERFLOW = 0, -1, -2, -3, -4
-ABI_VERSION = 5  # RR_ABI_VERSION of include/rr.h these signatures follow
+ABI_VERSION = 6  # RR_ABI_VERSION of include/rr.h these signatures follow
 AMAX_SLOTS = 64  # RR_AMAX_SLOTS
 
 # timing classes (rr_timing_enable / rr_timing_collect)
@@ -24,8 +24,8 @@ TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM, TIME_COSINE_SEED, TIME_ATTN = 0,
 # rr_set_tuning keys
 # (6, 7 and 12 -- sweep_order, sweep_pf, lp_il -- were retired in ABI 5)
 TUNE_GEMM_CFG, TUNE_GEMM_BK, TUNE_LP_CFG, TUNE_S3_CFG, TUNE_S3_STAGGER, \
-    TUNE_SWEEP_MF16, TUNE_SWEEP_IL, TUNE_CONV_IL, TUNE_HALO_MF, TUNE_S3_CFG_RES = \
-    1, 2, 3, 4, 5, 8, 9, 10, 11, 13
+    TUNE_SWEEP_MF16, TUNE_SWEEP_IL, TUNE_CONV_IL, TUNE_HALO_MF, TUNE_S3_CFG_RES, TUNE_SWEEP_FORM = \
+    1, 2, 3, 4, 5, 8, 9, 10, 11, 13, 14
 
 _lib = None
 _lock = threading.RLock()
@@ -60,16 +60,11 @@ SIGNATURES = {
     "rr_preprocess_u8_ex": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _i, _vp, _vp]),
     "rr_nchw_to_nhwc_ex": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp]),
     "rr_conv2d": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
-    "rr_conv2d_s3": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp]),
-    "rr_linear_s3": (_i, [_vp, _vp, _i, _i, _vp, _vp, _i, _vp, _i, _vp, _vp]),
-    "rr_split3_bf16": (_i, [_vp, _vp, _ll, _vp, _vp]),
     "rr_conv2d_h2": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp]),
     "rr_split2_f16": (_i, [_vp, _vp, _i, _i, _i, _vp, _vp, _vp]),
     "rr_stem_pool_h2": (_i, [_vp, _vp, _vp, _i, _i, _i, _vp, _vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
     "rr_bottleneck_out_h2": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _vp,
                                   _vp, _vp]),
-    "rr_bottleneck_seam_h2": (_i, [_vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
-                                   _vp]),
     "rr_amax_f32": (_i, [_vp, _vp, _ll, _vp, _vp]),
     "rr_resize_bilinear": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _f, _f, _vp, _vp]),
     "rr_maxpool2d": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),

@@ -965,6 +965,16 @@ static hipError_t launch_lp(const GemmArgs& g, hipStream_t s, const rr_handle_s:
   int cfg = pick_lp(g, EM, DT == DT_BF16, tu);
   if (g.stats_out != nullptr || g.stats_in != nullptr) cfg = 3;  // the LayerNorm fold: 256-column tiles
   if ((cfg == 3 || cfg == 4) && (g.K % EPR) != 0) cfg = 1;  // LDS-DMA configs need whole k-tiles
+  if constexpr (EM == E_FILTER && DT == DT_BF16) {
+    // the hand-scheduled 16x16x32 sweep on 128-B LDS rows (sweep16.hip): the
+    // pick for K >= 1024 (the C3 prefilter's 1.6 M x 2048 sweep).  Measured
+    // against the 256x320 tile below (tools/prefilter_ab.py, 1280 queries,
+    // profiles/r06m_*): random queries 9.57 -> 7.26 ms, near-parallel 7.39 ->
+    // 7.04, and 6.86 -> 7.01 on identical queries (the bench's random-weight
+    // descriptors); at K = 512 (C4) 2.43 -> 2.49 ms, so short K keeps the tile
+    const int form = tu.sweep_form >= 0 ? tu.sweep_form : (g.K >= 1024 && (g.K % 64) == 0 ? 1 : 0);
+    if ((form == 1 || form == 2) && sweep16_eligible(g)) return launch_sweep16(g, s, form == 1);
+  }
   if constexpr (EM == E_FILTER) {
     // the 256x320 bf16 tile's default: v_mfma_f32_32x32x16_bf16 with the next
     // k-tile's DMA spread among the MFMAs (sweep_il).  On the C3 bench's own

@@ -1,28 +1,26 @@
-// gemm_s3.hip — fp32-accurate GEMM on the bf16 matrix cores (3-way split).
+// gemm_s3.hip — fp32-accurate GEMM on the 16-bit matrix cores: the f16x2
+// split core of the ResNet trunk (rr_conv2d_h2, rr_bottleneck_out_h2,
+// rr_stem_pool_h2; networks/backbone.py:60-109, :305-346).
 //
 // gfx950 has no xf32/TF32 MFMA, and its f32-input MFMA runs at 1/16 of the
-// bf16 rate (MI355X_MICROARCH.md: 157 vs 2500 TF/s dense).  Every fp32 value
-// is split EXACTLY into three bf16 pieces, x = x0 + x1 + x2:
-//   x0 = x with the low 16 bits cleared, x1 = the same of x - x0,
-//   x2 = x - x0 - x1 (at most 8 significant bits left, so exact in bf16);
-// |x1| < 2^-7 |x|, |x2| < 2^-15 |x|.  The product a.b keeps the six terms of
-// order >= 2^-15 — a0b0 + (a0b1 + a1b0) + (a0b2 + a1b1 + a2b0) — each a bf16
-// MFMA (exact products, fp32 accumulation); the dropped terms are < 2^-22
-// |a||b|, below fp32's own rounding of a long dot product.  a0b0 accumulates
-// in one register tile and the five small terms in a second one, so the small
-// terms never round against the large running sum; the two are added once in
-// the epilogue.  Measured against float64 (tests/test_gpu_s3.py), the error
-// is at or below the exact-fp32 MFMA fmaf chain's.  Six bf16 MFMAs cost 6/16
-// of one f32 MFMA: the fp32 convolutions of the ResNet trunk
-// (networks/backbone.py:60-109) run on this core.
+// bf16 rate (MI355X_MICROARCH.md: 157 vs 2500 TF/s dense).  Every fp32
+// operand is scaled by a power of two and split into two fp16 pieces,
+// x 2^e = x0 + x1 + r with |r| <= 2^-22 |x 2^e|; a.b keeps a0b0 (its own
+// accumulator) + a0b1 + a1b0 (DESIGN.md, f16x2 split core): three fp16 MFMAs
+// per fp32 product with exact products and fp32 accumulation, error vs
+// float64 at the exact-fp32 MFMA chain's (tests/test_gpu_h2.py).
+//
+// The kernel templates carry the split kind SP (planes per operand).  Rounds
+// 1-2 ran a three-plane bf16 split (SP 3: six bf16 MFMAs per product) here;
+// it lost to f16x2 in round 3 and its instantiations and entry points
+// (rr_conv2d_s3, rr_linear_s3, rr_split3_bf16) were retired in ABI 6: SP 2
+// is the only split these templates compile for (static_assert).
 //
 // Operands: A = fp32 activations (dense rows or the implicit im2col of an
 // NHWC map with Cin % 32 == 0), split in registers while staging into LDS;
-// B = weights pre-split once on the host side into three bf16 planes
-// [3][N][K] (rr_split3_bf16), copied global -> LDS by LDS-DMA
-// (global_load_lds).  LDS per stage: 3 planes of A and 3 of B, BK bf16 per
-// plane row, 16-B slots XOR-swizzled so both the staging writes and the
-// fragment ds_read_b128 (v_mfma_f32_32x32x16_bf16 operands) are conflict-free.
+// B = weights pre-split once into fp16 planes [2][N][K] (rr_split2_f16),
+// copied global -> LDS by LDS-DMA (global_load_lds).  16-B slots of the LDS
+// rows are XOR-swizzled so the fragment ds_read_b128 are conflict-free.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -104,7 +102,7 @@ struct S3Phases {
 // k-tile but one instruction group at a time among the first MFMAs of its
 // first k-step (see gemm_f32.hip IL: a burst of every wave's loads at once
 // fills the vector-memory issue queue and stalls the MFMAs behind it).
-template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0, int EPI = -1, int SP = 3,
+template <int WM, int WN, int FM, int FN, int BK, int AMODE, int MINB, int MF16 = 0, int EPI = -1, int SP = 2,
           int NSTG = 2, int POOL = 0, int ACC1 = 0, int IL = 0>
 __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g, int tiles_n) {
   static_assert(!ACC1 || SP == 2, "one accumulator: the f16x2 split");
@@ -112,7 +110,7 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
   static_assert(NSTG == 2 || (NSTG == 3 && MF16 && SP == 2), "three LDS stages: the f16x2 16x16x32 tile");
   static_assert(!IL || (!MF16 && NSTG == 2 && !POOL), "IL: the 32x32x16 two-stage loop");
   static_assert(!MF16 || BK == 32, "MF16: BK 32");
-  static_assert(SP == 2 || SP == 3, "split kind");
+  static_assert(SP == 2, "split kind: f16x2 (the bf16x3 instantiations were retired in ABI 6)");
   static_assert(SP == 3 || (EPI >= 0 && (EPI & EP_SCALE)), "f16x2: scaled epilogue");
   typedef typename S3Frag<SP>::T frag_t;
   constexpr int NP = SP;                     // planes per operand
@@ -810,9 +808,9 @@ __global__ __launch_bounds__(64 * WM * WN, MINB) void gemm_s3_kernel(GemmArgs g,
 // epilogue / loader switch cannot be hoisted out of the loop -- its results
 // would then be live through the whole k-loop and spill it)
 
-template <int EPI, int SP = 3, int SEG2 = 0>
+template <int EPI, int SP = 2, int SEG2 = 0>
 __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_n, int ntiles) {
-  static_assert(!SEG2 || SP == 2, "two-segment A: f16x2 only");
+  static_assert(SP == 2, "split kind: f16x2 (the bf16x3 instantiations were retired in ABI 6)");
   static_assert(SP == 3 || (EPI & EP_SCALE), "f16x2: scaled epilogue");
   typedef typename S3Frag<SP>::T frag_t;
   constexpr int NP = SP;
@@ -1213,7 +1211,7 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
   if constexpr (SP == 2) RR_PH_FLUSH(1);
 }
 
-template <int EPI, int SP = 3, int SEG2 = 0>
+template <int EPI, int SP = 2, int SEG2 = 0>
 static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   const long long tiles_m = (g.M + 127) / 128, tiles_n = g.N / 256;
   const long long ntiles = tiles_m * tiles_n;
@@ -2178,15 +2176,11 @@ static hipError_t launch_s3p(const GemmArgs& g, hipStream_t s, int n_cu, int st)
       default: return launch_s3p_t<H2_EP, 2>(g, s, n_cu, st);
     }
   } else {
-    switch (ep_flags(g)) {
-      case EP_BIAS | EP_RELU: return launch_s3p_t<EP_BIAS | EP_RELU>(g, s, n_cu, st);
-      case EP_BIAS | EP_RES | EP_RELU: return launch_s3p_t<EP_BIAS | EP_RES | EP_RELU>(g, s, n_cu, st);
-      default: return launch_s3p_t<EP_BIAS>(g, s, n_cu, st);
-    }
+    static_assert(SP == 2, "launch_s3p: the f16x2 split only (ABI 6)");
   }
 }
 
-template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int EPI = -1, int SP = 3,
+template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int EPI = -1, int SP = 2,
           int NSTG = 2, int POOL = 0, int ACC1 = 0, int IL = 0>
 static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) {
   constexpr int BM = 32 * FM * WM, BN = 32 * FN * WN;
@@ -2236,7 +2230,7 @@ static hipError_t launch_s3_t(GemmArgs g, hipStream_t s, int n_cu, int stagger) 
 //      dense N == 128, K >= 256, its 256x64 form dense N == 64, K >= 64
 // (all others on v_mfma_f32_32x32x16_{bf16,f16}).  The f16x2 split is built
 // for configs 3, 4, 7, 8, 9, 10 and 11 (a forced 1, 2, 5 or 6 runs the pick).
-// Measured per R101 layer at 320 images (tools/s3_bench.py): 3 is the fastest
+// Measured per R101 layer at 320 images (round 2's tools/s3_bench.py): 3 is the fastest
 // wherever N >= 128 (1.1-1.3x config 1 per FLOP); 4 on 16x16x32 runs every
 // N % 256 == 0 layer 3-14 % faster than 3 (the 16x16 shape holds a higher
 // clock on random operands, MI355X_MICROARCH.md 'DVFS give-back' item 7; the
@@ -2281,7 +2275,7 @@ static int pick_h2(const GemmArgs& g, int forced) {
 // The picked configs (3, 4, 7) with the ResNet's epilogues compiled in:
 // conv + BN + ReLU, + residual + ReLU, projection conv + BN (f16x2: the four
 // residual / ReLU combinations of H2_EP).
-template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int SP = 3, int NSTG = 2,
+template <int WM, int WN, int FM, int FN, int BK, int AM, int MINB, int MF16 = 0, int SP = 2, int NSTG = 2,
           int ACC1 = 0, int IL = 0>
 static hipError_t launch_s3_ep(const GemmArgs& g, hipStream_t s, int n_cu, int st) {
   if constexpr (SP == 2) {
@@ -2296,37 +2290,7 @@ static hipError_t launch_s3_ep(const GemmArgs& g, hipStream_t s, int n_cu, int s
       default: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, H2_EP, 2, NSTG, 0, ACC1, IL>(g, s, n_cu, st);
     }
   } else {
-    switch (ep_flags(g)) {
-      case EP_BIAS | EP_RELU: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS | EP_RELU>(g, s, n_cu, st);
-      case EP_BIAS | EP_RES | EP_RELU:
-        return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS | EP_RES | EP_RELU>(g, s, n_cu, st);
-      case EP_BIAS: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16, EP_BIAS>(g, s, n_cu, st);
-      default: return launch_s3_t<WM, WN, FM, FN, BK, AM, MINB, MF16>(g, s, n_cu, st);
-    }
-  }
-}
-
-template <int AM>
-static hipError_t launch_s3_am(const GemmArgs& g, hipStream_t s, int forced, int n_cu, int st) {
-  int cfg = pick_s3(g, forced);
-  // config 8 is the default wherever it serves (every dense R101 layer with
-  // N % 256 == 0: 1.0-1.1x config 4, residual expansions -4 to -9 %,
-  // profiles/r02k_s3p_ab.txt)
-  if (forced == 0 && AM == A_DENSE && s3_persist_ok<3>(g, AM)) cfg = 8;
-  if (cfg == 8) {
-    if constexpr (AM == A_DENSE) {
-      if (s3_persist_ok<3>(g, AM)) return launch_s3p<3>(g, s, n_cu, st);
-    }
-    cfg = pick_s3(g, 0);  // a shape or flag set config 8 does not serve
-  }
-  switch (cfg) {
-    case 2: return launch_s3_t<2, 2, 2, 2, 32, AM, 1>(g, s, n_cu, st);
-    case 3: return launch_s3_ep<4, 2, 2, 2, 32, AM, 1>(g, s, n_cu, st);
-    case 4: return launch_s3_ep<2, 4, 2, 2, 32, AM, 1, 1>(g, s, n_cu, st);
-    case 5: return launch_s3_t<4, 1, 2, 2, 32, AM, 1>(g, s, n_cu, st);
-    case 6: return launch_s3_t<4, 1, 2, 2, 16, AM, 2>(g, s, n_cu, st);
-    case 7: return launch_s3_ep<8, 1, 1, 2, 16, AM, 4>(g, s, n_cu, st);
-    default: return launch_s3_t<2, 2, 2, 2, 16, AM, 2>(g, s, n_cu, st);
+    static_assert(SP == 2, "launch_s3_ep: the f16x2 split only (ABI 6)");
   }
 }
 
@@ -2684,13 +2648,11 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
     return set_error(h, RR_EINVAL, "gemm_s3: unsupported A mode");
   if ((g.ldb & 7) || (g.b_plane & 7) || ((uintptr_t)g.B & 15))
     return set_error(h, RR_EINVAL, "gemm_s3: B planes need ldb % 8 == 0, plane stride % 8 == 0, 16-B alignment");
-  if (sp != 2 && sp != 3) return set_error(h, RR_EINVAL, "gemm_s3: split kind must be 2 or 3");
-  if (sp == 2) {
-    if (g.col_scale == nullptr || g.a_amax == nullptr || ((uintptr_t)g.col_scale & 15))
-      return set_error(h, RR_EINVAL, "gemm_h2: needs 16-B aligned column scales and the A max-|x| record");
-    if (g.relu == 2 || g.out_bf16 || (g.N & 3) || (g.ldc & 3))
-      return set_error(h, RR_EINVAL, "gemm_h2: fp32 output, ReLU or none, N % 4 == 0");
-  }
+  if (sp != 2) return set_error(h, RR_EINVAL, "gemm_h2: the f16x2 split (the bf16x3 core was retired in ABI 6)");
+  if (g.col_scale == nullptr || g.a_amax == nullptr || ((uintptr_t)g.col_scale & 15))
+    return set_error(h, RR_EINVAL, "gemm_h2: needs 16-B aligned column scales and the A max-|x| record");
+  if (g.relu == 2 || g.out_bf16 || (g.N & 3) || (g.ldc & 3))
+    return set_error(h, RR_EINVAL, "gemm_h2: fp32 output, ReLU or none, N % 4 == 0");
   if (g.M == 0) return RR_OK;
   // default stagger: the residual layers only (their 256 KB-per-tile epilogue
   // is the HBM-heavy phase): 256->1024 x23 -5 %, the other residual layers
@@ -2701,7 +2663,7 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
     TimedLaunch tl(h, timer_cls, s);
     const int f = (g.residual != nullptr && h->tune.s3_cfg_res > 0) ? h->tune.s3_cfg_res : h->tune.s3_cfg;
     const int n_cu = device_cu_count(h);
-    if (sp == 2) {
+    {
       // conv_il (opt-in): every R101 layer the 256x256 tile serves ran 1-3 %
       // faster alone at 1280 images (256->1024 0.681 -> 0.668 ms; profiles/
       // r04g_h2_cfg_il.txt, r04h_h2_cfg_il.txt), but the bench's whole embed
@@ -2714,30 +2676,9 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
       e = amode == A_DENSE ? launch_h2_am<A_DENSE>(g2, s, f, n_cu, st)
           : amode == A_CONV ? launch_h2_am<A_CONV>(g2, s, f, n_cu, st)
                             : launch_h2_am<A_CONV_C4>(g2, s, f, n_cu, st);
-    } else
-      e = amode == A_DENSE ? launch_s3_am<A_DENSE>(g, s, f, n_cu, st)
-          : amode == A_CONV ? launch_s3_am<A_CONV>(g, s, f, n_cu, st)
-                            : launch_s3_am<A_CONV_C4>(g, s, f, n_cu, st);
+    }
   }
-  return check_hip(h, e, sp == 2 ? "gemm_h2 launch" : "gemm_s3 launch");
-}
-
-// ---- weight split: x[n] -> planes [3][n] of bf16 (x0, x1, x2) ----
-__global__ void split3_kernel(const float* __restrict__ x, long long n, uint16_t* __restrict__ planes) {
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
-    uint32_t h, m, l;
-    split3(x[i], h, m, l);
-    planes[i] = (uint16_t)(h >> 16);
-    planes[n + i] = (uint16_t)(m >> 16);
-    planes[2 * n + i] = (uint16_t)(l >> 16);
-  }
-}
-
-int launch_split3(rr_handle_s* h, const float* x, long long n, uint16_t* planes, hipStream_t s) {
-  if (n <= 0) return RR_OK;
-  const long long blocks = std::min<long long>((n + 255) / 256, 4096);
-  hipLaunchKernelGGL(split3_kernel, dim3((unsigned)blocks), dim3(256), 0, s, x, n, planes);
-  return check_hip(h, hipGetLastError(), "split3 launch");
+  return check_hip(h, e, "gemm_h2 launch");
 }
 
 // ---- weight split, f16x2: row n of w [rows][k] at scale 2^e_n (h2_exp of

@@ -1,5 +1,6 @@
-// h2_common.hpp — pieces shared by the split-core GEMM kernels (gemm_s3.hip,
-// gemm_seam.hip): vector types, the f16x2 / bf16x3 MFMA wrappers, the f16x2
+// h2_common.hpp — pieces of the split-core GEMM kernels (gemm_s3.hip):
+// vector types, the f16x2 MFMA wrappers (and the retired bf16x3 ones the
+// SP-templated kernels still name), the f16x2
 // split of an 8-k chunk, the plane-row slot swizzle and the asynchronous
 // (inline-asm) A loads with their register laundering.
 #pragma once

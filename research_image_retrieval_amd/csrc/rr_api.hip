@@ -77,7 +77,7 @@ using namespace rr;
 
 extern "C" {
 
-const char* rr_version(void) { return "librr 0.3.0 (gfx950: fp32 / f16x2 / bf16x3 / bf16 / fp8 MFMA)"; }
+const char* rr_version(void) { return "librr 0.4.0 (gfx950: fp32 / f16x2 / bf16 / fp8 MFMA)"; }
 
 int rr_abi_version(void) { return RR_ABI_VERSION; }
 
@@ -170,6 +170,10 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
     case RR_TUNE_S3_CFG_RES:
       if (value < 0 || value > 15) break;
       h->tune.s3_cfg_res = value;
+      return RR_OK;
+    case RR_TUNE_SWEEP_FORM:
+      if (!in({-1, 0, 1, 2})) break;
+      h->tune.sweep_form = value;
       return RR_OK;
     default:
       return set_error(h, RR_EINVAL, "rr_set_tuning: unknown key");
@@ -482,51 +486,6 @@ int rr_conv2d(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, c
   return launch_gemm(h, amode, E_STORE, g, (hipStream_t)stream, kTimeGemm);
 }
 
-int rr_conv2d_s3(rr_handle_t h, const float* x, int b, int hgt, int wid, int cin, const void* w3,
-                 const float* bias, int cout, int kh, int kw, int stride, int pad, const float* residual, int relu,
-                 float* y, void* stream) {
-  RR_ENTRY(h);
-  if (!x || !w3 || !y || b < 0 || hgt <= 0 || wid <= 0 || cin <= 0 || cout <= 0 || kh <= 0 || kw <= 0 ||
-      stride <= 0 || pad < 0 || relu < 0 || relu > 1)
-    return set_error(h, RR_EINVAL, "rr_conv2d_s3: bad argument");
-  if (cin % 32 && cin != 4) return set_error(h, RR_EINVAL, "rr_conv2d_s3: cin must be a multiple of 32, or 4 (NHWC4 stem)");
-  const int oh = (hgt + 2 * pad - kh) / stride + 1, ow = (wid + 2 * pad - kw) / stride + 1;
-  if (oh <= 0 || ow <= 0) return set_error(h, RR_EINVAL, "rr_conv2d_s3: empty output");
-  const long long M = (long long)b * oh * ow;
-  if (M > 0x7fffffffLL) return set_error(h, RR_EINVAL, "rr_conv2d_s3: too many output pixels");
-  if (((uintptr_t)x & 15) || ((uintptr_t)w3 & 15)) return set_error(h, RR_EINVAL, "rr_conv2d_s3: x/w3 must be 16-byte aligned");
-  // cout % 4 == 0: the epilogue's vector path (f32x4 bias, 16-byte C / residual rows)
-  if ((cout & 3) == 0 && (((uintptr_t)y & 15) || (bias && ((uintptr_t)bias & 15)) || (residual && ((uintptr_t)residual & 15))))
-    return set_error(h, RR_EINVAL, "rr_conv2d_s3: bias/residual/y must be 16-byte aligned");
-  GemmArgs g;
-  g.A = x;
-  g.M = (int)M;
-  g.K = kh * kw * cin;
-  g.H = hgt;
-  g.W = wid;
-  g.Cin = cin;
-  g.OH = oh;
-  g.OW = ow;
-  g.KH = kh;
-  g.KW = kw;
-  g.stride = stride;
-  g.pad = pad;
-  // NHWC4 stem: the weight planes hold K = KH*KW*4 padded with zeros to a multiple of 32
-  if (cin == 4) g.K = (g.K + 31) / 32 * 32;
-  g.B = reinterpret_cast<const float*>(w3);
-  g.ldb = g.K;
-  g.b_plane = (long long)cout * g.K;
-  g.N = cout;
-  g.C = y;
-  g.ldc = cout;
-  g.bias = bias;
-  g.residual = residual;
-  g.relu = relu;
-  const bool dense = kh == 1 && kw == 1 && stride == 1 && pad == 0 && cin != 4;
-  if (dense) g.lda = cin;
-  return launch_gemm_s3(h, dense ? A_DENSE : (cin == 4 ? A_CONV_C4 : A_CONV), g, (hipStream_t)stream, kTimeGemm);
-}
-
 int rr_conv2d_h2(rr_handle_t h, const float* x, const unsigned* x_amax, int b, int hgt, int wid, int cin,
                  const void* w2, const float* w_iscale, const float* bias, int cout, int kh, int kw, int stride,
                  int pad, const float* residual, int relu, float* y, unsigned* y_amax, void* stream) {
@@ -684,34 +643,6 @@ int rr_amax_f32(rr_handle_t h, const float* x, long long n, unsigned* amax, void
   return launch_amax(h, x, n, amax, (hipStream_t)stream);
 }
 
-int rr_linear_s3(rr_handle_t h, const float* x, int m, int k, const void* w3, const float* bias, int n,
-                 const float* residual, int act, float* y, void* stream) {
-  RR_ENTRY(h);
-  if (!x || !w3 || !y || m < 0 || k <= 0 || n <= 0 || act < 0 || act > 2) return set_error(h, RR_EINVAL, "rr_linear_s3: bad argument");
-  if (k % 32) return set_error(h, RR_EINVAL, "rr_linear_s3: k must be a multiple of 32");
-  GemmArgs g;
-  g.A = x;
-  g.lda = k;
-  g.M = m;
-  g.K = k;
-  g.B = reinterpret_cast<const float*>(w3);
-  g.ldb = k;
-  g.b_plane = (long long)n * k;
-  g.N = n;
-  g.C = y;
-  g.ldc = n;
-  g.bias = bias;
-  g.residual = residual;
-  g.relu = act;
-  return launch_gemm_s3(h, A_DENSE, g, (hipStream_t)stream, kTimeGemm);
-}
-
-int rr_split3_bf16(rr_handle_t h, const float* x, long long n, void* planes, void* stream) {
-  RR_ENTRY(h);
-  if (!x || !planes || n < 0) return set_error(h, RR_EINVAL, "rr_split3_bf16: bad argument");
-  TimedLaunch tl(h, kTimeElem, (hipStream_t)stream);
-  return launch_split3(h, x, n, reinterpret_cast<uint16_t*>(planes), (hipStream_t)stream);
-}
 
 int rr_linear(rr_handle_t h, const float* x, int m, int k, const float* w, const float* bias, int n, float* y,
               void* stream) {

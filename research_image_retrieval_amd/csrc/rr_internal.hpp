@@ -27,6 +27,7 @@ struct rr_handle_s {
     int conv_il = -1;      // f16x2 256x256 conv tile (s3_cfg 12) and halo 16x16x32 tile: next k-tiles' loads spread among the MFMAs (1) or one burst (0); -1: the pick (0)
     int halo_mf = -1;      // f16x2 halo 3x3 tiles on v_mfma_f32_16x16x32_f16 (1) or 32x32x16 (0); -1: the pick (the 256x256 tile 1, the others 0)
     int s3_cfg_res = 0;    // split cores: forced tile config for the GEMMs with a residual epilogue only (0: s3_cfg's)
+    int sweep_form = -1;   // bf16 filter sweeps: 0 = gemm_f32.hip's tiles, 1 / 2 = sweep16.hip on 128-B / 64-B LDS rows; -1: the pick
   } tune;
   int n_cu = 0;  // compute units of the handle's device (device_cu_count)
   // timing (see rr_timing_enable)
@@ -277,10 +278,9 @@ int launch_gemm(rr_handle_s* h, int amode, int emode, const GemmArgs& a, hipStre
                 int dt = DT_F32);
 
 // fp32-accurate GEMM on the 16-bit matrix cores (gemm_s3.hip): A fp32
-// (A_DENSE, A_CONV or A_CONV_C4), E_STORE epilogue; sp = 3: B = bf16 planes
-// [3][N][ldb] from launch_split3; sp = 2: B = fp16 planes [2][N][ldb] +
-// col_scale from launch_split2h, A scaled by its a_amax
-int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls, int sp = 3);
+// (A_DENSE, A_CONV or A_CONV_C4), E_STORE epilogue; sp must be 2: B = fp16
+// planes [2][N][ldb] + col_scale from launch_split2h, A scaled by its a_amax
+int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, int timer_cls, int sp = 2);
 // f16x2 two-segment GEMM (GemmArgs A2 / K1): the persistent tile, N % 256 == 0
 int launch_gemm_h2_seg2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int timer_cls);
 // f16x2 NHWC4 stem conv + ReLU + 3x3/2 pad-1 max-pool (GemmArgs pool_*), N == 64
@@ -296,7 +296,6 @@ int launch_amax(rr_handle_s* h, const float* x, long long n, uint32_t* slots, hi
 // MFMA): dense A/B, K a multiple of two k-tiles
 bool gemm_8p_eligible(const GemmArgs& g, int dt);
 hipError_t launch_gemm_8p(const GemmArgs& g, int emode, hipStream_t s, int dt);
-int launch_split3(rr_handle_s* h, const float* x, long long n, uint16_t* planes, hipStream_t s);
 
 // ---- top-k kernels (topk.hip) -------------------------------------------
 // Dense scores, query-major [nq][ld] (first `rows` valid) -> per query the
@@ -314,6 +313,12 @@ int launch_prefilter_rescore(rr_handle_s* h, unsigned long long* cand, long long
                              const float* eps2, float* t2, const float* q, const float* g, int d, hipStream_t s);
 int launch_merge(rr_handle_s* h, const float* ps, const long long* pi, int nparts, int nq, int kin,
                  int kout, float* os, long long* oi, hipStream_t s);
+
+// sweep16.hip: the bf16 filter sweep on 16x16x32 MFMA with a hand-placed
+// k-loop (256 gallery rows x 320 queries per block, 8 waves); rows128: LDS
+// rows of 128 B (K % 64 == 0; else 64-B rows)
+bool sweep16_eligible(const GemmArgs& g);
+hipError_t launch_sweep16(const GemmArgs& g, hipStream_t s, int rows128);
 
 // gemm_lpp.hip: the bf16 stored-C GEMM as a persistent 256x256 k-stream
 bool lpp_eligible(const GemmArgs& g);

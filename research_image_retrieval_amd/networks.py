@@ -27,9 +27,8 @@ class ResNet:
     mean error vs float64 within 1.05x and max within 1.25x of the exact-fp32
     core's, descriptors within 2x and <= 1e-6, tests/test_gpu_h2.py; three
     fp16 MFMAs per product; weights split once here, each conv publishes max
-    |y| for the next one's split scale); "s3" runs them on the split-bf16 core
-    (six bf16 MFMAs per product); "f32" keeps all convs on the exact-fp32 MFMA
-    core.
+    |y| for the next one's split scale); "f32" keeps all convs on the
+    exact-fp32 MFMA core.  (The split-bf16 core, "s3", was retired in round 6.)
 
     stride_on: "3x3" (default) = torchvision v1.5 bottlenecks; "1x1" = the
     reference's own torchvision-free R101, ResNet_DOLG
@@ -41,8 +40,8 @@ class ResNet:
     outputdim_block4 = 1024
 
     def __init__(self, name="resnet101", state_dict=None, seed=0, device="cuda", conv_math="h2", stride_on="3x3"):
-        if conv_math not in ("h2", "s3", "f32"):
-            raise ValueError("conv_math must be 'h2', 's3' or 'f32'")
+        if conv_math not in ("h2", "f32"):
+            raise ValueError("conv_math must be 'h2' or 'f32'")
         W.block_strides(1, stride_on)  # validates
         self.stride_on = stride_on
         if name not in W.RESNET_LAYERS:
@@ -57,21 +56,13 @@ class ResNet:
         self.convs = {k: (w.to(self.device), b.to(self.device)) for k, (w, b) in folded.items()}
         self.layers = W.RESNET_LAYERS[name]
         self.conv_math = conv_math
-        self.convs_s3 = {}
-        self.stem_s3 = None
         self.convs_h2 = {}
-        if conv_math == "s3":
-            self.convs_s3 = {k: ops.split3_bf16(w) for k, (w, _) in self.convs.items() if w.shape[-1] % 32 == 0}
-            self.stem_s3 = ops.split3_stem(self.convs["conv1"][0])
-        elif conv_math == "h2":
+        if conv_math == "h2":
             self.convs_h2 = {k: ops.H2Conv(w) for k, (w, _) in self.convs.items()}
             # each stage's first block: conv3 + downsample as one GEMM (ops.H2Bottleneck)
             self.fuse_downsample = True
             # the stem conv + ReLU + max-pool as one launch (ops.stem_pool_h2)
             self.fuse_stem_pool = True
-            # block i's conv3 (+ residual) and block i+1's conv1 as one launch
-            # inside a stage (ops.bottleneck_seam_h2) for planes 64 / 128 / 256
-            self.fuse_seams = False  # measured per release: see DESIGN.md (the seam kernel)
             self.bneck_h2 = {}
             for li in range(len(self.layers)):
                 p = f"layer{li + 1}.0"
@@ -81,11 +72,6 @@ class ResNet:
 
     def _conv(self, x, name, stride, pad, relu, residual=None):
         w, b = self.convs[name]
-        if name == "conv1" and self.stem_s3 is not None:
-            return ops.conv2d_s3_stem(x, self.stem_s3[0], self.stem_s3[1], b, stride, pad, relu)
-        w3 = self.convs_s3.get(name)
-        if w3 is not None:
-            return ops.conv2d_s3(x, w3, b, stride, pad, residual, relu)
         return ops.conv2d(x, w, b, stride, pad, residual, relu)
 
     def _forward_h2(self, x, return_x3):
@@ -96,10 +82,7 @@ class ResNet:
         its ReLU and the max-pool run as one launch (ops.stem_pool_h2), so the
         stem's full-resolution map never reaches HBM.  A stage's
         first block runs conv3 and its downsample projection as one GEMM
-        (ops.bottleneck_out_h2), so the projected identity never reaches HBM;
-        inside a stage, block i's conv3 and block i+1's conv1 run as one
-        launch (ops.bottleneck_seam_h2, fuse_seams), so block i's output is
-        not read back for that conv1."""
+        (ops.bottleneck_out_h2), so the projected identity never reaches HBM."""
         cv, h2 = self.convs, self.convs_h2
         rec = ops.amax_records(2 + 3 * sum(self.layers), x.device)
         ops.amax_f32(x, rec[0])
@@ -110,27 +93,16 @@ class ResNet:
             x = ops.maxpool2d(x, 3, 2, 1)
         xa, r, x3 = rec[1], 2, None
         for li, nb in enumerate(self.layers):
-            h1 = None  # the next block's conv1 output, when a seam launch produced it
             for bi in range(nb):
                 p = f"layer{li + 1}.{bi}"
                 s1, s2 = W.block_strides(2 if (bi == 0 and li > 0) else 1, self.stride_on)
                 d = f"{p}.downsample.0"
                 fused = bi == 0 and self.fuse_downsample and p in self.bneck_h2
                 idn = ops.conv2d_h2(x, xa, h2[d], cv[d][1], s1 * s2, 0, None, False) if bi == 0 and not fused else x
-                if h1 is None:
-                    y = ops.conv2d_h2(x, xa, h2[f"{p}.conv1"], cv[f"{p}.conv1"][1], s1, 0, None, True, rec[r])
-                else:
-                    y = h1
+                y = ops.conv2d_h2(x, xa, h2[f"{p}.conv1"], cv[f"{p}.conv1"][1], s1, 0, None, True, rec[r])
                 y = ops.conv2d_h2(y, rec[r], h2[f"{p}.conv2"], cv[f"{p}.conv2"][1], s2, 1, None, True, rec[r + 1])
-                # a seam: this block's conv3 with the next (non-entry) block's conv1
-                seam = (self.fuse_seams and 1 <= bi < nb - 1 and h2[f"{p}.conv3"].cin in (64, 128, 256))
-                h1 = None
                 if fused:
                     x = ops.bottleneck_out_h2(y, rec[r + 1], x, xa, self.bneck_h2[p], s1 * s2, rec[r + 2])
-                elif seam:
-                    q = f"layer{li + 1}.{bi + 1}.conv1"
-                    x, h1 = ops.bottleneck_seam_h2(y, rec[r + 1], idn, h2[f"{p}.conv3"], cv[f"{p}.conv3"][1], h2[q],
-                                                   cv[q][1], rec[r + 2], rec[r + 3])
                 else:
                     x = ops.conv2d_h2(y, rec[r + 1], h2[f"{p}.conv3"], cv[f"{p}.conv3"][1], 1, 0, idn, True,
                                       rec[r + 2])
@@ -367,12 +339,16 @@ class VisionTransformer(_Extractor):
                 for k in ("attn.in_proj_weight", "attn.out_proj.weight", "mlp.c_fc.weight", "mlp.c_proj.weight"):
                     blk[k + ".bf16"] = blk[k].to(torch.bfloat16)
                 # ln_1 / ln_2 folded into the in-proj / c_fc GEMMs (rr_linear_bf16_ln)
+                if not ops.ln_fold_supported(width, dtype):
+                    continue
                 blk["qkv.fold"] = ops.ln_fold_weights(blk["attn.in_proj_weight"], blk["attn.in_proj_bias"],
                                                       blk["ln_1.weight"], blk["ln_1.bias"])
                 blk["fc.fold"] = ops.ln_fold_weights(blk["mlp.c_fc.weight"], blk["mlp.c_fc.bias"],
                                                      blk["ln_2.weight"], blk["ln_2.bias"])
-        # the LayerNorm fold needs 256-column residual rows
-        self.ln_fold = dtype == "bf16" and width % 256 == 0
+        # the LayerNorm fold needs 256-column residual rows and K <= 768 (a
+        # wider model, e.g. ViT-L/14's 1024, which networks/model.py:405
+        # builds, runs the LayerNorm passes)
+        self.ln_fold = ops.ln_fold_supported(width, dtype)
 
     def _forward_bf16(self, x_nhwc, b):
         # patch rows straight to bf16; ln_pre fused into the token assembly

@@ -89,101 +89,6 @@ def conv2d(x, w, bias, stride=1, pad=0, residual=None, relu=False):
     return y
 
 
-def split3_bf16(x):
-    """Exact 3-way bf16 split of an fp32 tensor: int16 planes [3, *x.shape]
-    (bf16 bit patterns) with x == p0 + p1 + p2 exactly (rr_split3_bf16)."""
-    x = _f32(x.contiguous(), "split3_bf16")
-    dev = _dev(x)
-    planes = torch.empty((3,) + tuple(x.shape), dtype=torch.int16, device=x.device)
-    hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_split3_bf16(hd, _ptr(x), x.numel(), _ptr(planes), _stream(dev)), hd, "rr_split3_bf16")
-    return planes
-
-
-def split3_stem(w):
-    """Weight planes of an NHWC4 stem conv for conv2d_s3: w [Cout,KH,KW,4]
-    flattened to [Cout, KH*KW*4], zero-padded to a multiple of 32, split
-    (int16 [3, Cout, Kp]); the kernel shape travels in stem_shape."""
-    w = _f32(w.contiguous(), "split3_stem")
-    cout, kh, kw, c = w.shape
-    if c != 4:
-        raise ValueError("split3_stem: NHWC4 filters (4 input channels)")
-    k = kh * kw * 4
-    kp = (k + 31) // 32 * 32
-    flat = torch.nn.functional.pad(w.reshape(cout, k), (0, kp - k)).contiguous()
-    return split3_bf16(flat), (kh, kw)
-
-
-def conv2d_s3_stem(x, w3p, stem_shape, bias, stride, pad, relu=True):
-    """The NHWC4 stem conv on the split-bf16 core (rr_conv2d_s3, cin == 4)."""
-    _f32(x, "conv2d_s3_stem x")
-    if x.shape[-1] != 4:
-        raise ValueError("conv2d_s3_stem: x must be NHWC4")
-    kh, kw = stem_shape
-    cout, kp = w3p.shape[1], w3p.shape[2]
-    if w3p.dtype != torch.int16 or w3p.shape[0] != 3 or kp != (kh * kw * 4 + 31) // 32 * 32 or not w3p.is_contiguous():
-        raise ValueError("conv2d_s3_stem: w3p must be split3_stem planes")
-    dev = _dev(x)
-    b, h, wd, _ = x.shape
-    oh = (h + 2 * pad - kh) // stride + 1
-    ow = (wd + 2 * pad - kw) // stride + 1
-    y = torch.empty((b, oh, ow, cout), dtype=torch.float32, device=x.device)
-    if bias is not None:
-        _f32(bias, "conv2d_s3_stem bias")
-    hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_conv2d_s3(hd, _ptr(x), b, h, wd, 4, _ptr(w3p), _ptr(bias), cout, kh, kw, stride, pad,
-                                       None, int(relu), _ptr(y), _stream(dev)), hd, "rr_conv2d_s3 (stem)")
-    return y
-
-
-def conv2d_s3(x, w3, bias, stride=1, pad=0, residual=None, relu=False):
-    """conv2d on the split-bf16 core: fp32-accurate, w3 = split3_bf16(w) with
-    w [Cout,KH,KW,Cin], Cin % 32 == 0."""
-    _f32(x, "conv2d_s3 x")
-    if w3.dtype != torch.int16 or w3.dim() != 5 or w3.shape[0] != 3 or not w3.is_contiguous():
-        raise ValueError("conv2d_s3: w3 must be contiguous int16 [3,Cout,KH,KW,Cin] (split3_bf16)")
-    dev = _dev(x)
-    b, h, wd, cin = x.shape
-    _, cout, kh, kw, cin_w = w3.shape
-    if cin_w != cin:
-        raise ValueError(f"conv2d_s3: Cin mismatch {cin} vs {cin_w}")
-    oh = (h + 2 * pad - kh) // stride + 1
-    ow = (wd + 2 * pad - kw) // stride + 1
-    y = torch.empty((b, oh, ow, cout), dtype=torch.float32, device=x.device)
-    if residual is not None:
-        _f32(residual, "conv2d_s3 residual")
-        if tuple(residual.shape) != tuple(y.shape):
-            raise ValueError("conv2d_s3: residual shape mismatch")
-    if bias is not None:
-        _f32(bias, "conv2d_s3 bias")
-    hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_conv2d_s3(hd, _ptr(x), b, h, wd, cin, _ptr(w3), _ptr(bias), cout, kh, kw, stride, pad,
-                                       _ptr(residual), int(relu), _ptr(y), _stream(dev)), hd, "rr_conv2d_s3")
-    return y
-
-
-def linear_s3(x, w3, bias=None, residual=None, act=0):
-    """y = act(x @ w.T + bias + residual) on the split-bf16 core; w3 =
-    split3_bf16(w) with w [N,K], K % 32 == 0."""
-    _f32(x, "linear_s3 x")
-    if w3.dtype != torch.int16 or w3.dim() != 3 or w3.shape[0] != 3 or not w3.is_contiguous():
-        raise ValueError("linear_s3: w3 must be contiguous int16 [3,N,K] (split3_bf16)")
-    dev = _dev(x)
-    m, k = x.shape
-    n = w3.shape[1]
-    if w3.shape[2] != k:
-        raise ValueError("linear_s3: K mismatch")
-    y = torch.empty((m, n), dtype=torch.float32, device=x.device)
-    if residual is not None:
-        _f32(residual, "linear_s3 residual")
-        if tuple(residual.shape) != (m, n):
-            raise ValueError("linear_s3: residual shape mismatch")
-    hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_linear_s3(hd, _ptr(x), m, k, _ptr(w3), _ptr(bias), n, _ptr(residual), int(act), _ptr(y),
-                                       _stream(dev)), hd, "rr_linear_s3")
-    return y
-
-
 AMAX_SLOTS = 64  # RR_AMAX_SLOTS: words of one tensor's max-|x| record
 
 
@@ -332,39 +237,6 @@ def bottleneck_out_h2(y, y_amax, x, x_amax, wb, stride, out_amax=None):
                                                _ptr(wb.bias), wb.cout, _ptr(out), _ptr(out_amax), _stream(dev)),
                hd, "rr_bottleneck_out_h2")
     return out
-
-
-def bottleneck_seam_h2(y2, y2_amax, res, c3, b3, c1, b1, out_amax=None, h1_amax=None):
-    """Block i's conv3 (+ residual, ReLU) and block i+1's conv1 (+ ReLU) as one
-    f16x2 launch (rr_bottleneck_seam_h2): y2 [B,H,W,P] (block i's conv2
-    output, record y2_amax), res [B,H,W,4P] (block i's input), c3 / c1 the
-    1x1 H2Conv weights (4P x P and P x 4P).  -> (out [B,H,W,4P], h1
-    [B,H,W,P])."""
-    _f32(y2, "bottleneck_seam_h2 y2")
-    _f32(res, "bottleneck_seam_h2 res")
-    if not isinstance(c3, H2Conv) or not isinstance(c1, H2Conv):
-        raise TypeError("bottleneck_seam_h2: c3 and c1 must be ops.H2Conv")
-    b, h, w, planes = y2.shape
-    if (c3.kh, c3.kw, c3.cin, c3.cout) != (1, 1, planes, 4 * planes) or \
-            (c1.kh, c1.kw, c1.cin, c1.cout) != (1, 1, 4 * planes, planes):
-        raise ValueError("bottleneck_seam_h2: conv3 must be 1x1 P -> 4P and conv1 1x1 4P -> P")
-    if tuple(res.shape) != (b, h, w, 4 * planes):
-        raise ValueError("bottleneck_seam_h2: residual shape mismatch")
-    for t, nm in ((b3, "b3"), (b1, "b1")):
-        if t is not None:
-            _f32(t, "bottleneck_seam_h2 " + nm)
-    for r, nm in ((y2_amax, "y2_amax"), (out_amax, "out_amax"), (h1_amax, "h1_amax")):
-        if r is not None and (r.dtype != torch.int32 or r.numel() != AMAX_SLOTS or not r.is_contiguous()):
-            raise ValueError(f"bottleneck_seam_h2: {nm} must be a contiguous int32 [RR_AMAX_SLOTS] record")
-    dev = _dev(y2)
-    out = torch.empty((b, h, w, 4 * planes), dtype=torch.float32, device=y2.device)
-    h1 = torch.empty((b, h, w, planes), dtype=torch.float32, device=y2.device)
-    hd = _lib.handle(dev)
-    _lib.check(_lib.lib().rr_bottleneck_seam_h2(hd, _ptr(y2), _ptr(y2_amax), b * h * w, planes, _ptr(res),
-                                                _ptr(c3.planes), _ptr(c3.iscale), _ptr(b3), _ptr(c1.planes),
-                                                _ptr(c1.iscale), _ptr(b1), _ptr(out), _ptr(out_amax), _ptr(h1),
-                                                _ptr(h1_amax), _stream(dev)), hd, "rr_bottleneck_seam_h2")
-    return out, h1
 
 
 def resize_bilinear(x_nhwc, out_h, out_w, scale_factor=None):
@@ -553,9 +425,10 @@ def topk_merge(part_scores, part_idx, k_out):
 _TUNE_KEYS = {"gemm_cfg": _lib.TUNE_GEMM_CFG, "gemm_bk": _lib.TUNE_GEMM_BK, "lp_cfg": _lib.TUNE_LP_CFG,
               "s3_cfg": _lib.TUNE_S3_CFG, "s3_stagger": _lib.TUNE_S3_STAGGER, "sweep_mf16": _lib.TUNE_SWEEP_MF16,
               "sweep_il": _lib.TUNE_SWEEP_IL, "conv_il": _lib.TUNE_CONV_IL,
-              "halo_mf": _lib.TUNE_HALO_MF, "s3_cfg_res": _lib.TUNE_S3_CFG_RES}
+              "halo_mf": _lib.TUNE_HALO_MF, "s3_cfg_res": _lib.TUNE_S3_CFG_RES,
+              "sweep_form": _lib.TUNE_SWEEP_FORM}
 _TUNE_DEFAULT = {"s3_stagger": -1, "sweep_mf16": -1, "sweep_il": -1,
-                 "conv_il": -1, "halo_mf": -1}  # the library's own pick (0 elsewhere)
+                 "conv_il": -1, "halo_mf": -1, "sweep_form": -1}  # the library's own pick (0 elsewhere)
 
 
 class tuning:
@@ -779,6 +652,17 @@ def linear_bf16_ln_produce(x, w, bias, residual):
     _lib.check(_lib.lib().rr_linear_bf16_ln(hd, _ptr(x), m, k, _ptr(w), _ptr(bias), n, _ptr(residual), 0, 0, _ptr(y),
                                             None, None, 0.0, _ptr(st), _ptr(yb), _stream(dev)), hd, "rr_linear_bf16_ln")
     return y, yb, st
+
+
+# widest K the fold's consumer serves: rr_linear_bf16_ln stages LN_TMAX = 3
+# column-sum tiles of 256 (csrc/gemm_epilogue.hpp; rr.h: stats_in needs k <= 768)
+LN_FOLD_MAX_K = 768
+
+
+def ln_fold_supported(width, dtype):
+    """Whether the ViT LayerNorm fold (rr_linear_bf16_ln) serves a width:
+    bf16, 256-column tiles, and K = width within the consumer's limit."""
+    return dtype == "bf16" and width % 256 == 0 and width <= LN_FOLD_MAX_K
 
 
 def linear_bf16_ln_fold(xb, stats, w_folded, colsum, bias_folded, act=0, eps=1e-5):

@@ -60,10 +60,6 @@ static void cpu_checks() {
   EXPECT(rr_nchw_to_nhwc_ex(nullptr, nullptr, 1, 1, 1, 1, 1, nullptr, nullptr) == RR_EINVAL);
   EXPECT(rr_conv2d(nullptr, nullptr, 1, 1, 1, 1, nullptr, nullptr, 1, 1, 1, 1, 0, nullptr, 0, nullptr, nullptr) ==
          RR_EINVAL);
-  EXPECT(rr_conv2d_s3(nullptr, nullptr, 1, 1, 1, 32, nullptr, nullptr, 1, 1, 1, 1, 0, nullptr, 0, nullptr, nullptr) ==
-         RR_EINVAL);
-  EXPECT(rr_linear_s3(nullptr, nullptr, 1, 32, nullptr, nullptr, 1, nullptr, 0, nullptr, nullptr) == RR_EINVAL);
-  EXPECT(rr_split3_bf16(nullptr, nullptr, 1, nullptr, nullptr) == RR_EINVAL);
   EXPECT(rr_resize_bilinear(nullptr, nullptr, 1, 1, 1, 1, 1, 1, 0.f, 0.f, nullptr, nullptr) == RR_EINVAL);
   EXPECT(rr_maxpool2d(nullptr, nullptr, 1, 1, 1, 1, 3, 2, 1, nullptr, nullptr) == RR_EINVAL);
   EXPECT(rr_gem_pool(nullptr, nullptr, 1, 1, 1, 3.f, 1e-6f, nullptr, nullptr) == RR_EINVAL);
@@ -142,8 +138,6 @@ static void gpu_checks() {
   EXPECT(rr_cosine_topk(h, q + 1, nq, g, n, d, k, 0, os, oi, ws, ws_n, nullptr) == RR_EINVAL);  // misaligned
   EXPECT(rr_cosine_topk(h, q, nq, g, 0x100000000LL, d, k, 0, os, oi, ws, ws_n, nullptr) == RR_EINVAL);
   EXPECT(rr_conv2d(h, q, 1, 4, 4, 4, g, nullptr, 8, 9, 9, 1, 0, nullptr, 0, os, nullptr) == RR_EINVAL);  // empty out
-  EXPECT(rr_conv2d_s3(h, q, 1, 4, 4, 5, g, nullptr, 8, 1, 1, 1, 0, nullptr, 0, os, nullptr) == RR_EINVAL);  // cin
-  EXPECT(rr_linear_s3(h, q, 2, 33, g, nullptr, 4, nullptr, 0, os, nullptr) == RR_EINVAL);  // k % 32
   EXPECT(rr_alpha_qe(h, q, nq, g, n, d, oi, os, k, k + 1, 3.f, 0, q, nullptr) == RR_EINVAL);  // n > k
   EXPECT(rr_topk_merge(h, os, oi, 0, nq, k, k, os, oi, nullptr) == RR_EINVAL);
   EXPECT(rr_quantize_rows(h, q, nq, d, 3, g, nullptr, nullptr) == RR_EINVAL);

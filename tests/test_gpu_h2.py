@@ -1,7 +1,7 @@
 """The f16x2 split core (gemm_s3.hip, SP 2; rr_conv2d_h2): the power-of-two
 scaled 2-way fp16 split, and fp32-grade accuracy of the convolutions it runs,
 measured against float64 next to the exact-fp32 MFMA core and the split-bf16
-core on the same inputs (the bar tests/test_gpu_s3.py set for the s3 core:
+core on the same inputs (the bar the retired split-bf16 core's tests set:
 error relative to sum |a||b| per output, max and mean, at most the exact-fp32
 core's), plus the max-|y| records the convs hand to each other.
 
@@ -116,14 +116,12 @@ def test_conv2d_h2_vs_float64(cuda, b, h, w, cin, cout, k, s, p, res):
     xd, wd = x.to(cuda), wt.to(cuda)
     rd = r.to(cuda) if res else None
     y_f32 = ops.conv2d(xd, wd, bias.to(cuda), s, p, rd, True).cpu()
-    y_s3 = ops.conv2d_s3(xd, ops.split3_bf16(wd), bias.to(cuda), s, p, rd, True).cpu()
     y_h2 = y_h2.cpu()
     live = ref > 0
     eh2 = _rel_err(y_h2[live], ref[live], scale[live])
     ef32 = _rel_err(y_f32[live], ref[live], scale[live])
-    es3 = _rel_err(y_s3[live], ref[live], scale[live])
     print(f"conv {b}x{h}x{w}x{cin}->{cout} k{k}s{s}: h2 max {eh2[0]:.3g} mean {eh2[1]:.3g} | "
-          f"s3 max {es3[0]:.3g} mean {es3[1]:.3g} | f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
+          f"f32 max {ef32[0]:.3g} mean {ef32[1]:.3g}")
     # mean error at most 1.05x the exact-fp32 core's (+1e-9); max within 1.25x of it: the
     # one-accumulator tiles the library picks for K >= 256, N % 256 == 0
     # (configs 10-12) round the a0b1 + a1b0 terms against the running sum, three

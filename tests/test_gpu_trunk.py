@@ -22,7 +22,7 @@ GOLD = os.path.join(os.path.dirname(__file__), "golden")
 sys.path.insert(0, GOLD)
 import inputs as I  # noqa: E402
 
-# fp32-accurate trunk (exact-fp32 MFMA core, or split-bf16 "s3") vs the CPU
+# fp32-accurate trunk (exact-fp32 MFMA core, or the f16x2 split "h2") vs the CPU
 # reference through 33 bottlenecks; fixture values are O(0.1-1), measured
 # errors 1.2-5.4e-7 (round 2)
 TRUNK_TOL = 2e-6
@@ -33,7 +33,7 @@ def fixture():
     return np.load(os.path.join(GOLD, "resnet_dolg.npz"))
 
 
-@pytest.mark.parametrize("conv_math", ["h2", "s3", "f32"])
+@pytest.mark.parametrize("conv_math", ["h2", "f32"])
 @pytest.mark.parametrize("tag", ["b2_224", "b1_odd"])
 def test_trunk_vs_reference_resnet_dolg(cuda, fixture, conv_math, tag):
     sd = W.to_dolg_keys(W.synthetic_resnet_state_dict("resnet101", int(fixture["weight_seed"])))
@@ -52,7 +52,7 @@ def test_trunk_vs_reference_resnet_dolg(cuda, fixture, conv_math, tag):
         assert err3 < TRUNK_TOL
 
 
-@pytest.mark.parametrize("conv_math", ["h2", "s3", "f32"])
+@pytest.mark.parametrize("conv_math", ["h2", "f32"])
 @pytest.mark.parametrize("tag", ["b2_224", "b1_odd"])
 def test_trunk_v15_vs_reference_modules(cuda, conv_math, tag):
     """The default torchvision-v1.5 placement (stride on the 3x3) against

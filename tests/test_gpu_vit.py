@@ -256,6 +256,22 @@ def test_vit_bf16_ln_fold_matches_unfused(cuda):
     assert float(cos_ref.min()) >= 0.9999
 
 
+def test_vit_bf16_width1024_takes_layernorm_passes(cuda):
+    """ADVICE r5: a width-1024 bf16 ViT (ViT-L/14's width, 16 heads of 64;
+    one block at 112 px to stay small) is past the fold's K <= 768: it runs
+    the LayerNorm passes, and its descriptors match the fp32 network's."""
+    from research_image_retrieval_amd import weights as W
+    sd = W.synthetic_vit_state_dict(width=1024, layers=1, heads=16, res=112, out_dim=256, seed=2)
+    net = VisionTransformer(112, 16, 1024, 1, 16, 256, state_dict=sd, device=cuda, dtype="bf16")
+    assert not net.ln_fold
+    ref = VisionTransformer(112, 16, 1024, 1, 16, 256, state_dict=sd, device=cuda, dtype="fp32")
+    imgs = torch.from_numpy(np.random.RandomState(3).randint(0, 256, size=(4, 112, 112, 3), dtype=np.uint8)).to(cuda)
+    d16 = net.forward_test_u8(imgs).double()
+    d32 = ref.forward_test_u8(imgs).double()
+    assert torch.isfinite(d16).all()
+    assert float((d16 * d32).sum(1).min()) >= 0.9999
+
+
 def test_linear_bf16_ln_argument_checks_and_edges(cuda):
     """rr_linear_bf16_ln: exactly one of stats_in / stats_out, the producer's
     n % 256 and residual requirements, the consumer's k % 64 and bf16 output

@@ -74,3 +74,20 @@ def test_ln_fold_weights_prep():
     assert cs2.shape == (3, 8)
     torch.testing.assert_close(cs2.double(), ref2, rtol=1e-6, atol=1e-6)
     torch.testing.assert_close(bf.double(), b.double() + w.double() @ bet.double(), rtol=1e-6, atol=1e-6)
+
+
+def test_fold_gate_matches_the_kernel_limit():
+    """the network's fold gate and rr_linear_bf16_ln's consumer
+    limit agree (LN_TMAX = 3 column-sum tiles of 256 in
+    csrc/gemm_epilogue.hpp, rr.h: stats_in needs k <= 768), so a wider bf16
+    ViT (ViT-L/14, width 1024, networks/model.py:405) takes the LayerNorm
+    passes instead of failing at its first folded GEMM."""
+    import os
+    import re
+    hpp = os.path.join(os.path.dirname(ops.__file__), "csrc", "gemm_epilogue.hpp")
+    tmax = int(re.search(r"constexpr int LN_TMAX = (\d+)", open(hpp).read()).group(1))
+    assert ops.LN_FOLD_MAX_K == 256 * tmax
+    assert ops.ln_fold_supported(768, "bf16") and ops.ln_fold_supported(512, "bf16")
+    assert not ops.ln_fold_supported(1024, "bf16")  # ViT-L/14
+    assert not ops.ln_fold_supported(640, "bf16")   # not 256-column tiles
+    assert not ops.ln_fold_supported(768, "fp32")

@@ -56,7 +56,7 @@ def split(c):
 
 def owner(k):
     """the extractor object holding attribute k: the extractor itself or a
-    nested part (GeMPCAw.net, GeM.backbone: e.g. fuse_seams on the trunk)"""
+    nested part (GeMPCAw.net, GeM.backbone: e.g. fuse_stem_pool on the trunk)"""
     o = net
     while not hasattr(o, k):
         o = getattr(o, "net", None) or getattr(o, "backbone", None)

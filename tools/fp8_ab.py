@@ -4,7 +4,7 @@ C5 shape (Q fp8 queries x 1.6 M fp8 rows x 2048, top-100) or the C4 bf16
 shape (LP_DT=bf16, d = 512): the sweep launch's HIP-event time, its fraction
 of the dtype's dense peak, and the ranker's top-k compared between configs
 (the accumulation order differs, so scores within 1e-5 and index sets).
-usage: LP_CFGS="0 5" LP_Q=1280 LP_DT=fp8 python tools/fp8_ab.py"""
+usage: [LP_KEY=lp_cfg|sweep_form|...] LP_CFGS="0 5" LP_Q=1280 LP_DT=fp8 python tools/fp8_ab.py"""
 import json
 import os
 import statistics
@@ -20,6 +20,7 @@ dev = torch.device("cuda:0")
 Q = int(os.environ.get("LP_Q", "1280"))
 DT = os.environ.get("LP_DT", "fp8")
 cfgs = [int(c) for c in os.environ.get("LP_CFGS", "0 5").split()]
+KEY = os.environ.get("LP_KEY", "lp_cfg")
 N = int(os.environ.get("LP_N", "1600000"))
 D = int(os.environ.get("LP_D", "2048" if DT == "fp8" else "512"))
 K = 100
@@ -35,7 +36,7 @@ timer = ops.KernelTimer(0)
 
 
 def run(cfg, iters=3):
-    with ops.tuning(0, lp_cfg=cfg):
+    with ops.tuning(0, **{KEY: cfg}):
         ops.cosine_topk_lp(qq, qs, gq, gs, K, DT)
         torch.cuda.synchronize()
         timer.enable(True)
@@ -60,7 +61,7 @@ for c in cfgs:
     ms = statistics.median(res[c])
     ds = (outs[c][0] - outs[base][0]).abs().max().item()
     same_sets = sum(len(set(a.tolist()) & set(b.tolist())) for a, b in zip(outs[c][1].cpu(), outs[base][1].cpu())) / (Q * K)
-    print(json.dumps({"lp_cfg": c, "dtype": DT, "Q": Q, "N": N, "D": D, "sweep_ms": round(ms, 3),
+    print(json.dumps({KEY: c, "dtype": DT, "Q": Q, "N": N, "D": D, "sweep_ms": round(ms, 3),
                       "tflops": round(fl / ms / 1e9, 1), "frac_peak": round(fl / ms / 1e9 / PEAK, 4),
                       "max_score_diff_vs_cfg_%d" % base: ds, "topk_overlap_vs_cfg_%d" % base: round(same_sets, 5)}),
           flush=True)

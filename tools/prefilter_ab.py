@@ -27,8 +27,10 @@ N, D, K = int(os.environ.get("PF_N", "1600000")), 2048, 100
 g = torch.Generator(device=dev).manual_seed(0)
 gal = F.normalize(torch.randn(N, D, device=dev, generator=g), dim=1)
 q = F.normalize(torch.randn(Q, D, device=dev, generator=g), dim=1)
-if os.environ.get("PF_QKIND") == "corr":  # near-parallel queries, like random-weight-network descriptors
+if os.environ.get("PF_QKIND") == "corr":  # near-parallel queries (cosine ~0.999 to each other)
     q = F.normalize(q[:1] + 0.05 * q, dim=1)
+elif os.environ.get("PF_QKIND") == "same":  # the C3 bench's own descriptors: one vector to ~1e-6
+    q = F.normalize(q[:1] + 1e-6 * q, dim=1)
 gbf, _ = ops.quantize_rows(gal, "bf16")
 bound = ops.prefilter_gallery_bound(gal, gbf)
 ws = torch.empty(ops.cosine_topk_prefilter_workspace_size(Q, N, D, K), dtype=torch.uint8, device=dev)

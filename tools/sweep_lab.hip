@@ -1,0 +1,196 @@
+// sweep_lab.hip — ablations of the hand-scheduled bf16 filter sweep
+// (research_image_retrieval_amd/csrc/sweep16.hip) at the C3 shape: 1 567 232
+// gallery rows (1.6 M minus the prefilter's seed rows) x 1280 queries x 2048,
+// bf16, every threshold +inf (no survivors: the loop alone).  Each variant
+// removes one part of the k-loop (ABL bits: 1 = the DMA, 2 = the step-top
+// vmcnt wait + barrier, 4 = the fragment reads and their waits, 8 = the
+// MFMAs); variants are interleaved over rounds in one process, medians
+// reported, on random (Gaussian-like) queries and on near-parallel ones (the
+// bench's random-weight-extractor descriptors are near-parallel).
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/sweep_lab.hip -o tools/sweep_lab
+#include "../research_image_retrieval_amd/csrc/sweep16.hip"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+__device__ inline float lab_hash01(unsigned x) {
+  x ^= x >> 16;
+  x *= 0x7feb352dU;
+  x ^= x >> 15;
+  x *= 0x846ca68bU;
+  x ^= x >> 16;
+  return (x >> 8) * (1.0f / 16777216.0f);
+}
+
+// rows of ~N(0, 1/d) (sum of 4 uniforms), as bf16; corr > 0: every row is
+// base row 0's values + corr x its own noise
+__global__ void lab_fill(uint16_t* p, long long rows, int d, unsigned seed, float corr) {
+  const long long n = rows * d;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(i % d);
+    auto gauss = [&](unsigned s) {
+      const unsigned b = (unsigned)(s * 2654435761u) ^ seed;
+      return (lab_hash01(b) + lab_hash01(b + 1) + lab_hash01(b + 2) + lab_hash01(b + 3) - 2.0f) * 1.7320508f;
+    };
+    float v = gauss((unsigned)i * 4u);
+    if (corr > 0.f) v = gauss((unsigned)k * 4u + 0x9e3779b9u) + corr * v;
+    v *= rsqrtf((float)d);
+    const unsigned u = __float_as_uint(v);
+    p[i] = (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+  }
+}
+
+__global__ void lab_tau(float* t, int n, float v) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) t[i] = v;
+}
+
+#include <functional>
+
+struct Variant {
+  const char* name;
+  std::function<void(const rr::GemmArgs&)> run;
+};
+
+int main(int argc, char** argv) {
+  const int reps = argc > 1 ? atoi(argv[1]) : 3;
+  const int rounds = argc > 2 ? atoi(argv[2]) : 3;
+  const long long N = 1600000 - 32768;
+  const int Q = 1280, D = 2048;
+  uint16_t *gal, *qr, *qc;
+  float* tau;
+  int* cnt;
+  unsigned long long* cand;
+  CK(hipMalloc(&gal, (size_t)N * D * 2));
+  CK(hipMalloc(&qr, (size_t)Q * D * 2));
+  CK(hipMalloc(&qc, (size_t)Q * D * 2));
+  CK(hipMalloc(&tau, Q * 4));
+  CK(hipMalloc(&cnt, Q * 4));
+  const long long CAP = 24576;  // the survivors of the realistic threshold below
+  CK(hipMalloc(&cand, (size_t)Q * CAP * 8));
+  hipLaunchKernelGGL(lab_fill, dim3(8192), dim3(256), 0, 0, gal, N, D, 1u, 0.f);
+  hipLaunchKernelGGL(lab_fill, dim3(1024), dim3(256), 0, 0, qr, (long long)Q, D, 7u, 0.f);
+  hipLaunchKernelGGL(lab_fill, dim3(1024), dim3(256), 0, 0, qc, (long long)Q, D, 7u, 0.05f);
+  uint16_t* qs;  // the C3 bench's descriptors: every query the same vector
+  CK(hipMalloc(&qs, (size_t)Q * D * 2));
+  hipLaunchKernelGGL(lab_fill, dim3(1024), dim3(256), 0, 0, qs, (long long)Q, D, 7u, 1e-6f);
+  // +inf: no survivors (the loop alone); tau_real: ~0.8 % of rows pass, the
+  // C3 bench's 12 383 survivors per query
+  const float tau_real = argc > 3 ? (float)atof(argv[3]) : 0.0535f;
+  hipLaunchKernelGGL(lab_tau, dim3((Q + 255) / 256), dim3(256), 0, 0, tau, Q, __builtin_inff());
+  CK(hipMemset(cnt, 0, Q * 4));
+  CK(hipDeviceSynchronize());
+
+  rr::GemmArgs g;
+  g.A = (const float*)gal;
+  g.lda = D;
+  g.M = (int)N;
+  g.K = D;
+  g.ldb = D;
+  g.N = Q;
+  g.tau = tau;
+  g.cand = cand;
+  g.cnt = cnt;
+  g.cap = CAP;
+  const int tiles_n = (Q + rr::SW_BN - 1) / rr::SW_BN;
+  const long long nblk = ((N + rr::SW_BM - 1) / rr::SW_BM) * tiles_n;
+  const double flop = 2.0 * N * Q * D;
+
+  const unsigned nb = (unsigned)nblk;
+  auto v16 = [&](auto k) { return [=](const rr::GemmArgs& x) { hipLaunchKernelGGL(k, dim3(nb), dim3(512), 0, 0, x, tiles_n); }; };
+  auto v128 = [&](auto k, unsigned grid) {
+    return [=](const rr::GemmArgs& x) { hipLaunchKernelGGL(k, dim3(grid), dim3(512), 0, 0, x, tiles_n, (int)nb); };
+  };
+  std::vector<Variant> vs = {
+      {"64-B rows: full loop", v16(rr::sweep16_kernel<8, 0>)},
+      {"128-B rows: full loop", v128(rr::sweep128_kernel<0, 0>, nb)},
+      {"128-B rows: waves 4-7 at prio 1", v128(rr::sweep128_kernel<1024, 0>, nb)},
+      {"128-B rows: prio 1 around MFMAs", v128(rr::sweep128_kernel<2048, 0>, nb)},
+      {"128-B rows: no DMA (stale)", v128(rr::sweep128_kernel<1, 0>, nb)},
+      {"128-B rows: MFMAs + DMA (racy)", v128(rr::sweep128_kernel<6, 0>, nb)},
+      {"128-B rows: MFMAs only", v128(rr::sweep128_kernel<7, 0>, nb)},
+  };
+  // in-kernel clock (MHz, median over blocks) of the main variants
+  std::vector<Variant> cs = {
+      {"clock: 128-B rows full", v128(rr::sweep128_kernel<64, 0>, nb)},
+      {"clock: 128-B MFMAs only", v128(rr::sweep128_kernel<64 + 7, 0>, nb)},
+  };
+  float* stamps;
+  CK(hipMalloc(&stamps, (size_t)nblk * 4));
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  for (int kind = 0; kind < 3; ++kind) {
+    g.B = (const float*)(kind == 2 ? qs : kind ? qc : qr);
+    printf("queries: %s  (%lld blocks, %d reps x %d rounds)\n", kind == 2 ? "identical (bench)" : kind ? "near-parallel" : "random",
+           nblk, reps, rounds);
+    std::vector<std::vector<float>> ms(vs.size());
+    for (int r = 0; r < rounds; ++r)
+      for (size_t v = 0; v < vs.size(); ++v) {
+        vs[v].run(g);
+        CK(hipEventRecord(a));
+        for (int i = 0; i < reps; ++i) vs[v].run(g);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float t = 0;
+        CK(hipEventElapsedTime(&t, a, b));
+        ms[v].push_back(t / reps);
+      }
+    // the full loops again with the realistic threshold (survivors appended)
+    hipLaunchKernelGGL(lab_tau, dim3((Q + 255) / 256), dim3(256), 0, 0, tau, Q, tau_real);
+    for (int v = 0; v < 4; ++v) {
+      std::vector<float> tt;
+      for (int r = 0; r < rounds; ++r) {
+        CK(hipMemset(cnt, 0, Q * 4));
+        vs[v].run(g);
+        CK(hipMemset(cnt, 0, Q * 4));
+        CK(hipEventRecord(a));
+        vs[v].run(g);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float t = 0;
+        CK(hipEventElapsedTime(&t, a, b));
+        tt.push_back(t);
+      }
+      std::vector<int> hc(Q);
+      CK(hipMemcpy(hc.data(), cnt, Q * 4, hipMemcpyDeviceToHost));
+      long long tot = 0;
+      for (int x : hc) tot += x;
+      std::sort(tt.begin(), tt.end());
+      printf("  %-34s %8.3f ms  (tau %.4f: %lld survivors per query)\n", (std::string(vs[v].name) + " + survivors").c_str(),
+             tt[tt.size() / 2], tau_real, tot / Q);
+    }
+    hipLaunchKernelGGL(lab_tau, dim3((Q + 255) / 256), dim3(256), 0, 0, tau, Q, __builtin_inff());
+    for (size_t v = 0; v < vs.size(); ++v) {
+      std::sort(ms[v].begin(), ms[v].end());
+      const float med = ms[v][ms[v].size() / 2];
+      printf("  %-34s %8.3f ms  %7.1f TF/s  %.3f of 2500\n", vs[v].name, med, flop / med / 1e9, flop / med / 1e9 / 2500);
+    }
+    fflush(stdout);
+    rr::GemmArgs gc = g;
+    gc.C = stamps;
+    for (size_t v = 0; v < cs.size(); ++v) {
+      for (int i = 0; i < 4; ++i) cs[v].run(gc);
+      CK(hipDeviceSynchronize());
+      const long long nst = std::string(cs[v].name).find("persistent") != std::string::npos ? 256 : nblk;
+      std::vector<float> h(nst);
+      CK(hipMemcpy(h.data(), stamps, nst * 4, hipMemcpyDeviceToHost));
+      std::sort(h.begin(), h.end());
+      printf("  %-34s median %6.0f MHz (p10 %6.0f, p90 %6.0f)\n", cs[v].name, h[nst / 2], h[nst / 10], h[nst * 9 / 10]);
+    }
+    fflush(stdout);
+  }
+  return 0;
+}
