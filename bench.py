@@ -509,6 +509,9 @@ def main():
     ap.add_argument("--pipeline", type=int, choices=(0, 1), default=0,
                     help="1: rank batch i on a second HIP stream while batch i+1 is embedded (n embeds + n rankings "
                          "per n steps either way)")
+    ap.add_argument("--embed-streams", type=int, default=1,
+                    help="C3: the trunk's batch cut into this many parts, each on its own HIP stream, part i+1 one "
+                         "conv behind part i (networks forward_test_u8_streams; bit-identical to serial parts)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--c2-dataset", choices=("both", "roxford5k", "rparis6k"), default="both",
                     help="C2 sets per step (BASELINE C2: full ROxford5k + RParis6k)")
@@ -591,7 +594,16 @@ def main():
 
     scales = (1.0, 1.0 / np.sqrt(2.0), 0.5)  # C5 multi-scale set
 
+    # the schedule of the timed steps (--embed-streams / --pipeline); C3 also
+    # reports the overlapped one (2 embed streams + the ranker on a third)
+    # beside it, timed after the main loop (its kernels co-run, so per-launch
+    # durations there are not single-kernel durations)
+    sched = {"streams": a.embed_streams if a.workload == "c3" else 1, "pipeline": bool(a.pipeline)}
+    e_streams = [torch.cuda.Stream(dev) for _ in range(max(2, a.embed_streams))] if a.workload == "c3" else None
+
     def embed():
+        if sched["streams"] > 1:
+            return net.forward_test_u8_streams(imgs, e_streams[:sched["streams"]], lag=1)
         if a.workload != "c5":
             return net.forward_test_u8(imgs)
         # multi-scale extraction (utils/helpfunc.py:30-46): rescale, embed, average, renormalise
@@ -632,7 +644,7 @@ def main():
                                              max_workspace_bytes=ws_max)
         return ops.cosine_topk(desc, gallery, a.k, idx_offset=lo, workspace=ws, max_workspace_bytes=ws_max)
 
-    s_rank = torch.cuda.Stream(dev) if a.pipeline else None
+    s_rank = torch.cuda.Stream(dev)
 
     def run_steps(n):
         """n steps.  --pipeline: batch i's ranking runs on its own HIP stream
@@ -640,7 +652,7 @@ def main():
         on the current stream -- the ranker's MFMA / L2-bound sweep beside the
         trunk's HBM-bound layers; still exactly n embeds and n rankings, the
         last ranking joined before returning."""
-        if s_rank is None:
+        if not sched["pipeline"]:
             out = None
             for _ in range(n):
                 out = step()
@@ -732,6 +744,24 @@ def main():
                                         "frac": round(ach / PEAK_TFLOPS["fp32"], 4),
                                         "ms_per_step": round(f_ms / a.steps, 3)},
                       "bit_identical_to_prefilter": True}
+
+    overlapped = None
+    if a.workload == "c3" and not DIST_ON and (sched["streams"], sched["pipeline"]) != (2, True):
+        main_sched = dict(sched)
+        sched.update(streams=2, pipeline=True)
+        run_steps(1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run_steps(a.steps)
+        torch.cuda.synchronize()
+        el_o = time.perf_counter() - t0
+        sched.update(main_sched)
+        overlapped = {"embed_streams": 2, "pipeline": True, "value": round(a.batch * a.steps / el_o, 2),
+                      "ms_per_step": round(el_o / a.steps * 1e3, 3),
+                      "detail": "the same steps with the trunk's batch in two parts on two HIP streams (part 2 one "
+                                "conv behind) and the ranking of batch i on a third stream beside the embed of "
+                                "batch i+1; descriptors bit-identical to the one-stream schedule "
+                                "(tests/test_gpu_overlap.py)"}
 
     decorrelated = None
     if gal_bf is not None:
@@ -900,6 +930,7 @@ def main():
                       "parallelism": f"query-dp{world} + gallery-shard{world}",
                       "conv_math": a.conv_math if a.workload != "c4" else None,
                       "pipeline": bool(a.pipeline),
+                      "embed_streams": sched["streams"],
                       **({"tuning": a.tune} if a.tune else {}),
                       "ranker_workspace_bytes_per_rank": int(ws.numel()),
                       "ranker_workspace_worst_case_bytes": int(ws_full)},
@@ -912,6 +943,8 @@ def main():
                          "select_and_rescore_ms_per_step": rk.get("select", {}).get("ms_per_step"),
                          **(prefilter_stats or {}),
                          **({"decorrelated_queries": decorrelated} if decorrelated else {})}
+    if overlapped is not None:
+        res["overlapped_schedule"] = overlapped
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "c3":
         t = time.time()
         res["cpu_baseline"] = cpu_baseline(a.arch, a.gallery, a.dim, a.k)

@@ -74,7 +74,7 @@ class ResNet:
         w, b = self.convs[name]
         return ops.conv2d(x, w, b, stride, pad, residual, relu)
 
-    def _forward_h2(self, x, return_x3):
+    def _forward_h2(self, x, return_x3, hook=None):
         """The trunk on the f16x2 core: every conv reads its input's max-|x|
         record and writes its output's (one zeroed [2 + 3 blocks, 64] tensor per
         forward); the max-pool output reuses the stem's record (every stem
@@ -82,8 +82,11 @@ class ResNet:
         its ReLU and the max-pool run as one launch (ops.stem_pool_h2), so the
         stem's full-resolution map never reaches HBM.  A stage's
         first block runs conv3 and its downsample projection as one GEMM
-        (ops.bottleneck_out_h2), so the projected identity never reaches HBM."""
+        (ops.bottleneck_out_h2), so the projected identity never reaches HBM.
+        hook(i), if given, is called after the i-th conv launch (i = 0: the
+        stem) -- the point where a caller can record a stream event."""
         cv, h2 = self.convs, self.convs_h2
+        hook = hook or (lambda i: None)
         rec = ops.amax_records(2 + 3 * sum(self.layers), x.device)
         ops.amax_f32(x, rec[0])
         if self.fuse_stem_pool and h2["conv1"].cout == 64:
@@ -91,7 +94,8 @@ class ResNet:
         else:
             x = ops.conv2d_h2(x, rec[0], h2["conv1"], cv["conv1"][1], 2, 3, None, True, rec[1])
             x = ops.maxpool2d(x, 3, 2, 1)
-        xa, r, x3 = rec[1], 2, None
+        hook(0)
+        xa, r, x3, ci = rec[1], 2, None, 1
         for li, nb in enumerate(self.layers):
             for bi in range(nb):
                 p = f"layer{li + 1}.{bi}"
@@ -100,25 +104,29 @@ class ResNet:
                 fused = bi == 0 and self.fuse_downsample and p in self.bneck_h2
                 idn = ops.conv2d_h2(x, xa, h2[d], cv[d][1], s1 * s2, 0, None, False) if bi == 0 and not fused else x
                 y = ops.conv2d_h2(x, xa, h2[f"{p}.conv1"], cv[f"{p}.conv1"][1], s1, 0, None, True, rec[r])
+                hook(ci)
                 y = ops.conv2d_h2(y, rec[r], h2[f"{p}.conv2"], cv[f"{p}.conv2"][1], s2, 1, None, True, rec[r + 1])
+                hook(ci + 1)
                 if fused:
                     x = ops.bottleneck_out_h2(y, rec[r + 1], x, xa, self.bneck_h2[p], s1 * s2, rec[r + 2])
                 else:
                     x = ops.conv2d_h2(y, rec[r + 1], h2[f"{p}.conv3"], cv[f"{p}.conv3"][1], 1, 0, idn, True,
                                       rec[r + 2])
+                hook(ci + 2)
+                ci += 3
                 xa, r = rec[r + 2], r + 3
             if li == 2:
                 x3 = x
         return (x3, x) if return_x3 else x
 
-    def forward(self, x, return_x3=False):
+    def forward(self, x, return_x3=False, hook=None):
         """x: NHWC fp32 with 3 channels or 4 (zero 4th channel, preferred).
         return_x3: also return layer3's output, as ResNet_DOLG.forward's
         (x3, x4) (networks/backbone.py:236-242)."""
         if x.shape[-1] == 3:
             x = torch.nn.functional.pad(x, (0, 1))
         if self.conv_math == "h2":
-            return self._forward_h2(x.contiguous(), return_x3)
+            return self._forward_h2(x.contiguous(), return_x3, hook)
         x = self._conv(x, "conv1", 2, 3, True)
         x = ops.maxpool2d(x, 3, 2, 1)
         x3 = None
@@ -181,6 +189,54 @@ class _Extractor:
         into the first kernel (dataset/configdataset.py:417)."""
         return self.forward_test_nhwc(ops.preprocess_u8(img_nhwc_u8, out_c=self.in_channels))
 
+    @torch.no_grad()
+    def forward_test_u8_streams(self, img_nhwc_u8, streams, lag=1):
+        """forward_test_u8 with the batch cut into len(streams) contiguous parts,
+        part i on HIP stream streams[i], part i + 1 held back until part i has
+        launched its lag-th conv (ResNet._forward_h2's hook; lag 0 = after the
+        stem).  The parts' kernels then run side by side, offset by about one
+        layer, so an MFMA-bound conv of one part shares the chip with an
+        HBM-bound conv of the other instead of every layer holding the chip by
+        itself.  (Giving each stream's persistent kernels half the CUs, so
+        that two kernels always co-run, measured slower: 68.5 vs 66.5 ms per
+        1280-image embed, DESIGN.md.)  Each part is exactly
+        forward_test_u8 of its images (its own
+        max-|x| records for the f16x2 split scales): descriptors are
+        bit-identical to running the parts one after another
+        (tests/test_gpu_overlap.py) and within the split core's bar of the
+        whole batch in one part.  Returns [B, outputdim] on the current stream."""
+        x = img_nhwc_u8
+        dev = x.device
+        cur = torch.cuda.current_stream(dev)
+        n = len(streams)
+        b = x.shape[0]
+        cuts = [b * i // n for i in range(n + 1)]
+        outs, gate = [], None
+        for i, s in enumerate(streams):
+            if cuts[i] == cuts[i + 1]:
+                continue
+            s.wait_stream(cur)
+            if gate is not None:
+                s.wait_event(gate)
+            ev = torch.cuda.Event()
+
+            def hook(ci, ev=ev, s=s):
+                if ci == lag:
+                    ev.record(s)
+
+            with torch.cuda.stream(s):
+                f = self.forward_test_nhwc(ops.preprocess_u8(x[cuts[i]:cuts[i + 1]], out_c=self.in_channels),
+                                           hook=hook)
+            outs.append(f)
+            gate = ev
+        if not outs:
+            return self.forward_test_u8(x)
+        for s in streams:
+            cur.wait_stream(s)
+        for f in outs:
+            f.record_stream(cur)
+        return torch.cat(outs)
+
 
 class GeM(_Extractor):
     """GeM network (networks/RetrievalNet.py:327-344): backbone -> gem(p=3) ->
@@ -208,8 +264,8 @@ class GeM(_Extractor):
         self.whiten_b = wb.float().contiguous().to(self.device)
         self.outputdim = outputdim
 
-    def forward_test_nhwc(self, x_nhwc):
-        f = self.backbone(x_nhwc)
+    def forward_test_nhwc(self, x_nhwc, hook=None):
+        f = self.backbone(x_nhwc, hook=hook)
         f = self.pooling(f)
         f = ops.linear(f, self.whiten_w, self.whiten_b)
         return ops.l2_normalize(f, EPS_L2, out=f)
@@ -284,8 +340,8 @@ class GeMPCAw(_Extractor):
         self.pcaw = pcaw
         self.outputdim = pcaw.dim
 
-    def forward_test_nhwc(self, x_nhwc):
-        f = self.net.forward_test_nhwc(x_nhwc)
+    def forward_test_nhwc(self, x_nhwc, hook=None):
+        f = self.net.forward_test_nhwc(x_nhwc, hook=hook)
         f = self.pcaw(f)
         return ops.l2_normalize(f, EPS_L2, out=f)
 
