@@ -1110,7 +1110,10 @@ __global__ __launch_bounds__(512, 1) void gemm_s3p_kernel(GemmArgs g, int tiles_
     load_bias();
     stage(0);
     load_res(1);
-    if constexpr ((EPI & EP_RES) != 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // every load issued so far has landed, the next tile's A(j+1) included:
+    // the next iteration's skipped A wait (wait_a) relies on this explicit
+    // wait, not on the one hipcc places for the plain bias / scale loads
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     launder_bias();
     store(0);
     stage(1);
@@ -1250,10 +1253,11 @@ static hipError_t launch_s3p_t(GemmArgs g, hipStream_t s, int n_cu, int stagger)
 // at K = 64, where one accumulator's error passes the exact-fp32 core's).
 // Every column of the 256x128 form is config 12's column bit for bit, the
 // 256x64 form's output config 7's.
-// Counted waits: vector-memory operations retire in issue order (stores
-// included), so each wait names how many younger operations may remain; where
-// fewer were issued (rows past M store nothing) the wait is longer, never
-// shorter.
+// Counted waits rely only on loads returning in issue order among
+// themselves: each names how many younger loads may remain, and stores are
+// never counted (a wait issued after stores also covers them, which makes it
+// longer, never shorter); where fewer loads were issued (rows past M) the
+// wait is longer, never shorter.
 template <int EPI, int FN = 2, int WM = 2, int ACC2 = 0>
 __global__ __launch_bounds__(512, 1) void gemm_s3q_kernel(GemmArgs g, int tiles_n, int ntiles) {
   static_assert((EPI & EP_SCALE) != 0, "f16x2: scaled epilogue");
@@ -1709,7 +1713,10 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     m0 = (wgid / tiles_n) * BM;
     n0 = (wgid % tiles_n) * BN;
   }
-  const int W = g.W, H = g.H, KW = g.KW, ntap = g.KH * g.KW;
+  // 3x3 only (h2_halo_rows): the tap -> (kh, kw) split and the group count
+  // are compile-time constants
+  const int W = g.W, H = g.H;
+  constexpr int KW = 3, KH = 3, ntap = KH * KW;
   const int nch = g.Cin / BK, ngrp = ntap / TPK, nk = nch * ngrp;  // k-step kt = (slice, group of TPK taps)
   const int hoff = g.pad * W + g.pad;  // halo row 0 = input raster index m0 - hoff
 
@@ -1820,7 +1827,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
         const int m = mb + wm * WTM + i * 32 + (MF ? 16 * a + l16 : lr);
         const int rem = m % (H * W), oh = rem / W, ow = rem - oh * W;
         int mk = 0;
-        for (int kh = 0; kh < g.KH; ++kh)
+        for (int kh = 0; kh < KH; ++kh)
           for (int kw = 0; kw < KW; ++kw)
             if ((unsigned)(oh + kh - g.pad) < (unsigned)H && (unsigned)(ow + kw - g.pad) < (unsigned)W)
               mk |= 1 << (kh * KW + kw);
@@ -1987,13 +1994,18 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     // released, in 128-row slabs ----
     const int my_tiles = (ntiles - bid + nwg - 1) / nwg;
     const int Q = my_tiles * nk;
+    // the group whose top splits the next slice into the other buffer: the
+    // slice's third (its passes, loaded in the first group, then have two
+    // groups' MFMAs to arrive from HBM; the first group's end waits only for
+    // the B DMA issued before them), or the second with fewer groups
+    const int st_g = ngrp >= 3 ? 2 : 1;
     int tl = 0, c = 0, tg = 0, kt = 0, sg = 0;
     int m_next = my_tiles > 1 ? tile_m0(1) : m0;
     for (int q = 0; q < Q; ++q) {
       const bool last_slice = c + 1 == nch;
       const bool more = !last_slice || tl + 1 < my_tiles;
       if (q + 1 < Q) glds_b(kt + 1 == nk ? 0 : kt + 1, (q + 1) & 1);
-      if (more && tg == 1) {
+      if (more && tg == st_g) {
         const int nb = (sg + 1) & 1;
 #pragma unroll
         for (int p = 0; p < A_PASS; ++p) store_pass(nb, p);
@@ -2008,7 +2020,10 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
       }
 #pragma unroll
       for (int u = 0; u < TPK; ++u) compute(sg & 1, q & 1, tg * TPK + u, u);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next B (and the next slice's passes)
+      if (more && tg == 0 && st_g == 2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * A_PASS) : "memory");  // the next B (older than the passes)
+      else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next B (and the next slice's passes)
       launder_pass();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();

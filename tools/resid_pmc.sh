@@ -22,7 +22,7 @@ for shape in "1280 14 14 256 1024 1 1 0 1" "1280 14 14 1024 256 1 1 0 0" "1280 1
   i=1
   for P in "$P1" "$P2" "$P3" "$P4"; do
     mkdir -p $OUT/$tag
-    [ -n "$P" ] && timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $OUT/$tag/p$i -o run -- python3 $R/tools/s3_one.py $shape 5 > $OUT/$tag/p$i.log 2>&1 || echo "pass $tag p$i rc=$?" >> $OUT/passes.txt
+    [ -n "$P" ] && timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $OUT/$tag/p$i -o run -- python3 $R/tools/h2_one.py conv $shape 5 > $OUT/$tag/p$i.log 2>&1 || echo "pass $tag p$i rc=$?" >> $OUT/passes.txt
     i=$((i+1))
   done
 done
