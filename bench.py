@@ -513,6 +513,9 @@ def main():
                     help="C3: the trunk's batch cut into this many parts, each on its own HIP stream, part i+1 one "
                          "conv behind part i (networks forward_test_u8_streams; bit-identical to serial parts)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the side measurements after the timed loop (the decorrelated-query sweep and the "
+                         "overlapped schedule): tools/profile.sh, so that the profile holds the timed loop's launches")
     ap.add_argument("--c2-dataset", choices=("both", "roxford5k", "rparis6k"), default="both",
                     help="C2 sets per step (BASELINE C2: full ROxford5k + RParis6k)")
     ap.add_argument("--c2-gallery", type=int, default=0, help="override every C2 set's gallery size (0: revisitop's)")
@@ -746,7 +749,7 @@ def main():
                       "bit_identical_to_prefilter": True}
 
     overlapped = None
-    if a.workload == "c3" and not DIST_ON and (sched["streams"], sched["pipeline"]) != (2, True):
+    if a.workload == "c3" and not DIST_ON and not a.no_extras and (sched["streams"], sched["pipeline"]) != (2, True):
         main_sched = dict(sched)
         sched.update(streams=2, pipeline=True)
         run_steps(1)
@@ -764,7 +767,7 @@ def main():
                                 "(tests/test_gpu_overlap.py)"}
 
     decorrelated = None
-    if gal_bf is not None:
+    if gal_bf is not None and not a.no_extras:
         # The seeded random-weight trunk maps every image to nearly the same
         # descriptor (pairwise cosine ~1.0), so the timed queries are one
         # direction repeated.  The same ranker on q_total independent Gaussian

@@ -14,7 +14,7 @@ import sys
 from collections import defaultdict
 
 def short(name):
-    m = re.search(r"(rr::\w+(<[^>]*>)?)", name)
+    m = re.search(r"(rr::(?:\(anonymous namespace\)::)?\w+(<[^>]*>)?)", name)
     return m.group(1) if m else name[:60]
 
 
@@ -23,9 +23,13 @@ def cls_of(name):
     AMODE, EMODE, ...> by its epilogue (EMODE 2 = cosine filter sweep, 1 =
     seed scores, 0 = stored C: convs / linears); gemm_s3_kernel and the
     persistent gemm_s3p_kernel / gemm_s3q_kernel, the halo-staged gemm_h2_halo_kernel /
-    stem_pool_halo_kernel and the block seam seam_h2_kernel = convs."""
+    stem_pool_halo_kernel = convs; sweep128 / sweep16 = cosine filter."""
     if ("gemm_s3_kernel" in name or "gemm_s3p_kernel" in name or "gemm_s3q_kernel" in name
             or "gemm_h2_halo_kernel" in name or "stem_pool_halo_kernel" in name or "seam_h2_kernel" in name):
+        return "conv_gemm"
+    if "sweep128_kernel" in name or "sweep16_kernel" in name:  # the hand-scheduled bf16 filter sweeps
+        return "cosine_filter"
+    if "gemm_lpp" in name:  # the persistent bf16 stored-C tiles (ViT linears)
         return "conv_gemm"
     m = re.search(r"gemm_8p_kernel<(\d)>", name)
     if m:  # the 8-phase bf16 sweep (filter / seed scores only)
