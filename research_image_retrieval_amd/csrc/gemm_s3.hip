@@ -2453,21 +2453,34 @@ int launch_gemm_h2_seg2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int ti
 // 0..55 (the four dropped k-steps add exact zeros).  The next tile's patch is
 // loaded into registers under the k-loop; the pool epilogue stages the raw
 // accumulators through LDS exactly as the config-7 stem does.
+// Round 6 (PMC on this launch alone, profiles/r06y_halo_stem_pmc.txt: MFMA
+// busy 0.36, 3.3 LDS bank-conflict cycles per MFMA, four barriers per tile):
+//  - the C staging has its own LDS region (B 58 KB + patch 22 KB + C 68 KB),
+//    so tile i's pool epilogue (its LDS reads, the max / scale / bias / ReLU
+//    and the stores) runs inside tile i + 1's k-loop, between its k-steps,
+//    instead of after it with the matrix cores idle; two barriers per tile;
+//  - patch row hr keeps its even columns in slots 0..17 and its odd ones in
+//    18..34 (row stride 36 slots): a lane row reads every other pixel of a
+//    patch row, so consecutive lanes now read consecutive 8-B slots, where
+//    the raster layout put them 16 B apart (two lanes per bank pair).
+// Same products, order and epilogue arithmetic: bit-identical output.
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void stem_pool_halo_kernel(GemmArgs g, int ntiles) {
   constexpr int NT = 512, NW = 8, BN = 64, HR = 39, HC = 35, HP = HR * HC;  // 1365 patch pixels
+  constexpr int HS = 36, HPS = HR * HS;       // patch slots per row / in all (even | odd columns), zero slot HPS
   constexpr int KP = 224, BS = KP + 8;        // weight row (k) length; LDS row stride (u16, padded)
   constexpr int NKS = 13;                     // k-steps of 4 taps (taps 0..51)
   constexpr int B_U16 = 2 * BN * BS;          // both weight planes
-  constexpr int A_U16 = 2 * (HP + 1) * 4;     // both patch planes + the zero pixel
+  constexpr int A_U16 = 2 * (HPS + 1) * 4;    // both patch planes + the zero slot
   constexpr int CS = BN + 4;                  // C staging row stride (floats)
   constexpr int C_U16 = 256 * CS * 2;
-  constexpr int AC_U16 = A_U16 > C_U16 ? A_U16 : C_U16;
   constexpr int A_PASS = (HP + NT - 1) / NT;  // 3
-  __shared__ __attribute__((aligned(16))) uint16_t lds[B_U16 + AC_U16];
+  constexpr int C4 = BN / 4, NPOOL = 56 * C4;  // pool work items per tile (896: one or two per thread)
+  static_assert(NPOOL > NT && NPOOL <= 2 * NT, "one or two pool items per thread");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[B_U16 + A_U16 + C_U16];
   uint16_t* lb = lds;
   uint16_t* la = lds + B_U16;
-  float* ct = reinterpret_cast<float*>(lds + B_U16);
+  float* ct = reinterpret_cast<float*>(lds + B_U16 + A_U16);
   typedef f16x8 frag_t;
   typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
@@ -2519,26 +2532,60 @@ __global__ __launch_bounds__(512, 1) void stem_pool_halo_kernel(GemmArgs g, int 
 #pragma unroll
     for (int q = 0; q < A_PASS; ++q) {
       asm volatile("" : "+v"(px[q]));
-      const int p = tid + q * NT;
+      const int p = tid + q * NT, hr = p / HC, hc = p - hr * HC;
+      const int slot = hr * HS + (hc & 1) * (HS / 2) + (hc >> 1);
       const f32x4 v = px[q] * a_sc;
       const f16x4 hi = __builtin_convertvector(v, f16x4);
       const f16x4 lo = __builtin_convertvector(v - __builtin_convertvector(hi, f32x4), f16x4);
       if (p < HP) {
-        *reinterpret_cast<f16x4*>(la + p * 4) = hi;
-        *reinterpret_cast<f16x4*>(la + (HP + 1) * 4 + p * 4) = lo;
+        *reinterpret_cast<f16x4*>(la + slot * 4) = hi;
+        *reinterpret_cast<f16x4*>(la + (HPS + 1) * 4 + slot * 4) = lo;
       }
     }
-    if (tid < 2) *reinterpret_cast<uint2*>(la + tid * (HP + 1) * 4 + HP * 4) = uint2{0u, 0u};  // the zero pixel
+    if (tid < 2) *reinterpret_cast<uint2*>(la + tid * (HPS + 1) * 4 + HPS * 4) = uint2{0u, 0u};  // the zero slot
   };
 
   // lane rows: wave w owns tile rows 32 w .. +31; row r -> conv output (q, c) =
-  // (r / 15, r % 15) of the patch, input pixel of tap (kh, kw) = (2q + kh) 35 + 2c + kw
+  // (r / 15, r % 15) of the patch, input pixel of tap (kh, kw) = (2q + kh, 2c + kw),
+  // slot (2q + kh) 36 + (kw & 1) 18 + c + (kw >> 1)
   const int row = wave * 32 + lr, rq = row / 15, rc = row - rq * 15;
-  const int pbase = row < 255 ? (2 * rq) * HC + 2 * rc : -1;
+  const int sbase = row < 255 ? (2 * rq) * HS + rc : -1;
 
+  // ---- pool work item `it` of tile tl (C staged in ct): the pooled output
+  // (8 pr + it / 16 / 7, 7 pc + it / 16 % 7), channels 4 (it % 16) .. +3: max
+  // over the window's in-map conv outputs of the raw accumulators, then
+  // scale, bias, ReLU (all monotone) ----
   float am = 0.f;
+  auto pool_item = [&](int tl, int it) __attribute__((always_inline)) {
+    const int b = tl / tpi, t2 = tl - b * tpi, pr = t2 / g.pool_tc, pc = t2 - pr * g.pool_tc;
+    const int qd = it / C4, c4 = it - qd * C4, pi = qd / 7, pj = qd - 7 * pi;
+    const int ph = 8 * pr + pi, pw = 7 * pc + pj;
+    if (ph >= g.POH || pw >= g.POW) return;
+    f32x4 mx = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
+#pragma unroll
+    for (int dr = -1; dr <= 1; ++dr)
+#pragma unroll
+      for (int dc = -1; dc <= 1; ++dc) {
+        const int oh = 2 * ph + dr, ow = 2 * pw + dc;
+        if ((unsigned)oh >= (unsigned)g.OH || (unsigned)ow >= (unsigned)g.OW) continue;
+        const f32x4 v = *reinterpret_cast<const f32x4*>(ct + ((2 * pi + dr + 1) * 15 + 2 * pj + dc + 1) * CS + c4 * 4);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) mx[e] = __builtin_fmaxf(mx[e], v[e]);
+      }
+    const f32x4 sc = *reinterpret_cast<const f32x4*>(g.col_scale + c4 * 4) * a_isc;
+    const f32x4 bv = g.bias != nullptr ? *reinterpret_cast<const f32x4*>(g.bias + c4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = __builtin_fmaxf(mx[e] * sc[e] + bv[e], 0.f);
+      am = amax_acc(am, o[e]);
+    }
+    *reinterpret_cast<f32x4*>(g.pool_out + (((long long)b * g.POH + ph) * g.POW + pw) * BN + c4 * 4) = o;
+  };
+
   const int G = gridDim.x;
   int tl = blockIdx.x;
+  int prev = -1;  // the tile whose C is staged in ct (its pool still to run)
   load_patch(tl);
   store_patch();
   __syncthreads();
@@ -2557,11 +2604,11 @@ __global__ __launch_bounds__(512, 1) void stem_pool_halo_kernel(GemmArgs g, int 
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const int t = t0 + u, kh = t / 7, kw = t - kh * 7;
-        pix[u] = (pbase >= 0 && t < 49) ? pbase + kh * HC + kw : HP;
+        pix[u] = (sbase >= 0 && t < 49) ? sbase + kh * HS + (kw & 1) * (HS / 2) + (kw >> 1) : HPS;
       }
 #pragma unroll
       for (int p = 0; p < 2; ++p) {
-        const uint16_t* pl = la + p * (HP + 1) * 4;
+        const uint16_t* pl = la + p * (HPS + 1) * 4;
         const f16x4 x0 = *reinterpret_cast<const f16x4*>(pl + pix[0] * 4);
         const f16x4 x1 = *reinterpret_cast<const f16x4*>(pl + pix[1] * 4);
         a[p] = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
@@ -2576,48 +2623,25 @@ __global__ __launch_bounds__(512, 1) void stem_pool_halo_kernel(GemmArgs g, int 
         lo[j] = s3_mf32<2>(a[0], b[1][j], lo[j]);
         lo[j] = s3_mf32<2>(a[1], b[0][j], lo[j]);
       }
+      // the previous tile's pool epilogue, one work item at a time, among the MFMAs
+      if (prev >= 0) {
+        if (ks == 3) pool_item(prev, tid);
+        if (ks == 8 && tid + NT < NPOOL) pool_item(prev, tid + NT);
+      }
     }
-    __syncthreads();  // every wave done with the patch: its LDS becomes the C staging
+    __syncthreads();  // every wave done with the patch and with ct's previous tile
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
         ct[(wave * 32 + acc_row<false>(0, r, lane)) * CS + acc_col<false>(j, r, lane)] = hi[j][r] + lo[j][r];
-    __syncthreads();
-    // the pooled outputs of the tile: max over the window's in-map conv
-    // outputs of the raw accumulators, then scale, bias, ReLU (all monotone)
-    {
-      const int b = tl / tpi, t2 = tl - b * tpi, pr = t2 / g.pool_tc, pc = t2 - pr * g.pool_tc;
-      constexpr int C4 = BN / 4;
-      for (int it = tid; it < 56 * C4; it += NT) {
-        const int qd = it / C4, c4 = it - qd * C4, pi = qd / 7, pj = qd - 7 * pi;
-        const int ph = 8 * pr + pi, pw = 7 * pc + pj;
-        if (ph >= g.POH || pw >= g.POW) continue;
-        f32x4 mx = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};
-#pragma unroll
-        for (int dr = -1; dr <= 1; ++dr)
-#pragma unroll
-          for (int dc = -1; dc <= 1; ++dc) {
-            const int oh = 2 * ph + dr, ow = 2 * pw + dc;
-            if ((unsigned)oh >= (unsigned)g.OH || (unsigned)ow >= (unsigned)g.OW) continue;
-            const f32x4 v = *reinterpret_cast<const f32x4*>(ct + ((2 * pi + dr + 1) * 15 + 2 * pj + dc + 1) * CS + c4 * 4);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) mx[e] = __builtin_fmaxf(mx[e], v[e]);
-          }
-        const f32x4 sc = *reinterpret_cast<const f32x4*>(g.col_scale + c4 * 4) * a_isc;
-        const f32x4 bv = g.bias != nullptr ? *reinterpret_cast<const f32x4*>(g.bias + c4 * 4) : f32x4{0.f, 0.f, 0.f, 0.f};
-        f32x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[e] = __builtin_fmaxf(mx[e] * sc[e] + bv[e], 0.f);
-          am = amax_acc(am, o[e]);
-        }
-        *reinterpret_cast<f32x4*>(g.pool_out + (((long long)b * g.POH + ph) * g.POW + pw) * BN + c4 * 4) = o;
-      }
-    }
-    __syncthreads();  // the staging read: the next patch may overwrite it
     store_patch();
+    prev = tl;
     __syncthreads();
+  }
+  if (prev >= 0) {  // the last tile's pool
+    pool_item(prev, tid);
+    if (tid + NT < NPOOL) pool_item(prev, tid + NT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr ((EPI & EP_AMAX) != 0) {

@@ -428,12 +428,13 @@ def test_resnet_h2_fused_downsample_matches_unfused(cuda):
     assert d < 2e-6
 
 
-@pytest.mark.parametrize("b,h,w", [(2, 224, 224), (3, 37, 53), (1, 9, 7), (2, 64, 72)])
+@pytest.mark.parametrize("b,h,w", [(2, 224, 224), (3, 37, 53), (1, 9, 7), (2, 64, 72), (96, 64, 72)])
 def test_stem_pool_h2_bit_identical(cuda, b, h, w):
     """The stem with its max-pool fused (rr_stem_pool_h2) writes the same bits
     as the f16x2 stem conv + ReLU followed by the max-pool, on map sizes whose
     pooled grid leaves ragged 8 x 7 tiles; its max-|x| record equals the conv
-    output's (networks/backbone.py:103-109)."""
+    output's (networks/backbone.py:103-109).  96 x 64 x 72: 576 tiles, two or
+    three per persistent block (tile i's pool runs inside tile i + 1's k-loop)."""
     g = torch.Generator().manual_seed(b * h + w)
     x4 = F.pad(torch.randn(b, h, w, 3, generator=g) * 1.5, (0, 1)).contiguous().to(cuda)
     wt = F.pad(torch.randn(64, 7, 7, 3, generator=g) * (2.0 / 147) ** 0.5, (0, 1)).contiguous().to(cuda)
