@@ -506,12 +506,13 @@ def main():
     ap.add_argument("--ws-budget-gb", type=float, default=4.0,
                     help="ranker workspace budget per rank (bounded candidate buffers, overflowed queries re-run; "
                          "0 = the worst-case size, ~Q*N*8 bytes)")
-    ap.add_argument("--pipeline", type=int, choices=(0, 1), default=0,
+    ap.add_argument("--pipeline", type=int, choices=(0, 1), default=None,
                     help="1: rank batch i on a second HIP stream while batch i+1 is embedded (n embeds + n rankings "
-                         "per n steps either way)")
-    ap.add_argument("--embed-streams", type=int, default=1,
+                         "per n steps either way); default 1 for C3 on one GPU, else 0")
+    ap.add_argument("--embed-streams", type=int, default=None,
                     help="C3: the trunk's batch cut into this many parts, each on its own HIP stream, part i+1 one "
-                         "conv behind part i (networks forward_test_u8_streams; bit-identical to serial parts)")
+                         "conv behind part i (networks forward_test_u8_streams; bit-identical to serial parts); "
+                         "default 2 for C3, else 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the side measurements after the timed loop (the decorrelated-query sweep and the "
@@ -597,12 +598,17 @@ def main():
 
     scales = (1.0, 1.0 / np.sqrt(2.0), 0.5)  # C5 multi-scale set
 
-    # the schedule of the timed steps (--embed-streams / --pipeline); C3 also
-    # reports the overlapped one (2 embed streams + the ranker on a third)
-    # beside it, timed after the main loop (its kernels co-run, so per-launch
-    # durations there are not single-kernel durations)
-    sched = {"streams": a.embed_streams if a.workload == "c3" else 1, "pipeline": bool(a.pipeline)}
-    e_streams = [torch.cuda.Stream(dev) for _ in range(max(2, a.embed_streams))] if a.workload == "c3" else None
+    # the schedule of the timed steps (--embed-streams / --pipeline).  C3's
+    # default overlaps: the trunk's batch in two parts on two HIP streams and,
+    # on one GPU, batch i's ranking on a third beside batch i+1's embed.  Its
+    # kernels co-run, so their per-launch durations are not single-kernel
+    # durations: the line also times the one-stream schedule after the main
+    # loop and reports its per-kernel rooflines (`one_stream_schedule`).
+    c3 = a.workload == "c3"
+    n_es = a.embed_streams if a.embed_streams is not None else (2 if c3 else 1)
+    pipe = bool(a.pipeline) if a.pipeline is not None else (c3 and not DIST_ON)
+    sched = {"streams": n_es if c3 else 1, "pipeline": pipe}
+    e_streams = [torch.cuda.Stream(dev) for _ in range(max(2, n_es))] if c3 else None
 
     def embed():
         if sched["streams"] > 1:
@@ -748,23 +754,35 @@ def main():
                                         "ms_per_step": round(f_ms / a.steps, 3)},
                       "bit_identical_to_prefilter": True}
 
-    overlapped = None
-    if a.workload == "c3" and not DIST_ON and not a.no_extras and (sched["streams"], sched["pipeline"]) != (2, True):
+    alt_sched, alt_cls = None, None
+    if c3 and not DIST_ON and not a.no_extras:
+        # the other schedule: one stream if the timed loop overlapped, else the
+        # overlapped one; same steps, after one untimed step
         main_sched = dict(sched)
-        sched.update(streams=2, pipeline=True)
+        one = (sched["streams"], sched["pipeline"]) != (1, False)
+        sched.update(streams=1, pipeline=False) if one else sched.update(streams=2, pipeline=True)
         run_steps(1)
+        timer.enable(True)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run_steps(a.steps)
         torch.cuda.synchronize()
         el_o = time.perf_counter() - t0
-        sched.update(main_sched)
-        overlapped = {"embed_streams": 2, "pipeline": True, "value": round(a.batch * a.steps / el_o, 2),
-                      "ms_per_step": round(el_o / a.steps * 1e3, 3),
-                      "detail": "the same steps with the trunk's batch in two parts on two HIP streams (part 2 one "
+        alt_cls = {name: timer.collect(c) for name, c in (("cosine_filter", _lib.TIME_COSINE),
+                                                          ("conv_gemm", _lib.TIME_GEMM), ("select", _lib.TIME_SELECT),
+                                                          ("elementwise", _lib.TIME_ELEM),
+                                                          ("cosine_seed", _lib.TIME_COSINE_SEED),
+                                                          ("attention", _lib.TIME_ATTN))}
+        timer.enable(False)
+        alt_sched = {"embed_streams": sched["streams"], "pipeline": sched["pipeline"],
+                     "value": round(a.batch * a.steps / el_o, 2), "ms_per_step": round(el_o / a.steps * 1e3, 3),
+                     "detail": ("the same steps on one HIP stream, each kernel alone on the chip: its rooflines "
+                                "are single-kernel durations" if one else
+                                "the same steps with the trunk's batch in two parts on two HIP streams (part 2 one "
                                 "conv behind) and the ranking of batch i on a third stream beside the embed of "
-                                "batch i+1; descriptors bit-identical to the one-stream schedule "
-                                "(tests/test_gpu_overlap.py)"}
+                                "batch i+1")
+                               + "; descriptors bit-identical between the schedules (tests/test_gpu_overlap.py)"}
+        sched.update(main_sched)
 
     decorrelated = None
     if gal_bf is not None and not a.no_extras:
@@ -843,7 +861,6 @@ def main():
             floor += max(2 * 2 * 2048 * 2048 * a.batch / (PEAK_TFLOPS["fp32"] * 1e12), lin_by / (PEAK_HBM_GBS * 1e9))
         conv_floor_ms = floor * 1e3
     traffic = load_traffic()
-    rk = {}
     rank_dt = "bf16" if pre else a.dtype  # the dtype the gallery sweep runs in
     esz = {"fp32": 4, "bf16": 2, "fp8": 1}[rank_dt]
     rows_filter = max(0, (hi - lo) - s_rows)
@@ -863,54 +880,63 @@ def main():
                ("conv_gemm", conv_flops_img * a.batch, conv_bytes_step, conv_dt),
                ("cosine_seed", flop_seed, searches * float(s_rows) * a.dim * esz, rank_dt),
                ("attention", attn_flops_img * a.batch, attn_bytes, attn_dt))
-    for name, fl_step, by_step, dt in entries:
-        ms, n = cls[name]
-        if n == 0 or ms <= 0:
-            continue
-        sec = ms / 1e3 / a.steps
-        peak = PEAK_TFLOPS[dt]
-        t_mfma = fl_step / (peak * 1e12)
-        t_hbm = by_step / (PEAK_HBM_GBS * 1e9) if by_step else 0.0
-        if name == "conv_gemm" and floor_parts is not None:
-            # a class of layers with their own bounds: the bound of the layers that
-            # hold most of its roofline floor (not of the class's summed bytes vs FLOPs)
-            hbm_bound = floor_parts["hbm"] > floor_parts["mfma"]
-        else:
-            hbm_bound = t_hbm > t_mfma
-        if hbm_bound:
-            ach = by_step / sec / 1e9
-            e = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
-                 "frac": round(ach / PEAK_HBM_GBS, 4)}
-        else:
-            ach = fl_step / sec / 1e12
-            e = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                 "frac": round(ach / peak, 4)}
-        if dt in SPLIT_MATH:
-            e["math"] = SPLIT_MATH[dt][1] + (" (every conv incl. the stem; the whiten and PCA-w linears, 0.2% of "
-                                             "the FLOPs, run on the exact-fp32 core)")
-            e["mfma_flop_per_launch"] = SPLIT_MATH[dt][0] * fl_step / max(1.0, n / a.steps)
-            # the class's fp32-equivalent rate (algorithmic FLOPs / time) whichever
-            # bound is reported, against both split cores' ceilings
-            e["fp32_equiv_tflops"] = round(fl_step / sec / 1e12, 2)
-            e["frac_of_split_ceiling"] = round(fl_step / sec / 1e12 / PEAK_TFLOPS[dt], 4)
-            if dt == "h2":  # the previous core's ceiling, for comparison across rounds
-                e["frac_of_bf16x3_ceiling"] = round(fl_step / sec / 1e12 / PEAK_TFLOPS["s3"], 4)
-        e.update({"dtype": "fp32" if dt in SPLIT_MATH else dt, "ms_per_step": round(ms / a.steps, 3),
-                  "launches_per_step": n / a.steps,
-                  "algorithmic_flop_per_launch": fl_step / max(1.0, n / a.steps),
-                  "algorithmic_bytes_per_launch": (by_step / max(1.0, n / a.steps)) if by_step else None,
-                  "traffic": ((traffic or {}).get(name) or {}).get("hbm_bytes_per_launch")
-                  if (traffic and traffic.get("workload") == a.workload and a.gallery == 1_600_000
-                      and a.batch == traffic.get("batch", 320) and pre
-                      and a.conv_math == traffic.get("conv_math", "s3")) else None})
-        if name == "conv_gemm" and conv_floor_ms is not None:
-            e["layer_roofline_floor_ms_per_step"] = round(conv_floor_ms, 3)
-            e["frac_of_layer_floor"] = round(conv_floor_ms / (ms / a.steps), 4)
-            e["layer_floor_split_ms"] = {k: round(v * 1e3, 3) for k, v in floor_parts.items()}
-        rk[name] = e
-    for name in ("select", "elementwise"):
-        ms, n = cls[name]
-        rk[name] = {"ms_per_step": round(ms / a.steps, 3), "launches_per_step": n / a.steps}
+    def roofline_entries(cls):
+        rk = {}
+        for name, fl_step, by_step, dt in entries:
+            ms, n = cls[name]
+            if n == 0 or ms <= 0:
+                continue
+            sec = ms / 1e3 / a.steps
+            peak = PEAK_TFLOPS[dt]
+            t_mfma = fl_step / (peak * 1e12)
+            t_hbm = by_step / (PEAK_HBM_GBS * 1e9) if by_step else 0.0
+            if name == "conv_gemm" and floor_parts is not None:
+                # a class of layers with their own bounds: the bound of the layers that
+                # hold most of its roofline floor (not of the class's summed bytes vs FLOPs)
+                hbm_bound = floor_parts["hbm"] > floor_parts["mfma"]
+            else:
+                hbm_bound = t_hbm > t_mfma
+            if hbm_bound:
+                ach = by_step / sec / 1e9
+                e = {"bound": "hbm", "achieved": round(ach, 1), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": round(ach / PEAK_HBM_GBS, 4)}
+            else:
+                ach = fl_step / sec / 1e12
+                e = {"bound": "mfma", "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(ach / peak, 4)}
+            if dt in SPLIT_MATH:
+                e["math"] = SPLIT_MATH[dt][1] + (" (every conv incl. the stem; the whiten and PCA-w linears, 0.2% of "
+                                                 "the FLOPs, run on the exact-fp32 core)")
+                e["mfma_flop_per_launch"] = SPLIT_MATH[dt][0] * fl_step / max(1.0, n / a.steps)
+                # the class's fp32-equivalent rate (algorithmic FLOPs / time) whichever
+                # bound is reported, against both split cores' ceilings
+                e["fp32_equiv_tflops"] = round(fl_step / sec / 1e12, 2)
+                e["frac_of_split_ceiling"] = round(fl_step / sec / 1e12 / PEAK_TFLOPS[dt], 4)
+                if dt == "h2":  # the previous core's ceiling, for comparison across rounds
+                    e["frac_of_bf16x3_ceiling"] = round(fl_step / sec / 1e12 / PEAK_TFLOPS["s3"], 4)
+            e.update({"dtype": "fp32" if dt in SPLIT_MATH else dt, "ms_per_step": round(ms / a.steps, 3),
+                      "launches_per_step": n / a.steps,
+                      "algorithmic_flop_per_launch": fl_step / max(1.0, n / a.steps),
+                      "algorithmic_bytes_per_launch": (by_step / max(1.0, n / a.steps)) if by_step else None,
+                      "traffic": ((traffic or {}).get(name) or {}).get("hbm_bytes_per_launch")
+                      if (traffic and traffic.get("workload") == a.workload and a.gallery == 1_600_000
+                          and a.batch == traffic.get("batch", 320) and pre
+                          and a.conv_math == traffic.get("conv_math", "s3")) else None})
+            if name == "conv_gemm" and conv_floor_ms is not None:
+                e["layer_roofline_floor_ms_per_step"] = round(conv_floor_ms, 3)
+                e["frac_of_layer_floor"] = round(conv_floor_ms / (ms / a.steps), 4)
+                e["layer_floor_split_ms"] = {k: round(v * 1e3, 3) for k, v in floor_parts.items()}
+            rk[name] = e
+        for name in ("select", "elementwise"):
+            ms, n = cls[name]
+            rk[name] = {"ms_per_step": round(ms / a.steps, 3), "launches_per_step": n / a.steps}
+        return rk
+
+    rk = roofline_entries(cls)
+    if alt_sched is not None:
+        rk_alt = roofline_entries(alt_cls)
+        alt_sched["roofline_by_kernel"] = {k: rk_alt[k] for k in ("conv_gemm", "cosine_filter", "select",
+                                                                   "elementwise") if k in rk_alt}
     dominant = max(("cosine_filter", "conv_gemm"), key=lambda c: cls[c][0])
     roof = dict(rk[dominant])
     roof["kernel"] = dominant
@@ -932,7 +958,7 @@ def main():
                       "images_per_gpu_per_step": a.batch, "gallery_rows": a.gallery, "dim": a.dim, "k": a.k,
                       "parallelism": f"query-dp{world} + gallery-shard{world}",
                       "conv_math": a.conv_math if a.workload != "c4" else None,
-                      "pipeline": bool(a.pipeline),
+                      "pipeline": sched["pipeline"],
                       "embed_streams": sched["streams"],
                       **({"tuning": a.tune} if a.tune else {}),
                       "ranker_workspace_bytes_per_rank": int(ws.numel()),
@@ -946,8 +972,8 @@ def main():
                          "select_and_rescore_ms_per_step": rk.get("select", {}).get("ms_per_step"),
                          **(prefilter_stats or {}),
                          **({"decorrelated_queries": decorrelated} if decorrelated else {})}
-    if overlapped is not None:
-        res["overlapped_schedule"] = overlapped
+    if alt_sched is not None:
+        res["one_stream_schedule" if alt_sched["embed_streams"] == 1 else "overlapped_schedule"] = alt_sched
     if rank == 0 and world == 1 and not a.no_cpu_baseline and a.workload == "c3":
         t = time.time()
         res["cpu_baseline"] = cpu_baseline(a.arch, a.gallery, a.dim, a.k)
