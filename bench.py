@@ -508,11 +508,11 @@ def main():
                          "0 = the worst-case size, ~Q*N*8 bytes)")
     ap.add_argument("--pipeline", type=int, choices=(0, 1), default=None,
                     help="1: rank batch i on a second HIP stream while batch i+1 is embedded (n embeds + n rankings "
-                         "per n steps either way); default 1 for C3 on one GPU, else 0")
+                         "per n steps either way)")
     ap.add_argument("--embed-streams", type=int, default=None,
                     help="C3: the trunk's batch cut into this many parts, each on its own HIP stream, part i+1 one "
                          "conv behind part i (networks forward_test_u8_streams; bit-identical to serial parts); "
-                         "default 2 for C3, else 1")
+                         "default 1; C3 also reports the overlapped schedule (2 streams + pipelined ranker)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the side measurements after the timed loop (the decorrelated-query sweep and the "
@@ -598,15 +598,16 @@ def main():
 
     scales = (1.0, 1.0 / np.sqrt(2.0), 0.5)  # C5 multi-scale set
 
-    # the schedule of the timed steps (--embed-streams / --pipeline).  C3's
-    # default overlaps: the trunk's batch in two parts on two HIP streams and,
-    # on one GPU, batch i's ranking on a third beside batch i+1's embed.  Its
-    # kernels co-run, so their per-launch durations are not single-kernel
-    # durations: the line also times the one-stream schedule after the main
-    # loop and reports its per-kernel rooflines (`one_stream_schedule`).
+    # the schedule of the timed steps (--embed-streams / --pipeline): one
+    # stream by default, so that every kernel's HIP-event duration (the
+    # rooflines) is its own.  C3 also times the overlapped schedule after the
+    # main loop -- the trunk's batch in two parts on two HIP streams, batch i's
+    # ranking on a third beside batch i+1's embed -- and reports it as
+    # `overlapped_schedule` (its kernels co-run, so its per-launch durations
+    # include the other streams' work).
     c3 = a.workload == "c3"
-    n_es = a.embed_streams if a.embed_streams is not None else (2 if c3 else 1)
-    pipe = bool(a.pipeline) if a.pipeline is not None else (c3 and not DIST_ON)
+    n_es = a.embed_streams if a.embed_streams is not None else 1
+    pipe = bool(a.pipeline) if a.pipeline is not None else False
     sched = {"streams": n_es if c3 else 1, "pipeline": pipe}
     e_streams = [torch.cuda.Stream(dev) for _ in range(max(2, n_es))] if c3 else None
 
