@@ -561,7 +561,15 @@ __global__ __launch_bounds__(512, 1) void sweep128_kernel(GemmArgs g, int tiles_
   };
   auto tile_at = [&](int v) {
     int tm, tn;
-    tile_coords(v, ntiles, tiles_n, tm, tn);
+    if constexpr ((ABL & 4096) != 0) {
+      // lab: one query panel per XCD (8 / tiles_n XCDs share a panel and
+      // split its row blocks), so an XCD's L2 holds one 1.3 MB panel
+      const int x = v & 7, w = v >> 3, per = 8 / tiles_n;
+      tn = x % tiles_n;
+      tm = w * per + x / tiles_n;
+    } else {
+      tile_coords(v, ntiles, tiles_n, tm, tn);
+    }
     Tile x;
     x.m0 = tm * SW_BM;
     x.n0 = tn * SW_BN;

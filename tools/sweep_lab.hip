@@ -116,8 +116,8 @@ int main(int argc, char** argv) {
   std::vector<Variant> vs = {
       {"64-B rows: full loop", v16(rr::sweep16_kernel<8, 0>)},
       {"128-B rows: full loop", v128(rr::sweep128_kernel<0, 0>, nb)},
-      {"128-B rows: waves 4-7 at prio 1", v128(rr::sweep128_kernel<1024, 0>, nb)},
-      {"128-B rows: prio 1 around MFMAs", v128(rr::sweep128_kernel<2048, 0>, nb)},
+      {"128-B rows: panel per XCD", v128(rr::sweep128_kernel<4096, 0>, nb)},
+      {"64-B rows: full loop (again)", v16(rr::sweep16_kernel<8, 0>)},
       {"128-B rows: no DMA (stale)", v128(rr::sweep128_kernel<1, 0>, nb)},
       {"128-B rows: MFMAs + DMA (racy)", v128(rr::sweep128_kernel<6, 0>, nb)},
       {"128-B rows: MFMAs only", v128(rr::sweep128_kernel<7, 0>, nb)},
