@@ -2464,9 +2464,17 @@ int launch_gemm_h2_seg2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int ti
 //    patch row, so consecutive lanes now read consecutive 8-B slots, where
 //    the raster layout put them 16 B apart (two lanes per bank pair).
 // Same products, order and epilogue arithmetic: bit-identical output.
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void stem_pool_halo_kernel(GemmArgs g, int ntiles) {
-  constexpr int NT = 512, NW = 8, BN = 64, HR = 39, HC = 35, HP = HR * HC;  // 1365 patch pixels
+// NW = 4: four waves of 64 rows x 64 columns instead of eight of 32 x 64
+// (every wave reads the whole B operand each k-step: 32 KB of fragments per
+// k-step through LDS instead of 48 KB for the same MFMAs).  Bit-identical, and
+// measured slower: 2.20 vs 1.68 ms at 1280 images (one wave per SIMD leaves
+// nothing to cover the LDS latency; profiles/r06m_stem_4wave_ab.txt), so the
+// launch keeps NW = 8.
+template <int EPI, int NW = 8>
+__global__ __launch_bounds__(64 * NW, 1) void stem_pool_halo_kernel(GemmArgs g, int ntiles) {
+  constexpr int NT = 64 * NW, BN = 64, HR = 39, HC = 35, HP = HR * HC;  // 1365 patch pixels
+  constexpr int WR = 256 / NW, FM = WR / 32;  // rows per wave, 32-row MFMA tiles per wave
+  static_assert(NW == 8 || NW == 4, "8 waves of 32 rows or 4 of 64");
   constexpr int HS = 36, HPS = HR * HS;       // patch slots per row / in all (even | odd columns), zero slot HPS
   constexpr int KP = 224, BS = KP + 8;        // weight row (k) length; LDS row stride (u16, padded)
   constexpr int NKS = 13;                     // k-steps of 4 taps (taps 0..51)
@@ -2475,8 +2483,9 @@ __global__ __launch_bounds__(512, 1) void stem_pool_halo_kernel(GemmArgs g, int 
   constexpr int CS = BN + 4;                  // C staging row stride (floats)
   constexpr int C_U16 = 256 * CS * 2;
   constexpr int A_PASS = (HP + NT - 1) / NT;  // 3
-  constexpr int C4 = BN / 4, NPOOL = 56 * C4;  // pool work items per tile (896: one or two per thread)
-  static_assert(NPOOL > NT && NPOOL <= 2 * NT, "one or two pool items per thread");
+  constexpr int C4 = BN / 4, NPOOL = 56 * C4;  // pool work items per tile (896)
+  constexpr int QI = (NPOOL + NT - 1) / NT;     // pool items per thread (2 / 4), the last one partial
+  constexpr int PS = NKS / QI;                  // k-steps between them
   __shared__ __attribute__((aligned(16))) uint16_t lds[B_U16 + A_U16 + C_U16];
   uint16_t* lb = lds;
   uint16_t* la = lds + B_U16;
@@ -2545,11 +2554,16 @@ __global__ __launch_bounds__(512, 1) void stem_pool_halo_kernel(GemmArgs g, int 
     if (tid < 2) *reinterpret_cast<uint2*>(la + tid * (HPS + 1) * 4 + HPS * 4) = uint2{0u, 0u};  // the zero slot
   };
 
-  // lane rows: wave w owns tile rows 32 w .. +31; row r -> conv output (q, c) =
-  // (r / 15, r % 15) of the patch, input pixel of tap (kh, kw) = (2q + kh, 2c + kw),
-  // slot (2q + kh) 36 + (kw & 1) 18 + c + (kw >> 1)
-  const int row = wave * 32 + lr, rq = row / 15, rc = row - rq * 15;
-  const int sbase = row < 255 ? (2 * rq) * HS + rc : -1;
+  // lane rows: wave w owns tile rows WR w .. +WR-1 (MFMA row tile i: WR w + 32 i
+  // + lane & 31); row r -> conv output (q, c) = (r / 15, r % 15) of the patch,
+  // input pixel of tap (kh, kw) = (2q + kh, 2c + kw), slot (2q + kh) 36 +
+  // (kw & 1) 18 + c + (kw >> 1)
+  int sbase[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int row = wave * WR + 32 * i + lr, rq = row / 15, rc = row - rq * 15;
+    sbase[i] = row < 255 ? (2 * rq) * HS + rc : -1;
+  }
 
   // ---- pool work item `it` of tile tl (C staged in ct): the pooled output
   // (8 pr + it / 16 / 7, 7 pc + it / 16 % 7), channels 4 (it % 16) .. +3: max
@@ -2591,57 +2605,73 @@ __global__ __launch_bounds__(512, 1) void stem_pool_halo_kernel(GemmArgs g, int 
   __syncthreads();
   for (; tl < ntiles; tl += G) {
     load_patch(tl + G);  // the next tile's patch lands under this tile's k-loop
-    f32x16 hi[2], lo[2];
+    f32x16 hi[FM][2], lo[FM][2];
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) hi[j][r] = lo[j][r] = 0.f;
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) hi[i][j][r] = lo[i][j][r] = 0.f;
 #pragma unroll
     for (int ks = 0; ks < NKS; ++ks) {
-      frag_t a[2], b[2][2];
+      frag_t a[2][FM], b[2][2];
       const int t0 = 4 * ks + 2 * lh;
-      int pix[2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int t = t0 + u, kh = t / 7, kw = t - kh * 7;
-        pix[u] = (sbase >= 0 && t < 49) ? sbase + kh * HS + (kw & 1) * (HS / 2) + (kw >> 1) : HPS;
+      for (int i = 0; i < FM; ++i) {
+        int pix[2];
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          const int t = t0 + u, kh = t / 7, kw = t - kh * 7;
+          pix[u] = (sbase[i] >= 0 && t < 49) ? sbase[i] + kh * HS + (kw & 1) * (HS / 2) + (kw >> 1) : HPS;
+        }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+          const uint16_t* pl = la + p * (HPS + 1) * 4;
+          const f16x4 x0 = *reinterpret_cast<const f16x4*>(pl + pix[0] * 4);
+          const f16x4 x1 = *reinterpret_cast<const f16x4*>(pl + pix[1] * 4);
+          a[p][i] = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+        }
       }
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        const uint16_t* pl = la + p * (HPS + 1) * 4;
-        const f16x4 x0 = *reinterpret_cast<const f16x4*>(pl + pix[0] * 4);
-        const f16x4 x1 = *reinterpret_cast<const f16x4*>(pl + pix[1] * 4);
-        a[p] = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+      for (int p = 0; p < 2; ++p)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
           b[p][j] = *reinterpret_cast<const frag_t*>(lb + (p * BN + 32 * j + lr) * BS + 16 * ks + 8 * lh);
-      }
 #pragma unroll
-      for (int j = 0; j < 2; ++j) hi[j] = s3_mf32<2>(a[0], b[0][j], hi[j]);
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        lo[j] = s3_mf32<2>(a[0], b[1][j], lo[j]);
-        lo[j] = s3_mf32<2>(a[1], b[0][j], lo[j]);
-      }
+        for (int j = 0; j < 2; ++j) hi[i][j] = s3_mf32<2>(a[0][i], b[0][j], hi[i][j]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          lo[i][j] = s3_mf32<2>(a[0][i], b[1][j], lo[i][j]);
+          lo[i][j] = s3_mf32<2>(a[1][i], b[0][j], lo[i][j]);
+        }
       // the previous tile's pool epilogue, one work item at a time, among the MFMAs
       if (prev >= 0) {
-        if (ks == 3) pool_item(prev, tid);
-        if (ks == 8 && tid + NT < NPOOL) pool_item(prev, tid + NT);
+#pragma unroll
+        for (int q = 0; q < QI; ++q)
+          if (ks == q * PS + PS / 2 && tid + q * NT < NPOOL) pool_item(prev, tid + q * NT);
       }
     }
     __syncthreads();  // every wave done with the patch and with ct's previous tile
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
+    for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        ct[(wave * 32 + acc_row<false>(0, r, lane)) * CS + acc_col<false>(j, r, lane)] = hi[j][r] + lo[j][r];
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          ct[(wave * WR + 32 * i + acc_row<false>(0, r, lane)) * CS + acc_col<false>(j, r, lane)] =
+              hi[i][j][r] + lo[i][j][r];
     store_patch();
     prev = tl;
     __syncthreads();
   }
   if (prev >= 0) {  // the last tile's pool
-    pool_item(prev, tid);
-    if (tid + NT < NPOOL) pool_item(prev, tid + NT);
+#pragma unroll
+    for (int q = 0; q < QI; ++q)
+      if (tid + q * NT < NPOOL) pool_item(prev, tid + q * NT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr ((EPI & EP_AMAX) != 0) {
@@ -2666,7 +2696,7 @@ int launch_stem_pool_h2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int ti
     // the halo stem (7x7 / 2, pad 3; s3_cfg 7 forces the implicit-GEMM one)
     if (h->tune.s3_cfg != 7 && g.KH == 7 && g.KW == 7 && g.stride == 2 && g.pad == 3 && g.K == 224 && g.ldb == 224) {
       const int grid = (int)std::min<long long>(tiles, device_cu_count(h));
-      hipLaunchKernelGGL((stem_pool_halo_kernel<H2_EP | EP_RELU>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles);
+      hipLaunchKernelGGL((stem_pool_halo_kernel<H2_EP | EP_RELU, 8>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles);
       e = hipGetLastError();
     } else {
       e = launch_s3_t<8, 1, 1, 2, 16, A_CONV_C4, 4, 0, H2_EP | EP_RELU, 2, 2, 1>(q, s, device_cu_count(h), 0);
