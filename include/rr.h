@@ -126,8 +126,10 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     halo-staged 3x3 tile's 16x16x32 form with its B DMA spread the
  *                     same way; -1 = the library's pick (0)
  *   RR_TUNE_HALO_MF:  the f16x2 halo-staged 3x3 tiles on v_mfma_f32_16x16x32_f16 (1) or
- *                     v_mfma_f32_32x32x16_f16 (0); -1 = the library's pick (RR_TUNE_S3_CFG
- *                     13 / 14 override it)
+ *                     v_mfma_f32_32x32x16_f16 (0); for cout 64: 2 = the 512-row
+ *                     single-buffer tile (the pick where its 640-row halo holds the map,
+ *                     round 6), 3 = the persistent 256-row stream (round 5's pick);
+ *                     -1 = the library's pick (RR_TUNE_S3_CFG 13 / 14 override it)
  *   RR_TUNE_S3_CFG_RES: as RR_TUNE_S3_CFG, for the split-core GEMMs with a residual
  *                     epilogue only (0 = RR_TUNE_S3_CFG's choice)
  *   RR_TUNE_SWEEP_FORM: the bf16 filter sweeps (the prefilter's pass 2, bf16

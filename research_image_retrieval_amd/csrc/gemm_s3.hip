@@ -1676,7 +1676,13 @@ template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1, int
 __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int tiles_n) {
   constexpr int NP = 2, BK = 32, NT = 512, NW = 8;
   constexpr int WTM = 32 * FM, WTN = 32 * FN, BM = WTM * WM, BN = WTN * WN, SL = BK / 8;
-  static_assert(WM * WN == NW && BM == 256, "8 waves, 256-row tiles");
+  static_assert(WM * WN == NW && (BM == 256 || BM == 512), "8 waves, 256- or 512-row tiles");
+  // SB (the 512-row tile): ONE halo buffer.  The next slice's passes wait in
+  // registers through the slice's taps and are split into the buffer at the
+  // top of the next slice, behind a barrier of their own.
+  constexpr bool SB = BM == 512;
+  static_assert(!SB || (!PERS && !MF && !IL), "512-row tile: the one-tile form on 32x32x16");
+  constexpr int NHB = SB ? 1 : 2;  // halo buffers
   constexpr int HRA = HALO_HR + 1;                  // rows per A plane (+ the zero row)
   constexpr int A_EL = NP * HRA * BK;               // u16 per halo buffer
   constexpr int B_TAP = NP * BN * BK;               // u16 of one tap's B planes
@@ -1684,7 +1690,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   constexpr int B_RPI = 64 / SL;                    // plane rows per LDS-DMA wave instruction
   constexpr int B_INS = NP * BN / B_RPI / NW;       // LDS-DMA instructions per wave per k-tile (4 / 2 / 1)
   constexpr int A_PASS = (HALO_HR + NT / SL - 1) / (NT / SL);  // 128-row passes over the halo (3)
-  constexpr int LDS_U16 = 2 * A_EL + 2 * B_EL;
+  constexpr int LDS_U16 = NHB * A_EL + 2 * B_EL;
   static_assert(B_INS * NW * B_RPI == NP * BN, "B staging must tile the block");
   __shared__ __attribute__((aligned(16))) uint16_t lds[LDS_U16];
   typedef f16x8 frag_t;
@@ -1725,7 +1731,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   // never holds more than one pass beside the accumulators ----
   // (TPK > 1: the narrow tiles have the registers to hold every pass at once)
   const int a_slot = tid % SL, a_row = tid / SL;
-  constexpr int RA_N = TPK == 1 ? 1 : A_PASS;
+  constexpr int RA_N = (TPK == 1 && !SB) ? 1 : A_PASS;
   f32x4 ra[RA_N][2];
   auto load_pass_to = [&](int c, int p, f32x4(&r)[2], int mb) {
     const int hr = a_row + p * (NT / SL);
@@ -1734,7 +1740,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     const f32x4* src = ok ? reinterpret_cast<const f32x4*>(g.A + q * g.Cin + c * BK + a_slot * 8) : s3_zero_page();
     s3_load2<1>(src, r);
   };
-  auto load_pass = [&](int c, int p) { load_pass_to(c, p, ra[TPK == 1 ? 0 : p], m0); };
+  auto load_pass = [&](int c, int p) { load_pass_to(c, p, ra[RA_N == 1 ? 0 : p], m0); };
   auto launder_pass = [&]() {
 #pragma unroll
     for (int p = 0; p < RA_N; ++p) {
@@ -1753,7 +1759,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
       *reinterpret_cast<u32x4*>(la + HRA * BK + off) = p1;
     }
   };
-  auto store_pass = [&](int buf, int p) { store_pass_from(buf, p, ra[TPK == 1 ? 0 : p]); };
+  auto store_pass = [&](int buf, int p) { store_pass_from(buf, p, ra[RA_N == 1 ? 0 : p]); };
 
   // ---- B planes: LDS-DMA, instruction i of a wave fills plane rows
   // prow = (i NW + wave) B_RPI + lane / 4 of the [2][BN] stage (N % BN == 0:
@@ -1778,7 +1784,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
 #pragma unroll
     for (int u = 0; u < TPK; ++u) {
       const long long koff = (long long)(t0 + u) * g.Cin + c * BK;
-      uint16_t* lb = lds + 2 * A_EL + buf * B_EL + u * B_TAP;
+      uint16_t* lb = lds + NHB * A_EL + buf * B_EL + u * B_TAP;
 #pragma unroll
       for (int i = 0; i < B_INS; ++i) {
         const uint16_t* src = BN == 256 ? b_src[0] + (i >> 1) * g.b_plane + (long long)(i & 1) * (BN / 2) * g.ldb
@@ -1798,7 +1804,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     if constexpr (IL) {
       const int c = kt / ngrp, t0 = kt - c * ngrp;
       const long long koff = (long long)t0 * g.Cin + c * BK;
-      uint16_t* lb = lds + 2 * A_EL + buf * B_EL;
+      uint16_t* lb = lds + NHB * A_EL + buf * B_EL;
 #pragma unroll
       for (int i = 0; i < B_INS; ++i) {
         if (i * IL_STEP != idx) continue;
@@ -1859,7 +1865,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   auto compute = [&](int hb, int bs, int t, int u, int kt_next = 0) {
     const int kh = t / KW, kw = t - kh * KW;
     const uint16_t* la = lds + hb * A_EL;
-    const uint16_t* lb = lds + 2 * A_EL + bs * B_EL + u * B_TAP;
+    const uint16_t* lb = lds + NHB * A_EL + bs * B_EL + u * B_TAP;
     if constexpr (MF) {
       // one 32-deep k-step: lane group lg holds k 8 lg .. +7 (16-B slot lg)
 #pragma unroll
@@ -1936,8 +1942,8 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
 
   // ---- prologue: the zero rows, slice 0's halo (pass by pass), k-tile 0's B ----
   RR_PH_DECL
-  if (tid < 16) {
-    // row HALO_HR of both planes of both buffers: 4 x 64 B, 16 B per thread
+  if (tid < 8 * NHB) {
+    // row HALO_HR of both planes of every halo buffer: 64 B per plane, 16 B per thread
     const int buf = tid >> 3, p = (tid >> 2) & 1, sl = tid & 3;
     *reinterpret_cast<u32x4*>(lds + buf * A_EL + (p * HRA + HALO_HR) * BK + sl * 8) = u32x4{0u, 0u, 0u, 0u};
   }
@@ -2072,9 +2078,24 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   for (int kt = 0; kt < nk; ++kt) {
     const bool more = c + 1 < nch;
     if constexpr (!IL) glds_b(min(kt + 1, nk - 1), (kt + 1) & 1);
-    if constexpr (TPK == 1) {
+    if constexpr (TPK == 1 && !SB) {
       if (more && tg >= 1 && tg <= A_PASS) store_pass((c + 1) & 1, tg - 1);
       if (more && tg < A_PASS) load_pass(c + 1, tg);
+    } else if constexpr (SB) {
+      // one halo buffer: slice c's passes (loaded during slice c - 1) split
+      // into it once every wave is done with slice c - 1 (the last group's
+      // barrier), then a barrier before any tap reads them
+      if (c > 0 && tg == 0) {
+#pragma unroll
+        for (int p = 0; p < A_PASS; ++p) store_pass(0, p);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      if (more && tg == 0) {
+#pragma unroll
+        for (int p = 0; p < A_PASS; ++p) load_pass(c + 1, p);
+      }
     } else {
       // every pass loaded in the slice's first group, split in its second
       if (more && tg == 1) {
@@ -2088,7 +2109,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     }
     RR_PH(0);
 #pragma unroll
-    for (int u = 0; u < TPK; ++u) compute(c & 1, kt & 1, tg * TPK + u, u, min(kt + 1, nk - 1));
+    for (int u = 0; u < TPK; ++u) compute(SB ? 0 : (c & 1), kt & 1, tg * TPK + u, u, min(kt + 1, nk - 1));
     RR_PH(1);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the next B (and a halo pass)
     launder_pass();
@@ -2135,8 +2156,8 @@ static int h2_halo_rows(const GemmArgs& g) {
 }
 template <int EPI, int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int IL = 0, int PERS = 0>
 static hipError_t launch_h2_halo_t(const GemmArgs& g, hipStream_t s, int n_cu = 256) {
-  constexpr int BN = 32 * FN * WN;
-  const long long tiles_m = (g.M + 255) / 256, tiles_n = g.N / BN;
+  constexpr int BN = 32 * FN * WN, BM = 32 * FM * WM;
+  const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = g.N / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
@@ -2160,6 +2181,19 @@ static hipError_t launch_h2_halo_ep(const GemmArgs& g, hipStream_t s, int n_cu =
 // mf: 1 = the 16x16x32 form (s3_cfg 14 forces it); pers: the N = 64 instance
 // as a persistent stream (one column tile)
 static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s, int hr, int mf, bool pers = false, int n_cu = 256) {
+  // N = 64 (the 64@56 layers): the 512-row single-buffer tile, 8 waves of
+  // 64 x 64, wherever its 640-row halo holds the map (W <= 63): every wave
+  // reads 64 + 64 fragment rows per tap for 24 MFMAs instead of 64 + 32 for
+  // 12, and the taps of a barrier carry 72 MFMAs per wave instead of 36.
+  // 1.193 -> 1.059 ms at 1280 images, bit-identical
+  // (profiles/r06r_halo512_ab.txt).  halo_mf 3 forces the persistent
+  // 256-row stream (round 5's default), 2 the 512-row tile.
+  if (hr == 384 && g.N == 64 && (mf == 2 || (mf == 0 && pers)) && 512 + 2 * (g.W + 1) <= 640)
+    return launch_h2_halo_ep<8, 1, 2, 2, 640, 3, 0>(g, s);
+  if (mf >= 2) {
+    pers = pers || mf == 3;
+    mf = 0;
+  }
   if (hr == 384 && !mf && pers && g.N == 64) return launch_h2_halo_ep<4, 2, 2, 1, 384, 3, 0, 0, 1>(g, s, n_cu);
   // (the 16x16x32 256x256 form with its B DMA spread among the MFMAs: conv_il)
   if (hr == 288 && mf && g.issue_spread) return launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 1, 1>(g, s);

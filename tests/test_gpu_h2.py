@@ -559,9 +559,36 @@ def test_h2_halo_persistent_bit_identical(cuda, b, h, w, cin, res):
     bits and max-|y| record."""
     x, wt, bias, r, _, _ = _conv_case(cuda, b, h, w, cin, 64, 3, 1, 1, res, seed=29)
     outs, amax = {}, {}
-    for cfg in (13, 0):
-        with ops.tuning(0, s3_cfg=cfg):
+    # 13: the one-tile form; halo_mf 3: the persistent stream (round 5's
+    # default; the default is now the 512-row tile where it fits)
+    for cfg, mf in ((13, -1), (0, 3), (0, -1)):
+        with ops.tuning(0, s3_cfg=cfg, halo_mf=mf):
             y, rec = _run_h2(cuda, x, wt, bias, r, 1, 1)
-        outs[cfg], amax[cfg] = y.cpu(), ops.amax_value(rec[1])
-    assert torch.equal(outs[13], outs[0])
-    assert amax[13] == amax[0] == float(outs[0].abs().max())
+        outs[(cfg, mf)], amax[(cfg, mf)] = y.cpu(), ops.amax_value(rec[1])
+    ref = outs[(13, -1)]
+    for k in outs:
+        assert torch.equal(outs[k], ref), k
+        assert amax[k] == float(ref.abs().max()), k
+
+
+@pytest.mark.parametrize("b,h,w,cin,res", [
+    (24, 56, 56, 64, False),   # the R101 64@56 shape, 147 tiles of 512 rows
+    (7, 33, 63, 32, True),     # the widest map the 640-row halo holds, one slice per tile
+    (5, 20, 28, 128, False),   # four slices per tile
+    (1, 56, 56, 64, False),    # a ragged last tile
+])
+def test_h2_halo_512_bit_identical(cuda, b, h, w, cin, res):
+    """The 512-row single-buffer N = 64 halo tile (the default where its halo
+    holds the map; halo_mf 2 forces it: 8 waves of 64 x 64, one halo buffer
+    refilled behind a barrier per slice) computes the same products in the
+    same order as round 5's persistent 256-row stream (halo_mf 3): identical
+    bits and max-|y| record."""
+    x, wt, bias, r, _, _ = _conv_case(cuda, b, h, w, cin, 64, 3, 1, 1, res, seed=31)
+    outs, amax = {}, {}
+    for mf in (3, 2):
+        with ops.tuning(0, halo_mf=mf):
+            y, rec = _run_h2(cuda, x, wt, bias, r, 1, 1)
+        outs[mf], amax[mf] = y.cpu(), ops.amax_value(rec[1])
+    assert torch.equal(outs[3], outs[2])
+    assert amax[3] == amax[2] == float(outs[2].abs().max())
+

@@ -11,6 +11,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from research_image_retrieval_amd import ops  # noqa: E402
 
 dev = torch.device("cuda:0")
+if os.environ.get("H2_TUNE"):  # e.g. H2_TUNE=halo_mf=2 (rr_set_tuning keys, A/Bs)
+    ops.tuning(0, **{k: int(v) for k, v in (kv.split("=") for kv in os.environ["H2_TUNE"].split(","))}).__enter__()
 g = torch.Generator(device=dev).manual_seed(0)
 mode = sys.argv[1]
 if mode == "stem":
