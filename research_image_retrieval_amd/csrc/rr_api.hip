@@ -172,7 +172,7 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.s3_cfg_res = value;
       return RR_OK;
     case RR_TUNE_SWEEP_FORM:
-      if (!in({-1, 0, 1, 2, 3})) break;
+      if (!in({-1, 0, 1, 2})) break;
       h->tune.sweep_form = value;
       return RR_OK;
     default:
