@@ -2404,10 +2404,13 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
     // 0.671 -> 0.606; the 256x64 one lost on 64@56 (1.225 -> 1.334 ms) and
     // keeps the 32x32x16 form (profiles/r04c_h2_cfg_sweep.txt).  Forcing 13
     // selects the 32x32x16 form everywhere, 14 the 16x16x32 form everywhere.
-    if (forced == 13 || forced == 14 || (forced == 0 && ((g.N % 256) == 0 || g.N == 64))) {
+    // Round 6: N = 128 too (the 256x128 instance on 16x16x32): 128@28 1.035 ->
+    // 0.931 ms against config 11 at 1280 images, after the halo tiles' taps
+    // became compile-time (profiles/r06w_halo128_ab.txt)
+    if (forced == 13 || forced == 14 || (forced == 0 && ((g.N % 256) == 0 || g.N == 64 || g.N == 128))) {
       if (const int hr = h2_halo_rows(g))
         return launch_h2_halo(g, s, hr,
-                              forced == 14 ? 1 : forced == 13 ? 0 : g.halo_mf >= 0 ? g.halo_mf : (hr == 288 ? 1 : 0),
+                              forced == 14 ? 1 : forced == 13 ? 0 : g.halo_mf >= 0 ? g.halo_mf : (hr == 288 || hr == 320 ? 1 : 0),
                               hpers, n_cu);
     }
   }
