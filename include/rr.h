@@ -128,7 +128,9 @@ int rr_get_device(rr_handle_t h, int* device);
  *   RR_TUNE_HALO_MF:  the f16x2 halo-staged 3x3 tiles on v_mfma_f32_16x16x32_f16 (1) or
  *                     v_mfma_f32_32x32x16_f16 (0); for cout 64: 2 = the 512-row
  *                     single-buffer tile (the pick where its 640-row halo holds the map,
- *                     round 6), 3 = the persistent 256-row stream (round 5's pick);
+ *                     round 6), 3 = the persistent 256-row stream (round 5's pick); for
+ *                     cout 128: 4 = the two-buffer one-tap tile (the pick is the
+ *                     single-buffer three-tap one, round 6);
  *                     -1 = the library's pick (RR_TUNE_S3_CFG 13 / 14 override it)
  *   RR_TUNE_S3_CFG_RES: as RR_TUNE_S3_CFG, for the split-core GEMMs with a residual
  *                     epilogue only (0 = RR_TUNE_S3_CFG's choice)

@@ -1680,8 +1680,11 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   // SB (the 512-row tile): ONE halo buffer.  The next slice's passes wait in
   // registers through the slice's taps and are split into the buffer at the
   // top of the next slice, behind a barrier of their own.
-  constexpr bool SB = BM == 512;
-  static_assert(!SB || (!PERS && !MF && !IL), "512-row tile: the one-tile form on 32x32x16");
+  // (PERS 2: the one-tile form with one halo buffer at 256 rows too: room for
+  // three taps' B stages per barrier where two halo buffers left none)
+  constexpr bool SB = BM == 512 || PERS == 2;
+  constexpr bool PST = PERS == 1;  // the persistent stream
+  static_assert(!SB || (!PST && !IL && (BM == 256 || !MF)), "single-buffer halo: the one-tile form");
   constexpr int NHB = SB ? 1 : 2;  // halo buffers
   constexpr int HRA = HALO_HR + 1;                  // rows per A plane (+ the zero row)
   constexpr int A_EL = NP * HRA * BK;               // u16 per halo buffer
@@ -1701,11 +1704,11 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   const int wm = wave % WM, wn = wave / WM;
   const int lr = lane & 31, lh = lane >> 5;
 
-  static_assert(!PERS || (TPK > 1 && !IL), "persistent halo tile: the all-passes-at-once instance");
+  static_assert(!PST || (TPK > 1 && !IL), "persistent halo tile: the all-passes-at-once instance");
   const int nwg = gridDim.x, bid = blockIdx.x;
   // PERS: one block per CU walks the row tiles bid + t nwg (tiles_n == 1, so
   // the weights never change), remapped per virtual block as config 8 / 15
-  const int ntiles = PERS ? (g.M + BM - 1) / BM * tiles_n : nwg;
+  const int ntiles = PST ? (g.M + BM - 1) / BM * tiles_n : nwg;
   auto tile_m0 = [&](int tl) __attribute__((always_inline)) {
     const int v = bid + tl * nwg;
     const int xcd = v & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
@@ -1988,7 +1991,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   // landed by the end-of-tile wait) and split into the other buffer at the
   // start of tap p + 1's (that buffer's last reader was slice c - 1) ----
   static_assert(A_PASS < 9, "the halo passes must fit in one slice's taps");
-  if constexpr (PERS) {
+  if constexpr (PST) {
     // ---- the persistent stream: k-step q of the block = k-step q % nk of
     // local tile q / nk, B stage q & 1, halo buffer sg & 1 (sg: the block's
     // slice counter).  The next slice -- the tile's next, or after the
@@ -2164,7 +2167,7 @@ static hipError_t launch_h2_halo_t(const GemmArgs& g, hipStream_t s, int n_cu = 
   // PERS: one block per CU walking the row tiles (tiles_n == 1; a block that
   // owns several stays on its XCD: grid a multiple of 8)
   const int slots = std::max(8, n_cu & ~7);
-  const long long grid = PERS ? (nblk <= slots ? nblk : slots) : nblk;
+  const long long grid = PERS == 1 ? (nblk <= slots ? nblk : slots) : nblk;
   hipLaunchKernelGGL((gemm_h2_halo_kernel<EPI, WM, WN, FM, FN, HR, TPK, MF, IL, PERS>), dim3((unsigned)grid), dim3(512), 0,
                      s, g, (int)tiles_n);
   return hipGetLastError();
@@ -2190,9 +2193,15 @@ static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s, int hr, int m
   // 256-row stream (round 5's default), 2 the 512-row tile.
   if (hr == 384 && g.N == 64 && (mf == 2 || (mf == 0 && pers)) && 512 + 2 * (g.W + 1) <= 640)
     return launch_h2_halo_ep<8, 1, 2, 2, 640, 3, 0>(g, s);
+  // N = 128 on 16x16x32: one halo buffer and three taps per barrier (the
+  // LDS the second halo buffer held now holds three taps' B stages): 0.924 ->
+  // 0.897 ms at 128@28, bit-identical (profiles/r06z2_halo128_sb_ab.txt);
+  // halo_mf 4 keeps the two-buffer one-tap form for A/Bs
+  if (hr == 320 && mf == 4) return launch_h2_halo_ep<4, 2, 2, 2, 320, 1, 1>(g, s);
+  if (hr == 320 && mf == 1) return launch_h2_halo_ep<4, 2, 2, 2, 320, 3, 1, 0, 2>(g, s);
   if (mf >= 2) {
     pers = pers || mf == 3;
-    mf = 0;
+    mf = mf == 4 ? 1 : 0;
   }
   if (hr == 384 && !mf && pers && g.N == 64) return launch_h2_halo_ep<4, 2, 2, 1, 384, 3, 0, 0, 1>(g, s, n_cu);
   // (the 16x16x32 256x256 form with its B DMA spread among the MFMAs: conv_il)

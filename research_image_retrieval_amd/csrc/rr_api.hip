@@ -164,7 +164,7 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       h->tune.conv_il = value;
       return RR_OK;
     case RR_TUNE_HALO_MF:
-      if (!in({-1, 0, 1, 2, 3})) break;
+      if (!in({-1, 0, 1, 2, 3, 4})) break;
       h->tune.halo_mf = value;
       return RR_OK;
     case RR_TUNE_S3_CFG_RES:

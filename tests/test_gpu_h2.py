@@ -592,3 +592,17 @@ def test_h2_halo_512_bit_identical(cuda, b, h, w, cin, res):
     assert torch.equal(outs[3], outs[2])
     assert amax[3] == amax[2] == float(outs[2].abs().max())
 
+
+@pytest.mark.parametrize("b,h,w,cin,res", [(6, 28, 28, 128, False), (3, 17, 31, 64, True)])
+def test_h2_halo_n128_single_buffer_bit_identical(cuda, b, h, w, cin, res):
+    """N = 128: the single-buffer halo tile with three taps per barrier (the
+    default) against the two-buffer one-tap tile (halo_mf 4): same products in
+    the same order, identical bits."""
+    x, wt, bias, r, _, _ = _conv_case(cuda, b, h, w, cin, 128, 3, 1, 1, res, seed=37)
+    outs = {}
+    for mf in (-1, 4):
+        with ops.tuning(0, halo_mf=mf):
+            y, _ = _run_h2(cuda, x, wt, bias, r, 1, 1)
+        outs[mf] = y.cpu()
+    assert torch.equal(outs[-1], outs[4])
+

@@ -125,7 +125,7 @@ def test_handle_device_and_tuning_validation(cuda):
     assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_MF16, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_IL, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_CONV_IL, 2) == _lib.RR_EINVAL
-    assert L.rr_set_tuning(h, _lib.TUNE_HALO_MF, 4) == _lib.RR_EINVAL  # (2, 3: the N = 64 forms, round 6)
+    assert L.rr_set_tuning(h, _lib.TUNE_HALO_MF, 5) == _lib.RR_EINVAL  # (2-4: the N = 64 / 128 forms, round 6)
     assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_FORM, 3) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG_RES, 16) == _lib.RR_EINVAL
     for key in (_lib.TUNE_GEMM_CFG, _lib.TUNE_GEMM_BK, _lib.TUNE_LP_CFG, _lib.TUNE_S3_CFG, _lib.TUNE_SWEEP_MF16,
