@@ -139,6 +139,10 @@ int rr_get_device(rr_handle_t h, int* device);
  *                     applies), 1 = the hand-scheduled 16x16x32 sweep (csrc/sweep16.hip)
  *                     on 128-B LDS rows (K % 64 == 0; else as 2), 2 = the same on
  *                     64-B rows; -1 = the library's pick
+ *   RR_TUNE_HALO_2D:  the f16x2 stride-1 3x3 convs on 2-D block halo tiles (16 x 16 or,
+ *                     for cout 64, 16 x 32 outputs of one image; no residual epilogue):
+ *                     -1 = where no raster halo tile holds the map (the library's pick),
+ *                     1 = wherever one serves, 0 = never (ABI 6, round 6)
  * Any other key or value: RR_EINVAL. */
 #define RR_TUNE_GEMM_CFG 1
 #define RR_TUNE_GEMM_BK 2
@@ -153,6 +157,7 @@ int rr_get_device(rr_handle_t h, int* device);
 /* 12: retired (ABI 5) */
 #define RR_TUNE_S3_CFG_RES 13
 #define RR_TUNE_SWEEP_FORM 14
+#define RR_TUNE_HALO_2D 15
 int rr_set_tuning(rr_handle_t h, int key, int value);
 
 /* ---- search (ranker) ----------------------------------------------------

@@ -24,8 +24,8 @@ TIME_COSINE, TIME_GEMM, TIME_SELECT, TIME_ELEM, TIME_COSINE_SEED, TIME_ATTN = 0,
 # rr_set_tuning keys
 # (6, 7 and 12 -- sweep_order, sweep_pf, lp_il -- were retired in ABI 5)
 TUNE_GEMM_CFG, TUNE_GEMM_BK, TUNE_LP_CFG, TUNE_S3_CFG, TUNE_S3_STAGGER, \
-    TUNE_SWEEP_MF16, TUNE_SWEEP_IL, TUNE_CONV_IL, TUNE_HALO_MF, TUNE_S3_CFG_RES, TUNE_SWEEP_FORM = \
-    1, 2, 3, 4, 5, 8, 9, 10, 11, 13, 14
+    TUNE_SWEEP_MF16, TUNE_SWEEP_IL, TUNE_CONV_IL, TUNE_HALO_MF, TUNE_S3_CFG_RES, TUNE_SWEEP_FORM, TUNE_HALO_2D = \
+    1, 2, 3, 4, 5, 8, 9, 10, 11, 13, 14, 15
 
 _lib = None
 _lock = threading.RLock()

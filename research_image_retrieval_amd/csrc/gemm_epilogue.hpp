@@ -146,6 +146,24 @@ __device__ __forceinline__ int ep_opaque(int v) {
   return v;
 }
 
+// Row maps of epilogue_store / store_slab: (slab base mb, slab row) -> output
+// row, >= g.M for a row that is not stored.  RowsLinear: the raster tiles
+// (rows mb + row).  Rows2D<TW>: gemm_h2_halo_kernel's 2-D block tiles, tile
+// row r = mb + row is output pixel (y0 + r / TW, x0 + r % TW) of the image
+// whose first output row is img (H x W map), stored only inside the map.
+struct RowsLinear {
+  __device__ __forceinline__ int operator()(int mb, int row) const { return mb + row; }
+};
+template <int TW>
+struct Rows2D {
+  static constexpr int kTW = TW;
+  int img, y0, x0, H, W;
+  __device__ __forceinline__ int operator()(int mb, int row) const {
+    const int r = mb + row, y = y0 + r / TW, x = x0 + r % TW;
+    return (y < H && x < W) ? img + y * W + x : 0x7fffffff;
+  }
+};
+
 // Write one staged slab (rows mb.. of the tile, row-major in ct): the LDS
 // reads of a group of row chunks first (counted lgkmcnt waits instead of an
 // LDS round trip between consecutive stores; the whole slab at once when no
@@ -157,10 +175,12 @@ __device__ __forceinline__ int ep_opaque(int v) {
 // CSW: the staged rows are unpadded with their 16-B chunks XOR-swizzled,
 // chunk c of row r at c ^ (((r >> 2) & 1) << 2) (csw_chunk; gemm_lpp.hip)
 __device__ __forceinline__ int csw_chunk(int row, int c4) { return c4 ^ (((row >> 2) & 1) << 2); }
-template <int FL, int P, int ITERS, int NT, int C4, int CS, int BI, int CSW = 0>
+template <int FL, int P, int ITERS, int NT, int C4, int CS, int BI, int CSW = 0, class RM = RowsLinear>
 __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const float* ct, const f32x4 (&bias_v)[BI],
                                            const f32x4 (&res)[ITERS], int tid, int mb, int n0, const f32x4 (&sc_v)[BI],
-                                           float& am, const float* ln_l = nullptr, const float* ln_cs = nullptr) {
+                                           float& am, const float* ln_l = nullptr, const float* ln_cs = nullptr,
+                                           RM rm = RM{}) {
+  constexpr bool LIN = __is_same(RM, RowsLinear);
   typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
   constexpr bool FIXED = FL >= 0;
   // (the LayerNorm fold's epilogue holds two more values per row: fewer LDS reads ahead)
@@ -177,6 +197,14 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
 
   const int n_fix = n0 + c40 * 4;
   const long long o0 = (long long)(mb + r0) * g.ldc + n_fix;
+  // (Rows2D: the thread's first row's pixel and output row)
+  int r2y = 0, r2x = 0, r2m = 0;
+  if constexpr (!LIN) {
+    const int rb = mb + r0;
+    r2y = rm.y0 + rb / RM::kTW;
+    r2x = rm.x0 + rb % RM::kTW;
+    r2m = rm.img + r2y * rm.W + r2x;
+  }
   const long long ostep = (long long)RSTEP * g.ldc;
   f32x4 cv[ITERS];
 #pragma unroll
@@ -191,14 +219,26 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
     }
     int m, n;
     long long o;
-    if constexpr (FIXED && BI == 1) {
+    if constexpr (FIXED && BI == 1 && LIN) {
       m = mb + r0 + it * RSTEP;
       n = n_fix;
       o = o0 + it * ostep;
+    } else if constexpr (FIXED && BI == 1) {
+      // Rows2D: iteration it is the thread's base pixel + (k / TW) map rows +
+      // k % TW columns, k = it RSTEP (RSTEP divides TW, r0 < RSTEP and the
+      // slab starts a block row: no carry), so the compile-time steps cost an
+      // add each instead of a row map per iteration (that spilled the
+      // 256x256 tile)
+      constexpr int TW = RM::kTW;
+      static_assert(TW % RSTEP == 0, "Rows2D: whole steps per block row");
+      const int k = it * RSTEP, dy = k / TW, dx = k % TW;
+      m = (r2y + dy < rm.H && r2x + dx < rm.W) ? r2m + dy * rm.W + dx : 0x7fffffff;
+      n = n_fix;
+      o = (long long)m * g.ldc + n;
     } else {
       const int idx = tid + it * NT;
       const int row = idx / C4, c4 = idx - row * C4;
-      m = mb + row;
+      m = rm(mb, row);
       n = n0 + c4 * 4;
       o = (long long)m * g.ldc + n;
     }
@@ -269,9 +309,11 @@ __device__ __forceinline__ void store_slab(const GemmArgs& g, float* Cb, const f
 // (one HBM round trip per slab, overlapping the staging).  When the tile exceeds the CAPF floats of LDS it goes in P row
 // slabs.  Called by every thread of the block after the k-loop's last
 // barrier (the LDS is free).
-template <int WM, int WN, int FM, int FN, int CAPF, bool MF16 = false, int FL = -1>
+template <int WM, int WN, int FM, int FN, int CAPF, bool MF16 = false, int FL = -1, class RM = RowsLinear>
 __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, const f32x16 (&acc)[FM][FN], float* lds,
-                                               int m0, int n0, float a_isc = 1.f, const float* ln_lds = nullptr) {
+                                               int m0, int n0, float a_isc = 1.f, const float* ln_lds = nullptr,
+                                               RM rm = RM{}) {
+  // (rm: the tile's row map, RowsLinear or Rows2D; row r of the tile is output row rm(m0, r))
   // (EP_LNFOLD: ln_lds = [BM][LN_ROW] row statistics, then [LN_TMAX][BN] column sums)
   constexpr int NT = 64 * WM * WN;
   constexpr int WTM = 32 * FM, WTN = 32 * FN;
@@ -305,6 +347,9 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
   constexpr int BI = (NT % C4 == 0) ? 1 : ITERS;
   constexpr bool SCALED = FL >= 0 && (FL & EP_SCALE) != 0;
   static_assert(!(FL >= 0 && (FL & (EP_SCALE | EP_AMAX))) || BI == 1, "scaled epilogues: one column per thread");
+  // (a row-mapped tile with fixed flags and no residual drops the residual
+  // loads at compile time: their mapped addresses spilled the 256x256 tile)
+  constexpr bool RES_C = __is_same(RM, RowsLinear) || FL < 0 || (FL & EP_RES) != 0;
   f32x4 bias_v[BI], sc_v[BI];
   float am = 0.f;
   if (vec_ok) {
@@ -326,12 +371,12 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
     // accumulators and its barrier
     constexpr bool PREF = P == 1 && ITERS * 4 + FM * FN * 16 <= 160;
     f32x4 res[ITERS];
-    if (PREF && vec_ok && g.residual != nullptr) {
+    if (RES_C && PREF && vec_ok && g.residual != nullptr) {
 #pragma unroll
       for (int it = 0; it < ITERS; ++it) {
         const int idx = tid + it * NT;
         const int row = idx / C4, c4 = idx - row * C4;
-        const int m = m0 + rbase + row, n = n0 + c4 * 4;
+        const int m = rm(m0 + rbase, row), n = n0 + c4 * 4;
         if (m < g.M && n < g.N) res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
       }
     }
@@ -350,12 +395,12 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
     }
     __syncthreads();
     if (vec_ok) {
-      if (!PREF && g.residual != nullptr) {
+      if (RES_C && !PREF && g.residual != nullptr) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) {
           const int idx = tid + it * NT;
           const int row = idx / C4, c4 = idx - row * C4;
-          const int m = m0 + rbase + row, n = n0 + c4 * 4;
+          const int m = rm(m0 + rbase, row), n = n0 + c4 * 4;
           if (m < g.M && n < g.N) res[it] = *reinterpret_cast<const f32x4*>(g.residual + (long long)m * g.ldc + n);
         }
       }
@@ -370,17 +415,17 @@ __device__ __forceinline__ void epilogue_store(const GemmArgs& g, float* Cb, con
 #pragma unroll
         for (int it = 0; it < BI; ++it) asm volatile("" : "+v"(sc_v[it]));
       }
-      if (g.residual != nullptr) {
+      if (RES_C && g.residual != nullptr) {
 #pragma unroll
         for (int it = 0; it < ITERS; ++it) asm volatile("" : "+v"(res[it]));
       }
-      store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, CS, BI>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0, sc_v, am,
-                                                                 ln_lds ? ln_lds + LN_ROW * rbase : nullptr,
-                                                                 ln_lds ? ln_lds + LN_ROW * BM : nullptr);
+      store_slab<(BI == 1 ? FL : -1), P, ITERS, NT, C4, CS, BI, 0, RM>(g, Cb, ct, bias_v, res, tid, m0 + rbase, n0, sc_v,
+                                                                       am, ln_lds ? ln_lds + LN_ROW * rbase : nullptr,
+                                                                       ln_lds ? ln_lds + LN_ROW * BM : nullptr, rm);
     } else {
       for (int idx = tid; idx < SLAB * C4; idx += NT) {
         const int row = idx / C4, c4 = idx - row * C4;
-        const int m = m0 + rbase + row, n = n0 + c4 * 4;
+        const int m = rm(m0 + rbase, row), n = n0 + c4 * 4;
         if (m >= g.M || n >= g.N) continue;
         const f32x4 v = *reinterpret_cast<const f32x4*>(ct + row * CS + c4 * 4);
         const long long o = (long long)m * g.ldc + n;

@@ -1672,7 +1672,15 @@ __device__ __forceinline__ int hswz(int row, int slot) { return slot ^ ((row >> 
 // IL (16x16x32, one tap per barrier): the next k-tile's B DMA goes out one
 // instruction at a time among the k-tile's first MFMAs instead of as one
 // burst before them (the halo pass load stays at the top: it comes from HBM).
-template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1, int MF = 0, int IL = 0, int PERS = 0>
+// T2 (round 6): 2-D block tiles for maps too wide for a raster halo.  The
+// tile is TH x T2 output pixels of one image (TH = BM / T2); its halo is the
+// (TH + 2) x (T2 + 2) input block around them, out-of-image pixels loaded as
+// zeros, so every tap of an in-map row is live (no tap masks) and output row
+// r = (oy, ox) reads halo row (oy + kh)(T2 + 2) + ox + kw; rows outside the
+// map are neither computed from (the zero row) nor stored (Rows2D).  Same
+// products in the same order as the raster tile: bit-identical to it.
+template <int EPI, int WM, int WN, int FM, int FN, int HALO_HR, int TPK = 1, int MF = 0, int IL = 0, int PERS = 0,
+          int T2 = 0>
 __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int tiles_n) {
   constexpr int NP = 2, BK = 32, NT = 512, NW = 8;
   constexpr int WTM = 32 * FM, WTN = 32 * FN, BM = WTM * WM, BN = WTN * WN, SL = BK / 8;
@@ -1686,6 +1694,9 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   constexpr bool PST = PERS == 1;  // the persistent stream
   static_assert(!SB || (!PST && !IL && (BM == 256 || !MF)), "single-buffer halo: the one-tile form");
   constexpr int NHB = SB ? 1 : 2;  // halo buffers
+  constexpr int TH = T2 ? BM / T2 : 1, HWD = T2 + 2;  // T2: the tile's output rows, the halo's width
+  constexpr int NHR = T2 ? (TH + 2) * HWD : HALO_HR;   // halo rows a tile loads
+  static_assert(!T2 || (BM % T2 == 0 && T2 % (MF ? 16 : 32) == 0 && NHR <= HALO_HR && !PST && !IL), "2-D tile");
   constexpr int HRA = HALO_HR + 1;                  // rows per A plane (+ the zero row)
   constexpr int A_EL = NP * HRA * BK;               // u16 per halo buffer
   constexpr int B_TAP = NP * BN * BK;               // u16 of one tap's B planes
@@ -1728,6 +1739,20 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   constexpr int KW = 3, KH = 3, ntap = KH * KW;
   const int nch = g.Cin / BK, ngrp = ntap / TPK, nk = nch * ngrp;  // k-step kt = (slice, group of TPK taps)
   const int hoff = g.pad * W + g.pad;  // halo row 0 = input raster index m0 - hoff
+  // T2: the tile's image (its first output row) and top-left output pixel
+  int t_img = 0, t_y0 = 0, t_x0 = 0;
+  if constexpr (T2 != 0) {
+    const int mt = m0 / BM, tx_n = (W + T2 - 1) / T2, tpi = (H + TH - 1) / TH * tx_n;
+    const int im = mt / tpi, rem = mt - im * tpi, ty = rem / tx_n;
+    t_img = im * H * W;
+    t_y0 = ty * TH;
+    t_x0 = (rem - ty * tx_n) * T2;
+  }
+  // the halo row (tap (0, 0)) of tile row rb + l (rb a multiple of the
+  // fragment height, l below it, so l stays an offset: T2 % 32 == 0 for the
+  // 32x32 fragments), and the halo-row step of kh
+  auto hrow = [&](int rb, int l) __attribute__((always_inline)) { return T2 ? (rb / T2) * HWD + rb % T2 + l : rb + l; };
+  const int tstep = T2 ? HWD : W;
 
   // ---- halo loader: thread -> (row t / 4 + 128 pass, 16-B slot pair t % 4);
   // one 128-row pass at a time (8 registers), so the halo of the next slice
@@ -1738,8 +1763,18 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
   f32x4 ra[RA_N][2];
   auto load_pass_to = [&](int c, int p, f32x4(&r)[2], int mb) {
     const int hr = a_row + p * (NT / SL);
-    const long long q = (long long)mb - hoff + hr;
-    const bool ok = hr < HALO_HR && q >= 0 && q < g.M;
+    long long q;
+    bool ok;
+    if constexpr (T2 != 0) {
+      // (from an opaque row: hoisted out of the k-loop, the three passes'
+      // addresses and bounds would be held beside the accumulators)
+      const int ho = s3_opaque(hr), hy = ho / HWD, iy = t_y0 - 1 + hy, ix = t_x0 - 1 + (ho - hy * HWD);
+      q = (long long)t_img + iy * W + ix;
+      ok = hr < NHR && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+    } else {
+      q = (long long)mb - hoff + hr;
+      ok = hr < HALO_HR && q >= 0 && q < g.M;
+    }
     const f32x4* src = ok ? reinterpret_cast<const f32x4*>(g.A + q * g.Cin + c * BK + a_slot * 8) : s3_zero_page();
     s3_load2<1>(src, r);
   };
@@ -1834,6 +1869,12 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
 #pragma unroll
       for (int a = 0; a < RPT; ++a) {
         const int m = mb + wm * WTM + i * 32 + (MF ? 16 * a + l16 : lr);
+        if constexpr (T2 != 0) {
+          // every tap reads the halo (zeros off the image); rows off the map
+          // compute from it too, finite, and are not stored (Rows2D)
+          tmask[i][a] = (1 << ntap) - 1;
+          continue;
+        }
         const int rem = m % (H * W), oh = rem / W, ow = rem - oh * W;
         int mk = 0;
         for (int kh = 0; kh < KH; ++kh)
@@ -1876,7 +1917,7 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
         frag_t fa[NP][FM];
 #pragma unroll
         for (int i = 0; i < FM; ++i) {
-          const int ar = ((tmask[i][a] >> t) & 1) ? wm * WTM + i * 32 + 16 * a + l16 + kh * W + kw : HALO_HR;
+          const int ar = ((tmask[i][a] >> t) & 1) ? hrow(wm * WTM + i * 32 + 16 * a, l16) + kh * tstep + kw : HALO_HR;
 #pragma unroll
           for (int p = 0; p < NP; ++p)
             fa[p][i] = *reinterpret_cast<const frag_t*>(la + (p * HRA + ar) * BK + hswz(ar, lg) * 8);
@@ -1914,7 +1955,8 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
     }
     int ar[FM];
 #pragma unroll
-    for (int i = 0; i < FM; ++i) ar[i] = ((tmask[i][0] >> t) & 1) ? wm * WTM + i * 32 + lr + kh * W + kw : HALO_HR;
+    for (int i = 0; i < FM; ++i)
+      ar[i] = ((tmask[i][0] >> t) & 1) ? hrow(wm * WTM + i * 32, lr) + kh * tstep + kw : HALO_HR;
 #pragma unroll
     for (int st = 0; st < BK / 16; ++st) {
       frag_t a[NP][FM], b[NP][FN];
@@ -2137,8 +2179,12 @@ __global__ __launch_bounds__(512, 1) void gemm_h2_halo_kernel(GemmArgs g, int ti
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[i][j][4 * t + e] = acc4[i][j][t][e];
   }
-  epilogue_store<WM, WN, FM, FN, LDS_U16 / 2, (bool)MF, EPI>(g, g.C, acc, reinterpret_cast<float*>(lds), m0, n0,
-                                                             a_isc);
+  if constexpr (T2 != 0)
+    epilogue_store<WM, WN, FM, FN, LDS_U16 / 2, (bool)MF, EPI, Rows2D<T2>>(
+        g, g.C, acc, reinterpret_cast<float*>(lds), 0, n0, a_isc, nullptr, Rows2D<T2>{t_img, t_y0, t_x0, H, W});
+  else
+    epilogue_store<WM, WN, FM, FN, LDS_U16 / 2, (bool)MF, EPI>(g, g.C, acc, reinterpret_cast<float*>(lds), m0, n0,
+                                                               a_isc);
   RR_PH(6);
   RR_PH_FLUSH(3);
 }
@@ -2157,10 +2203,13 @@ static int h2_halo_rows(const GemmArgs& g) {
   if ((g.N % 64) == 0) return need <= 384 ? 384 : 0;
   return 0;
 }
-template <int EPI, int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int IL = 0, int PERS = 0>
+template <int EPI, int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int IL = 0, int PERS = 0, int T2 = 0>
 static hipError_t launch_h2_halo_t(const GemmArgs& g, hipStream_t s, int n_cu = 256) {
   constexpr int BN = 32 * FN * WN, BM = 32 * FM * WM;
-  const long long tiles_m = (g.M + BM - 1) / BM, tiles_n = g.N / BN;
+  // (T2: images x row blocks x column blocks of the map)
+  const long long tiles_m = T2 ? (long long)(g.M / (g.H * g.W)) * ((g.H + BM / T2 - 1) / (BM / T2)) * ((g.W + T2 - 1) / T2)
+                               : (g.M + BM - 1) / BM,
+                  tiles_n = g.N / BN;
   const long long nblk = tiles_m * tiles_n;
   if (nblk <= 0) return hipSuccess;
   if (nblk > 0x7fffffffLL) return hipErrorInvalidValue;
@@ -2168,8 +2217,8 @@ static hipError_t launch_h2_halo_t(const GemmArgs& g, hipStream_t s, int n_cu = 
   // owns several stays on its XCD: grid a multiple of 8)
   const int slots = std::max(8, n_cu & ~7);
   const long long grid = PERS == 1 ? (nblk <= slots ? nblk : slots) : nblk;
-  hipLaunchKernelGGL((gemm_h2_halo_kernel<EPI, WM, WN, FM, FN, HR, TPK, MF, IL, PERS>), dim3((unsigned)grid), dim3(512), 0,
-                     s, g, (int)tiles_n);
+  hipLaunchKernelGGL((gemm_h2_halo_kernel<EPI, WM, WN, FM, FN, HR, TPK, MF, IL, PERS, T2>), dim3((unsigned)grid), dim3(512),
+                     0, s, g, (int)tiles_n);
   return hipGetLastError();
 }
 template <int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int IL = 0, int PERS = 0>
@@ -2209,6 +2258,39 @@ static hipError_t launch_h2_halo(const GemmArgs& g, hipStream_t s, int hr, int m
   if (hr == 288) return mf ? launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 1>(g, s) : launch_h2_halo_ep<2, 4, 4, 2, 288, 1, 0>(g, s);
   if (hr == 320) return mf ? launch_h2_halo_ep<4, 2, 2, 2, 320, 1, 1>(g, s) : launch_h2_halo_ep<4, 2, 2, 2, 320, 1, 0>(g, s);
   return mf ? launch_h2_halo_ep<4, 2, 2, 1, 384, 3, 1>(g, s) : launch_h2_halo_ep<4, 2, 2, 1, 384, 3, 0>(g, s);
+}
+
+// The 2-D block tiles (T2) for the stride-1 3x3 layers of maps too wide for a
+// raster halo (C2's 1024-px layers 1-3: W 256 / 128 / 64): the tile's halo is
+// (TH + 2)(T2 + 2) rows whatever W is.  Instances: 16 x 16 outputs, 18 x 18 =
+// 324 halo rows, on the 256x256 (N % 256) and 256x128 single-buffer three-tap
+// (N = 128) tiles; 16 x 32 outputs, 18 x 34 = 612 rows, on the 512-row N = 64
+// tile.  No residual epilogue (the trunk's 3x3s have none).  Returns whether
+// one serves g.
+static bool h2_halo_2d_ok(const GemmArgs& g) {
+  if (!(g.KH == 3 && g.KW == 3 && g.stride == 1 && g.pad == 1 && g.OH == g.H && g.OW == g.W && (g.Cin % 32) == 0 &&
+        g.K == 9 * g.Cin && g.col_scale != nullptr && g.a_amax != nullptr && g.H > 0 && g.W > 0 &&
+        (g.M % (g.H * g.W)) == 0 && (ep_flags(g) & EP_RES) == 0))
+    return false;
+  if (g.N == 128) {
+    // the N = 128 tile needs a block per CU: below that config 11's
+    // 128-column tiles spread further (a batch-1 128@75x100 crop, 35 blocks:
+    // 0.040 -> 0.045 ms; 64 images of 128@128x96: 0.811 -> 0.685 ms;
+    // profiles/r06zb_halo2d_ab.txt)
+    const long long blocks = (long long)(g.M / (g.H * g.W)) * ((g.H + 15) / 16) * ((g.W + 15) / 16);
+    return blocks >= 256 || g.halo_2d == 1;
+  }
+  return (g.N % 256) == 0 || g.N == 64;
+}
+template <int WM, int WN, int FM, int FN, int HR, int TPK, int MF, int PERS, int T2>
+static hipError_t launch_h2_halo_2d_ep(const GemmArgs& g, hipStream_t s) {
+  if ((ep_flags(g) & EP_RELU) != 0) return launch_h2_halo_t<H2_EP | EP_RELU, WM, WN, FM, FN, HR, TPK, MF, 0, PERS, T2>(g, s);
+  return launch_h2_halo_t<H2_EP, WM, WN, FM, FN, HR, TPK, MF, 0, PERS, T2>(g, s);
+}
+static hipError_t launch_h2_halo_2d(const GemmArgs& g, hipStream_t s) {
+  if (g.N == 64) return launch_h2_halo_2d_ep<8, 1, 2, 2, 640, 3, 0, 0, 32>(g, s);
+  if (g.N == 128) return launch_h2_halo_2d_ep<4, 2, 2, 2, 324, 3, 1, 2, 16>(g, s);
+  return launch_h2_halo_2d_ep<2, 4, 4, 2, 324, 1, 1, 0, 16>(g, s);
 }
 
 // config 8 serves dense A (1x1 convs), N % 256 == 0 and the ResNet's flag
@@ -2416,6 +2498,10 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
     // Round 6: N = 128 too (the 256x128 instance on 16x16x32): 128@28 1.035 ->
     // 0.931 ms against config 11 at 1280 images, after the halo tiles' taps
     // became compile-time (profiles/r06w_halo128_ab.txt)
+    // halo_2d: the 2-D block tiles where no raster halo holds the map (-1),
+    // wherever one serves (1), never (0)
+    if (forced == 0 && g.halo_2d != 0 && h2_halo_2d_ok(g) && (g.halo_2d == 1 || !h2_halo_rows(g)))
+      return launch_h2_halo_2d(g, s);
     if (forced == 13 || forced == 14 || (forced == 0 && ((g.N % 256) == 0 || g.N == 64 || g.N == 128))) {
       if (const int hr = h2_halo_rows(g))
         return launch_h2_halo(g, s, hr,
@@ -2788,6 +2874,7 @@ int launch_gemm_s3(rr_handle_s* h, int amode, const GemmArgs& g, hipStream_t s, 
       GemmArgs g2 = g;
       g2.issue_spread = h->tune.conv_il == 1;
       g2.halo_mf = h->tune.halo_mf;
+      g2.halo_2d = h->tune.halo_2d;
       e = amode == A_DENSE ? launch_h2_am<A_DENSE>(g2, s, f, n_cu, st)
           : amode == A_CONV ? launch_h2_am<A_CONV>(g2, s, f, n_cu, st)
                             : launch_h2_am<A_CONV_C4>(g2, s, f, n_cu, st);

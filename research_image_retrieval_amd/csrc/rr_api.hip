@@ -175,6 +175,10 @@ int rr_set_tuning(rr_handle_t h, int key, int value) {
       if (!in({-1, 0, 1, 2})) break;
       h->tune.sweep_form = value;
       return RR_OK;
+    case RR_TUNE_HALO_2D:
+      if (!in({-1, 0, 1})) break;
+      h->tune.halo_2d = value;
+      return RR_OK;
     default:
       return set_error(h, RR_EINVAL, "rr_set_tuning: unknown key");
   }

@@ -26,6 +26,7 @@ struct rr_handle_s {
     int sweep_il = -1;     // bf16 256x320 filter sweep: next k-tile's DMA spread among the MFMAs (1) or one burst (0); -1: the pick (1)
     int conv_il = -1;      // f16x2 256x256 conv tile (s3_cfg 12) and halo 16x16x32 tile: next k-tiles' loads spread among the MFMAs (1) or one burst (0); -1: the pick (0)
     int halo_mf = -1;      // f16x2 halo 3x3 tiles on v_mfma_f32_16x16x32_f16 (1) or 32x32x16 (0); -1: the pick (the 256x256 tile 1, the others 0)
+    int halo_2d = -1;      // the 2-D block halo tiles: -1 where no raster halo holds the map, 1 wherever one serves, 0 never
     int s3_cfg_res = 0;    // split cores: forced tile config for the GEMMs with a residual epilogue only (0: s3_cfg's)
     int sweep_form = -1;   // bf16 filter sweeps: 0 = gemm_f32.hip's tiles, 1 / 2 = sweep16.hip on 128-B / 64-B LDS rows; -1: the pick
   } tune;
@@ -242,6 +243,7 @@ struct GemmArgs {
   int mf16_sweep = 0;
   int issue_spread = 0;
   int halo_mf = -1;
+  int halo_2d = -1;
 };
 
 // 64-lane sum, returned wave-uniform: DPP row_shr 1/2/4/8 sums each 16-lane

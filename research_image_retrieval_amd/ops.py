@@ -426,9 +426,9 @@ _TUNE_KEYS = {"gemm_cfg": _lib.TUNE_GEMM_CFG, "gemm_bk": _lib.TUNE_GEMM_BK, "lp_
               "s3_cfg": _lib.TUNE_S3_CFG, "s3_stagger": _lib.TUNE_S3_STAGGER, "sweep_mf16": _lib.TUNE_SWEEP_MF16,
               "sweep_il": _lib.TUNE_SWEEP_IL, "conv_il": _lib.TUNE_CONV_IL,
               "halo_mf": _lib.TUNE_HALO_MF, "s3_cfg_res": _lib.TUNE_S3_CFG_RES,
-              "sweep_form": _lib.TUNE_SWEEP_FORM}
+              "sweep_form": _lib.TUNE_SWEEP_FORM, "halo_2d": _lib.TUNE_HALO_2D}
 _TUNE_DEFAULT = {"s3_stagger": -1, "sweep_mf16": -1, "sweep_il": -1,
-                 "conv_il": -1, "halo_mf": -1, "sweep_form": -1}  # the library's own pick (0 elsewhere)
+                 "conv_il": -1, "halo_mf": -1, "sweep_form": -1, "halo_2d": -1}  # the library's own pick (0 elsewhere)
 
 
 class tuning:

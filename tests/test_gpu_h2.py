@@ -606,3 +606,59 @@ def test_h2_halo_n128_single_buffer_bit_identical(cuda, b, h, w, cin, res):
         outs[mf] = y.cpu()
     assert torch.equal(outs[-1], outs[4])
 
+
+
+@pytest.mark.parametrize("b,h,w,cin,cout", [
+    (2, 14, 14, 64, 256),    # one 16 x 16 block per image, two Cin slices
+    (3, 15, 13, 32, 256),    # ragged blocks, one slice
+    (2, 28, 28, 128, 128),   # 2 x 2 blocks per image
+    (1, 27, 31, 64, 128),    # the widest map the 320-row raster halo holds
+    (2, 56, 56, 64, 64),     # 16 x 32 blocks (the 512-row N = 64 tile), 4 x 2 per image
+    (3, 17, 40, 32, 64),     # ragged 16 x 32 blocks
+])
+def test_h2_halo_2d_bit_identical(cuda, b, h, w, cin, cout):
+    """The 2-D block halo tiles (halo_2d 1 forces them where the raster halo
+    also serves) compute every output from the same products in the same
+    order as the raster halo tiles (halo_2d 0): identical bits and max-|y|
+    record, the ragged blocks' off-map rows neither stored nor counted."""
+    x, wt, bias, r, _, _ = _conv_case(cuda, b, h, w, cin, cout, 3, 1, 1, False, seed=41)
+    outs, amax = {}, {}
+    for t2 in (0, 1):
+        with ops.tuning(0, halo_2d=t2):
+            y, rec = _run_h2(cuda, x, wt, bias, r, 1, 1)
+        outs[t2], amax[t2] = y.cpu(), ops.amax_value(rec[1])
+    assert torch.equal(outs[0], outs[1])
+    assert amax[0] == amax[1] == float(outs[1].abs().max())
+
+
+@pytest.mark.parametrize("b,h,w,cin,cout,res", [
+    (1, 20, 40, 64, 256, False),    # N % 256, W = 40: the raster tile would need 338 halo rows (288)
+    (2, 33, 50, 128, 128, False),   # N = 128, W = 50 (358 > 320)
+    (1, 18, 70, 64, 64, False),     # N = 64, W = 70 (654 > 640)
+    (1, 9, 130, 32, 64, False),     # N = 64, one ragged block row, five block columns
+    (1, 20, 40, 64, 256, True),     # a residual epilogue: not a 2-D tile's, falls back
+])
+def test_conv2d_h2_halo_2d_wide(cuda, b, h, w, cin, cout, res):
+    """Maps too wide for a raster halo: the 2-D block tiles (forced) at the
+    f16x2 bar against float64 and the exact-fp32 core, with the max-|y| record
+    exact; the default is bit-identical to them, except for N = 128 on fewer
+    blocks than CUs (and residual epilogues), where it keeps the implicit GEMM."""
+    x, wt, bias, r, ref, scale = _conv_case(cuda, b, h, w, cin, cout, 3, 1, 1, res, seed=43)
+    with ops.tuning(0, halo_2d=1):
+        y, rec = _run_h2(cuda, x, wt, bias, r, 1, 1)
+    y = y.cpu()
+    y_def, _ = _run_h2(cuda, x, wt, bias, r, 1, 1)
+    with ops.tuning(0, halo_2d=0):
+        y_off, _ = _run_h2(cuda, x, wt, bias, r, 1, 1)
+    small128 = cout == 128 and b * ((h + 15) // 16) * ((w + 15) // 16) < 256
+    assert torch.equal(y_def.cpu(), (y_off if small128 or res else y).cpu())
+    rd = r.to(cuda) if res else None
+    y_f32 = ops.conv2d(x.to(cuda), wt.to(cuda), bias.to(cuda), 1, 1, rd, True).cpu()
+    live = ref > 0
+    e = _rel_err(y[live], ref[live], scale[live])
+    ef32 = _rel_err(y_f32[live], ref[live], scale[live])
+    print(f"halo 2d {b}x{h}x{w}x{cin}->{cout}: max {e[0]:.3g} mean {e[1]:.3g} | f32 max {ef32[0]:.3g} "
+          f"mean {ef32[1]:.3g}")
+    assert e[0] <= 1.25 * max(ef32[0], 1e-7) and e[1] <= ef32[1] * 1.05 + 1e-9
+    assert ops.amax_value(rec[1]) == float(y.abs().max())
+    assert bool(torch.isfinite(y).all())

@@ -127,12 +127,13 @@ def test_handle_device_and_tuning_validation(cuda):
     assert L.rr_set_tuning(h, _lib.TUNE_CONV_IL, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_HALO_MF, 5) == _lib.RR_EINVAL  # (2-4: the N = 64 / 128 forms, round 6)
     assert L.rr_set_tuning(h, _lib.TUNE_SWEEP_FORM, 3) == _lib.RR_EINVAL
+    assert L.rr_set_tuning(h, _lib.TUNE_HALO_2D, 2) == _lib.RR_EINVAL
     assert L.rr_set_tuning(h, _lib.TUNE_S3_CFG_RES, 16) == _lib.RR_EINVAL
     for key in (_lib.TUNE_GEMM_CFG, _lib.TUNE_GEMM_BK, _lib.TUNE_LP_CFG, _lib.TUNE_S3_CFG, _lib.TUNE_SWEEP_MF16,
-                _lib.TUNE_SWEEP_IL, _lib.TUNE_CONV_IL, _lib.TUNE_HALO_MF, _lib.TUNE_S3_CFG_RES):
+                _lib.TUNE_SWEEP_IL, _lib.TUNE_CONV_IL, _lib.TUNE_HALO_MF, _lib.TUNE_S3_CFG_RES, _lib.TUNE_HALO_2D):
         assert L.rr_set_tuning(h, key, 0) == 0
     for key in (_lib.TUNE_S3_STAGGER, _lib.TUNE_SWEEP_MF16, _lib.TUNE_SWEEP_IL, _lib.TUNE_CONV_IL,
-                _lib.TUNE_HALO_MF):
+                _lib.TUNE_HALO_MF, _lib.TUNE_HALO_2D):
         assert L.rr_set_tuning(h, key, -1) == 0
     # a call made while another device is current still runs on the handle's device
     # (one-GPU box: the guard is exercised with the current device equal to the handle's)
