@@ -63,7 +63,8 @@ typedef struct rr_handle_s* rr_handle_t;
  * REMOVED: rr_bottleneck_seam_h2 (round 5's block seam, measured slower
  * than the two launches it fused) and the split-bf16 core's rr_conv2d_s3 /
  * rr_linear_s3 / rr_split3_bf16 (superseded by the f16x2 core in round 3);
- * the tuning key RR_TUNE_SWEEP_FORM (14) was added (round 6).
+ * the tuning keys RR_TUNE_SWEEP_FORM (14) and RR_TUNE_HALO_2D (15) were
+ * added (round 6).
  * Bindings compare rr_abi_version() with the RR_ABI_VERSION they were
  * written against.                                                          */
 #define RR_ABI_VERSION 6
