@@ -2602,15 +2602,27 @@ int launch_gemm_h2_seg2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int ti
 // measured slower: 2.20 vs 1.68 ms at 1280 images (one wave per SIMD leaves
 // nothing to cover the LDS latency; profiles/r06m_stem_4wave_ab.txt), so the
 // launch keeps NW = 8.
-template <int EPI, int NW = 8>
+// BREG: the weights in registers instead of LDS.  8 waves as 4 row groups of
+// 64 rows x 2 column groups of 32: a wave's B fragments for all 13 k-steps
+// (its 32 columns, both planes: 104 VGPRs) are loaded once per block, so the
+// k-loop reads only the patch from LDS, 4 KB of fragments per wave and k-step
+// instead of 6 KB for the same six MFMAs.  Same products and order per
+// accumulator: bit-identical.  BREG 1 spills (33 VGPRs; 16 even with the
+// pool items out of the k-loop).  BREG 2, the launch's form: only the high
+// plane in registers (52 VGPRs; it feeds two of the three products), the low
+// plane still read from LDS, 5 KB per wave and k-step; 256 VGPRs, no spill.
+// 1.759 -> 1.715 ms at 1280 images, bit-identical
+// (profiles/r06zd_stem_breg_ab.txt).
+template <int EPI, int NW = 8, int BREG = 0>
 __global__ __launch_bounds__(64 * NW, 1) void stem_pool_halo_kernel(GemmArgs g, int ntiles) {
   constexpr int NT = 64 * NW, BN = 64, HR = 39, HC = 35, HP = HR * HC;  // 1365 patch pixels
-  constexpr int WR = 256 / NW, FM = WR / 32;  // rows per wave, 32-row MFMA tiles per wave
-  static_assert(NW == 8 || NW == 4, "8 waves of 32 rows or 4 of 64");
+  constexpr int WR = BREG ? 64 : 256 / NW, FM = WR / 32;  // rows per wave, 32-row MFMA tiles per wave
+  constexpr int JN = BREG ? 1 : 2;                        // 32-column MFMA tiles per wave
+  static_assert(NW == 8 || (NW == 4 && !BREG), "8 waves of 32 rows or 4 of 64");
   constexpr int HS = 36, HPS = HR * HS;       // patch slots per row / in all (even | odd columns), zero slot HPS
   constexpr int KP = 224, BS = KP + 8;        // weight row (k) length; LDS row stride (u16, padded)
   constexpr int NKS = 13;                     // k-steps of 4 taps (taps 0..51)
-  constexpr int B_U16 = 2 * BN * BS;          // both weight planes
+  constexpr int B_U16 = BREG == 1 ? 0 : 2 * BN * BS;  // both weight planes
   constexpr int A_U16 = 2 * (HPS + 1) * 4;    // both patch planes + the zero slot
   constexpr int CS = BN + 4;                  // C staging row stride (floats)
   constexpr int C_U16 = 256 * CS * 2;
@@ -2627,6 +2639,7 @@ __global__ __launch_bounds__(64 * NW, 1) void stem_pool_halo_kernel(GemmArgs g, 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int lr = lane & 31, lh = lane >> 5;
+  const int wrg = BREG ? wave % 4 : wave, wn = BREG ? wave / 4 : 0;  // the wave's row / column group
   const uint32_t a_amax_w = amax_load_slot(g.a_amax);
   float a_sc, a_isc;
   {
@@ -2642,8 +2655,18 @@ __global__ __launch_bounds__(64 * NW, 1) void stem_pool_halo_kernel(GemmArgs g, 
     a_isc = __int_as_float((127 - e) << 23);
   }
 
-  // ---- both weight planes into LDS, once: [plane][n][k], rows padded ----
-  {
+  // ---- both weight planes into LDS, once: [plane][n][k], rows padded
+  // (BREG: the wave's own fragments into registers) ----
+  constexpr int BRP = BREG == 1 ? 2 : 1;  // weight planes in registers
+  frag_t breg[BREG ? NKS : 1][BRP];
+  if constexpr (BREG != 0) {
+    const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B) + (long long)(32 * wn + lr) * g.ldb + 8 * lh;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks)
+#pragma unroll
+      for (int p = 0; p < BRP; ++p) breg[ks][p] = *reinterpret_cast<const frag_t*>(Bp + p * g.b_plane + 16 * ks);
+  }
+  if constexpr (BREG != 1) {
     const uint16_t* Bp = reinterpret_cast<const uint16_t*>(g.B);
     for (int i = tid; i < 2 * BN * (KP / 8); i += NT) {
       const int row = i / (KP / 8), c8 = i - row * (KP / 8);  // row = plane * 64 + n
@@ -2693,7 +2716,7 @@ __global__ __launch_bounds__(64 * NW, 1) void stem_pool_halo_kernel(GemmArgs g, 
   int sbase[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int row = wave * WR + 32 * i + lr, rq = row / 15, rc = row - rq * 15;
+    const int row = wrg * WR + 32 * i + lr, rq = row / 15, rc = row - rq * 15;
     sbase[i] = row < 255 ? (2 * rq) * HS + rc : -1;
   }
 
@@ -2737,11 +2760,11 @@ __global__ __launch_bounds__(64 * NW, 1) void stem_pool_halo_kernel(GemmArgs g, 
   __syncthreads();
   for (; tl < ntiles; tl += G) {
     load_patch(tl + G);  // the next tile's patch lands under this tile's k-loop
-    f32x16 hi[FM][2], lo[FM][2];
+    f32x16 hi[FM][JN], lo[FM][JN];
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < JN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r) hi[i][j][r] = lo[i][j][r] = 0.f;
 #pragma unroll
@@ -2767,16 +2790,18 @@ __global__ __launch_bounds__(64 * NW, 1) void stem_pool_halo_kernel(GemmArgs g, 
 #pragma unroll
       for (int p = 0; p < 2; ++p)
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          b[p][j] = *reinterpret_cast<const frag_t*>(lb + (p * BN + 32 * j + lr) * BS + 16 * ks + 8 * lh);
+        for (int j = 0; j < JN; ++j)
+          b[p][j] = (BREG == 1 || (BREG == 2 && p == 0))
+                        ? breg[ks][BREG == 1 ? p : 0]
+                        : *reinterpret_cast<const frag_t*>(lb + (p * BN + 32 * (j + wn) + lr) * BS + 16 * ks + 8 * lh);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) hi[i][j] = s3_mf32<2>(a[0][i], b[0][j], hi[i][j]);
+        for (int j = 0; j < JN; ++j) hi[i][j] = s3_mf32<2>(a[0][i], b[0][j], hi[i][j]);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
+        for (int j = 0; j < JN; ++j) {
           lo[i][j] = s3_mf32<2>(a[0][i], b[1][j], lo[i][j]);
           lo[i][j] = s3_mf32<2>(a[1][i], b[0][j], lo[i][j]);
         }
@@ -2791,10 +2816,10 @@ __global__ __launch_bounds__(64 * NW, 1) void stem_pool_halo_kernel(GemmArgs g, 
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int j = 0; j < 2; ++j)
+      for (int j = 0; j < JN; ++j)
 #pragma unroll
         for (int r = 0; r < 16; ++r)
-          ct[(wave * WR + 32 * i + acc_row<false>(0, r, lane)) * CS + acc_col<false>(j, r, lane)] =
+          ct[(wrg * WR + 32 * i + acc_row<false>(0, r, lane)) * CS + 32 * wn + acc_col<false>(j, r, lane)] =
               hi[i][j][r] + lo[i][j][r];
     store_patch();
     prev = tl;
@@ -2828,7 +2853,7 @@ int launch_stem_pool_h2(rr_handle_s* h, const GemmArgs& g, hipStream_t s, int ti
     // the halo stem (7x7 / 2, pad 3; s3_cfg 7 forces the implicit-GEMM one)
     if (h->tune.s3_cfg != 7 && g.KH == 7 && g.KW == 7 && g.stride == 2 && g.pad == 3 && g.K == 224 && g.ldb == 224) {
       const int grid = (int)std::min<long long>(tiles, device_cu_count(h));
-      hipLaunchKernelGGL((stem_pool_halo_kernel<H2_EP | EP_RELU, 8>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles);
+      hipLaunchKernelGGL((stem_pool_halo_kernel<H2_EP | EP_RELU, 8, 2>), dim3((unsigned)grid), dim3(512), 0, s, g, (int)tiles);
       e = hipGetLastError();
     } else {
       e = launch_s3_t<8, 1, 1, 2, 16, A_CONV_C4, 4, 0, H2_EP | EP_RELU, 2, 2, 1>(q, s, device_cu_count(h), 0);
