@@ -2440,6 +2440,29 @@ static hipError_t launch_h2_am(const GemmArgs& g, hipStream_t s, int forced, int
   // forces the one-tile form); 64@56 3x3 1.212 -> 1.161 ms, bit-identical
   // (profiles/r05w_sweep.txt; the embed 68.26 / 68.22 ms, r05w_e2e.txt)
   const bool hpers = forced == 0;
+  // dense A past config 15's 32-bit byte offsets (A or C of 4 GB or more:
+  // C2's 1024-px gallery batches at layer 1, 6.4 GB at batch 128) ran config
+  // 7 / 11 instead: the GEMM now goes in row chunks that fit, each a config-15
+  // launch on offset pointers (chunks of 256-row multiples keep the one-launch
+  // tiling, so every row is the one launch's).  256->64 at 128 x 256 x 192:
+  // 1.738 -> 1.575 ms, 256->128 2.204 -> 2.136 (profiles/r06ze_dense4gb_ab.txt)
+  if constexpr (AM == A_DENSE) {
+    const bool q_shape = ((g.N % 256) == 0 && g.K >= 256) || (g.N == 128 && g.K >= 256) || (g.N == 64 && g.K >= 64);
+    if ((forced == 15 || forced == 0) && q_shape && !s3q_fits(g)) {
+      const long long per = ((1LL << 32) - 1) / (4LL * std::max(g.lda, g.ldc)) / 256 * 256;
+      if (per >= 256) {
+        for (long long m0 = 0; m0 < g.M; m0 += per) {
+          GemmArgs c = g;
+          c.M = (int)std::min<long long>(per, g.M - m0);
+          c.A = g.A + m0 * g.lda;
+          c.C = g.C + m0 * g.ldc;
+          if (g.residual != nullptr) c.residual = g.residual + m0 * g.ldc;
+          if (const hipError_t e = launch_h2_am<AM>(c, s, forced, n_cu, st)) return e;
+        }
+        return hipSuccess;
+      }
+    }
+  }
   // config 15 (config 12 as a persistent k-stream): the pick for dense A
   // with config 12's shape condition (forced 15: the same, every other GEMM
   // on the library's pick; forced 12 runs config 12).  Measured at 1280

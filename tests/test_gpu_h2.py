@@ -662,3 +662,28 @@ def test_conv2d_h2_halo_2d_wide(cuda, b, h, w, cin, cout, res):
     assert e[0] <= 1.25 * max(ef32[0], 1e-7) and e[1] <= ef32[1] * 1.05 + 1e-9
     assert ops.amax_value(rec[1]) == float(y.abs().max())
     assert bool(torch.isfinite(y).all())
+
+
+def test_conv2d_h2_dense_past_4gb_row_chunks(cuda):
+    """A dense 1x1 conv whose input passes 4 GB (config 15's 32-bit byte
+    offsets; C2's layer-1 batches) runs as row chunks of config-15 launches:
+    every output row equals, bit for bit, the same rows from a launch on its
+    image alone with the same input split scale, across the chunk boundary
+    (image 7 straddles it), and the max-|y| record is the whole output's."""
+    b, h, w, cin = 8, 725, 725, 256   # 4.3 GB of fp32 input
+    g = torch.Generator(device=cuda).manual_seed(5)
+    x = torch.relu(torch.randn(b, h, w, cin, device=cuda, generator=g))
+    rin = ops.amax_records(1, cuda)[0]
+    ops.amax_f32(x, rin)
+    for cout in (64, 256):
+        wc = ops.H2Conv(torch.randn(cout, 1, 1, cin, device=cuda, generator=g) * (2.0 / cin) ** 0.5)
+        bias = torch.randn(cout, device=cuda, generator=g) * 0.1
+        rout = ops.amax_records(1, cuda)[0]
+        y = ops.conv2d_h2(x, rin, wc, bias, 1, 0, None, True, rout)
+        for i in (0, 7):
+            ri = ops.amax_records(1, cuda)[0]
+            yi = ops.conv2d_h2(x[i:i + 1], rin, wc, bias, 1, 0, None, True, ri)
+            assert torch.equal(y[i:i + 1], yi), (cout, i)
+        assert ops.amax_value(rout) == float(y.abs().max())
+        del y
+    torch.cuda.empty_cache()
